@@ -1,0 +1,178 @@
+#!/usr/bin/env python3
+"""Benchmark: constraint-candidate evaluations/sec on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[2]): synthetic random 256-bit
+BitVec constraint DAGs (depth 32, MUL/DIV/EXP-heavy mix), 65,536 generated candidates each.
+A *step* is one batch of `--sets` DAGs searched over the full candidate budget on one GPU
+("full sweep": early exit off, every candidate evaluates the whole program — the unit of
+work is one complete set-evaluation per candidate).  Inputs (bytecode) are uploaded to HBM
+before the timed region; candidates are generated on device.
+
+Multi-GPU: one process per GPU (torch.distributed.run); every rank searches its own DAG ids
+(weak scaling, no data-path collective); the verdict bitmaps are all-gathered once after the
+timed region (RCCL), which is the only collective the path has.
+
+Prints one JSON line (rank 0) with roofline (integer VALU) and cpu_baseline objects.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# gfx950 integer VALU peak: 256 CUs x 4 SIMD-32 x 32 lanes x 2.4 GHz (MI355X_MICROARCH.md:
+# FP32 vector 157.3 TFLOPS = 78.6 T lane-ops/s counting an FMA as one op)
+INT32_PEAK_OPS = 256 * 4 * 32 * 2.4e9
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--sets", type=int, default=1024, help="DAGs per step per GPU")
+    ap.add_argument("--budget", type=int, default=65536, help="candidates per DAG")
+    ap.add_argument("--mode", choices=["full", "early"], default="full")
+    ap.add_argument("--seed", type=int, default=0x5EED)
+    ap.add_argument("--cpu-sample-s", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(programs, budget, seed, target_s):
+    """Oracle on the host cores (rank 0, N=1 only): the C restatement if built, else Python."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    try:
+        import coracle_py  # C restatement via ctypes (oracle/Makefile)
+
+        return coracle_py.baseline(programs, budget, seed, target_s)
+    except Exception as e:  # pragma: no cover - informative fallback for the baseline only
+        err = str(e)
+    import pyoracle as O
+    from mythril_amd import ir
+
+    b = ir.Batch(programs)
+    t0 = time.perf_counter()
+    evals = 0
+    s = 0
+    while time.perf_counter() - t0 < target_s and s < len(programs):
+        sv = O.SetView.from_batch(b, s)
+        n = 64
+        assigns = sv.gen_assignments(np.arange(n, dtype=np.uint64), seed)
+        for a in assigns:
+            sv.evaluate(a)
+        evals += n
+        s += 1
+    dt = time.perf_counter() - t0
+    return {"value": evals / dt, "unit": "evals/s", "cores": 1, "kind": "port",
+            "sample": f"python oracle, {s} sets x 64 candidates ({err[:60]})"}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", str(args.gpus)))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist_mod
+
+        dist = dist_mod
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from mythril_amd import ir, synth
+    from mythril_amd.engine import Engine
+
+    eng = Engine(local)
+    flags = ir.FLAG_COUNT_OPS | (ir.FLAG_EARLY_EXIT | ir.FLAG_SHORTCIRCUIT if args.mode == "early" else 0)
+    n_steps = args.warmup + args.steps
+    batches, step_progs = [], []
+    t_gen = time.perf_counter()
+    for k in range(n_steps):
+        first = (k * world + rank) * args.sets
+        progs = [synth.random_dag_set(first + i, plant=False)[0] for i in range(args.sets)]
+        step_progs.append(progs)
+        batches.append(eng.upload(progs))
+    t_gen = time.perf_counter() - t_gen
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    for k in range(args.warmup):
+        eng.check(batches[k], budget=args.budget, seed=args.seed, flags=flags)
+    barrier()
+    t0 = time.perf_counter()
+    evals = ops = 0
+    kms = []
+    founds = []
+    for k in range(args.warmup, n_steps):
+        r = eng.check(batches[k], budget=args.budget, seed=args.seed, flags=flags)
+        evals += r.evals_full if args.mode == "full" else r.cands_decided
+        ops += r.ops
+        kms.append(r.kernel_ms)
+        founds.append(r.found)
+    barrier()
+    dt = time.perf_counter() - t0
+
+    tot_evals, max_dt = float(evals), dt
+    if dist is not None:
+        t = torch.tensor([float(evals), dt], dtype=torch.float64, device="cuda")
+        ev = t[:1].clone()
+        dist.all_reduce(ev, op=dist.ReduceOp.SUM)
+        mx = t[1:].clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        tot_evals, max_dt = float(ev.item()), float(mx.item())
+        # the path's one collective: all-gather the per-set SAT verdicts
+        sat = torch.from_numpy(np.concatenate(founds).astype(np.int64)).to("cuda")
+        gathered = [torch.empty_like(sat) for _ in range(world)]
+        dist.all_gather(gathered, sat)
+
+    if rank == 0:
+        kernel_s = sum(kms) / 1e3
+        achieved = ops / kernel_s if kernel_s > 0 else 0.0
+        line = {
+            "metric": "constraint-candidate evals/sec",
+            "value": tot_evals / max_dt,
+            "unit": "evals/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * max_dt / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32 (256-bit as 8x32-bit limbs)",
+            "data": "synthetic (config-3 random DAGs, on-device Philox candidates)",
+            "config": {"workload": "synthetic-dags-depth32-muldivexp",
+                       "sets_per_step_per_gpu": args.sets, "candidates_per_set": args.budget,
+                       "mode": args.mode, "parallelism": f"sets sharded over {world} GPU(s)"},
+            "roofline": {"bound": "valu", "achieved": achieved / 1e12,
+                         "peak": INT32_PEAK_OPS / 1e12, "unit": "Tops/s (int32)",
+                         "frac": achieved / INT32_PEAK_OPS, "traffic": None,
+                         "kernel": "pf_check_kernel", "kernel_ms_avg": float(np.mean(kms))},
+            "node_evals_note": "ops counted with the SURVEY.md §8(d) per-op int32 table",
+            "gen_upload_s": t_gen,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(step_progs[args.warmup], args.budget, args.seed,
+                                                args.cpu_sample_s)
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

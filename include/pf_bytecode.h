@@ -1,0 +1,133 @@
+/*
+ * pf_bytecode.h — the flat register bytecode that carries one Mythril path-constraint
+ * set (a conjunction of 256-bit BitVec/Bool DAGs) across the C ABI into the gfx950
+ * evaluator.  This header is the single source of truth for opcode numbers, the
+ * instruction layout, the variable schema and the candidate-generator contract; the
+ * Python host (mythril_amd/ir.py) mirrors it and tests/test_abi.py checks the mirror.
+ *
+ * Semantics of every opcode are SMT-LIB2 FixedSizeBitVectors (z3's total-division
+ * conventions), i.e. what z3's model.eval(expr, model_completion=True) computes for the
+ * term shapes built by mythril/laser/smt/{bitvec,bitvec_helper,bool}.py.  The CPU
+ * restatement that pins them is oracle/pyoracle.py.
+ *
+ * Instruction = 4 x uint32:
+ *   w0 = op | (width << 8) | (flags << 18)      width = result width (W ops) or the
+ *                                               operand width (compare ops), 1..256
+ *   w1 = dst | (a << 8) | (b << 16) | (c << 24) register indices
+ *   w2 = aux0, w3 = aux1                        op specific
+ *
+ * Register classes
+ *   W : 256-bit values, PF_NW registers.  A value of width w < 256 is kept
+ *       zero-extended (bits >= w are 0) — every op re-masks its result.
+ *   B : booleans, PF_NB registers (0/1 per candidate).
+ * The conjunction root is an accumulator: PF_ASSERT ands a B register into it.
+ */
+#ifndef PF_BYTECODE_H
+#define PF_BYTECODE_H
+
+#include <stdint.h>
+
+#define PF_NW 15          /* usable wide registers (limb-sliced VGPR banks on gfx950) */
+#define PF_W_SINK 15      /* 16th bank slot: write sink of ops without a W result     */
+#define PF_NB 32          /* bool registers                                          */
+#define PF_LIMBS 8        /* 8 x 32-bit limbs = 256 bits, little-endian limb order   */
+#define PF_MAX_WIDTH 256
+
+/* ---- opcodes ------------------------------------------------------------------ */
+enum pf_opcode {
+    PF_END = 0,
+    /* W results */
+    PF_W_CONST = 1,   /* dst <- const[aux0]                                            */
+    PF_W_VAR = 2,     /* dst <- candidate value of variable aux0                       */
+    PF_W_MOV = 3,     /* dst <- a masked to width (zero_extend / no-op copy)           */
+    PF_W_ADD = 4,     /* bvadd                                                         */
+    PF_W_SUB = 5,     /* bvsub                                                         */
+    PF_W_MUL = 6,     /* bvmul                                                         */
+    PF_W_UDIV = 7,    /* bvudiv   (x / 0 = 2^w - 1)                                    */
+    PF_W_UREM = 8,    /* bvurem   (x % 0 = x)                                          */
+    PF_W_SDIV = 9,    /* bvsdiv   (x / 0 = x <s 0 ? 1 : 2^w - 1)                       */
+    PF_W_SREM = 10,   /* bvsrem   (sign of dividend; x % 0 = x)                        */
+    PF_W_SMOD = 11,   /* bvsmod   (sign of divisor;  x mod 0 = x)                      */
+    PF_W_AND = 12,
+    PF_W_OR = 13,
+    PF_W_XOR = 14,
+    PF_W_NOT = 15,    /* bvnot a                                                       */
+    PF_W_NEG = 16,    /* bvneg a                                                       */
+    PF_W_SHL = 17,    /* bvshl  (b >= w -> 0)                                          */
+    PF_W_LSHR = 18,   /* bvlshr (b >= w -> 0)                                          */
+    PF_W_ASHR = 19,   /* bvashr (b >= w -> sign fill)                                  */
+    PF_W_EXP = 20,    /* a ** b mod 2^w (EVM EXP; 256-step square-and-multiply)        */
+    PF_W_EXTRACT = 21,/* dst <- (a >> aux0) masked to width  ((_ extract hi lo), width = hi-lo+1) */
+    PF_W_CONCAT = 22, /* dst <- (a << aux0) | b   where aux0 = width(b)               */
+    PF_W_SEXT = 23,   /* dst <- sign_extend(a) from aux0 bits to width                 */
+    PF_W_ITE = 24,    /* dst <- B[c] ? a : b                                           */
+    /* B results */
+    PF_B_CONST = 40,  /* dst <- aux0 & 1                                               */
+    PF_B_VAR = 41,    /* dst <- candidate value of Bool variable aux0                  */
+    PF_B_EQ = 42,     /* W a == W b                                                    */
+    PF_B_ULT = 43,
+    PF_B_ULE = 44,
+    PF_B_SLT = 45,    /* signed at width w                                             */
+    PF_B_SLE = 46,
+    PF_B_AND = 47,    /* B a & B b                                                     */
+    PF_B_OR = 48,
+    PF_B_XOR = 49,
+    PF_B_NOT = 50,
+    PF_B_ITE = 51,    /* B[c] ? B a : B b                                              */
+    PF_B_UADD_NOOVF = 52, /* a + b < 2^w   (z3 BVAddNoOverflow(a, b, False))          */
+    PF_B_UMUL_NOOVF = 53, /* a * b < 2^w   (z3 BVMulNoOverflow(a, b, False), bvumul_noovfl) */
+    PF_ASSERT = 60,   /* root &= B a; with PF_FLAG_SHORTCIRCUIT a wave whose lanes are all
+                         false stops evaluating the set here                           */
+    PF_NUM_OPCODES = 64
+};
+
+/* ---- variable schema (4 x uint32 per variable) -------------------------------- */
+/* s0 = kind | (width << 8); s1 = hint0; s2 = hint1; s3 = parent slot (or PF_NO_PARENT) */
+enum pf_var_kind {
+    PF_VK_GENERIC = 0, /* plain BitVec symbol                                          */
+    PF_VK_ACTOR = 1,   /* sender_*: const[hint0 .. hint0+hint1) are the actor addresses */
+    PF_VK_KECCAK = 2,  /* keccak UF output slot: const[hint0] + 64*k, k < 2^117         */
+    PF_VK_SMALL = 3,   /* sizes: uniform in [0, hint0]                                  */
+    PF_VK_BOOL = 4     /* free Bool symbol                                              */
+};
+#define PF_NO_PARENT 0xffffffffu
+
+/* ---- per-set descriptor (8 x uint32) ------------------------------------------- */
+typedef struct pf_set_desc {
+    uint32_t code_off;   /* first instruction (in 16-byte instructions)               */
+    uint32_t n_ins;      /* instructions including the final PF_END                   */
+    uint32_t const_off;  /* first constant (in 32-byte constants)                     */
+    uint32_t n_const;
+    uint32_t var_off;    /* first schema entry                                        */
+    uint32_t n_vars;
+    uint32_t seed;       /* per-set candidate seed (independent of batch position)    */
+    uint32_t parent_off; /* first parent value (32-byte each) or PF_NO_PARENT          */
+} pf_set_desc;
+
+/* ---- candidate generator contract ---------------------------------------------- */
+/* Candidate c of a set with seed S and global seed G assigns variable v the value
+ * produced from three Philox4x32-10 blocks with key (G_lo ^ S, G_hi) and counters
+ * (c, v, 0, 0), (c, v, 1, 0), (c, v, 2, 0): r[0..7] (value bits) and m[0..3]
+ * (strategy bits).  Strategies (m[0] & 15) for PF_VK_GENERIC, width w:
+ *    0..4  uniform r masked to w
+ *    5..8  boundary table[m[1] % 12] with k = m[2] % w:
+ *          {0, 1, 2, 3, 2^w-1, 2^w-2, 2^(w-1), 2^(w-1)-1, 2^k, 2^k-1, 2^k+1, 2^160-1}
+ *    9..11 harvested constant const[m[1] % n_const] + {0,+1,-1}[m[2] % 3]  (uniform if n_const == 0)
+ *    12,13 parent value (bit m[2] % w flipped when (m[1] & 3) == 0), else r[0] & 0xff
+ *    14,15 small: r[0] & (2^(1 + m[1] % 16) - 1)
+ * Candidate 0 is the exact parent value for every variable that has one.
+ * PF_VK_ACTOR: m[1] % 4 < hint1 -> const[hint0 + m[1] % 4], else generic.
+ * PF_VK_KECCAK: const[hint0] + ((r[0..3] & (2^117 - 1)) << 6).
+ * PF_VK_SMALL: r[0] % (hint0 + 1).   PF_VK_BOOL: r[0] & 1.
+ * All results are masked to the variable's width.                                  */
+#define PF_PHILOX_M0 0xD2511F53u
+#define PF_PHILOX_M1 0xCD9E8D57u
+#define PF_PHILOX_W0 0x9E3779B9u
+#define PF_PHILOX_W1 0xBB67AE85u
+
+/* flags for pf_check_batch */
+#define PF_FLAG_SHORTCIRCUIT 1u  /* stop a wave's set evaluation once all its lanes are false */
+#define PF_FLAG_EARLY_EXIT 2u    /* stop a set once any candidate satisfies it             */
+#define PF_FLAG_COUNT_OPS 4u     /* accumulate algorithmic int32-op counts                  */
+
+#endif /* PF_BYTECODE_H */

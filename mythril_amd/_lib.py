@@ -1,0 +1,137 @@
+"""ctypes binding of libpathfeas.so (include/pathfeas.h).
+
+The library is built in-tree by ``mythril_amd.build.build_library()`` (or
+``__graft_entry__.build()``).  There is no CPU fallback: if the shared object or a GPU is
+missing, every call raises :class:`PathFeasError` — the product path never silently
+answers on the host.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Optional
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libpathfeas.so")
+
+
+class PathFeasError(RuntimeError):
+    pass
+
+
+class pf_stats(ctypes.Structure):
+    _fields_ = [
+        ("evals_full", ctypes.c_uint64),
+        ("cands_decided", ctypes.c_uint64),
+        ("ops", ctypes.c_uint64),
+        ("n_sat", ctypes.c_uint64),
+        ("kernel_ms", ctypes.c_float),
+        ("pad_", ctypes.c_float),
+    ]
+
+
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_sz = ctypes.c_size_t
+
+# name -> (restype, argtypes); kept in sync with include/pathfeas.h (tests/test_abi.py)
+SIGNATURES = {
+    "pf_init": (ctypes.c_int, [ctypes.c_int]),
+    "pf_shutdown": (ctypes.c_int, []),
+    "pf_last_error": (ctypes.c_char_p, []),
+    "pf_version": (ctypes.c_int, []),
+    "pf_device_count": (ctypes.c_int, []),
+    "pf_batch_create": (ctypes.c_int, [_u32p, _sz, _u32p, _sz, _u32p, _sz, _u32p, _sz, _u32p,
+                                       _sz, _u64p]),
+    "pf_batch_free": (ctypes.c_int, [ctypes.c_uint64]),
+    "pf_check_batch": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                                      ctypes.c_uint32, ctypes.c_uint32, _u32p, _u8p,
+                                      ctypes.POINTER(pf_stats)]),
+    "pf_check_batch_dev": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                                          ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
+                                          ctypes.POINTER(pf_stats), ctypes.c_void_p]),
+    "pf_materialize": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint64, _u32p, _u32p, _sz,
+                                      _u32p]),
+    "pf_eval_assignments": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32, _u32p,
+                                           ctypes.c_uint32, _u8p]),
+    "pf_eval_assignments_dev": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p,
+                                               ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
+    "pf_keccak256_batch": (ctypes.c_int, [_u8p, _u64p, _sz, _u8p]),
+    "pf_keccak256_fixed_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, _sz,
+                                              ctypes.c_void_p, ctypes.POINTER(ctypes.c_float),
+                                              ctypes.c_void_p]),
+}
+
+_lib = None
+_lib_lock = threading.Lock()
+_initialised_device: Optional[int] = None
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libpathfeas.so and bind every C-ABI symbol (no device work)."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        # One HIP runtime per process: torch ships its own libamdhip64.so.7 /
+        # libhsa-runtime64.so.1 (same SONAMEs as /opt/rocm's).  Importing torch first makes
+        # the dynamic loader bind this library to the already-loaded copies, so torch
+        # (device memory, streams, RCCL) and the engine share one runtime and one device
+        # context.  Loading ours first would map a second runtime and torch's device init
+        # then fails ("No HIP GPUs are available").
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+        if not os.path.exists(path):
+            raise PathFeasError(
+                f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+        lib = ctypes.CDLL(path)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+def lib() -> ctypes.CDLL:
+    return load_library()
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().pf_last_error().decode(errors="replace")
+        raise PathFeasError(f"{what} failed ({rc}): {msg}")
+
+
+def init(device: int = 0) -> None:
+    """Select the GPU for this process (one process per GPU)."""
+    global _initialised_device
+    L = lib()
+    if _initialised_device == device:
+        return
+    if L.pf_device_count() <= 0:
+        raise PathFeasError("no HIP device visible: the MI355X path-feasibility engine has no CPU fallback")
+    check(L.pf_init(device), f"pf_init({device})")
+    _initialised_device = device
+
+
+def ptr_u32(a: np.ndarray):
+    assert a.dtype == np.uint32 and a.flags.c_contiguous
+    return a.ctypes.data_as(_u32p)
+
+
+def ptr_u8(a: np.ndarray):
+    assert a.dtype == np.uint8 and a.flags.c_contiguous
+    return a.ctypes.data_as(_u8p)
+
+
+def ptr_u64(a: np.ndarray):
+    assert a.dtype == np.uint64 and a.flags.c_contiguous
+    return a.ctypes.data_as(_u64p)

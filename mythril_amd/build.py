@@ -1,0 +1,39 @@
+"""Build libpathfeas.so in-tree for gfx950 (hipcc cross-compiles without a GPU)."""
+
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+OUT = os.path.join(HERE, "libpathfeas.so")
+SOURCES = ["pathfeas.hip", "pf_eval.hip", "pf_keccak.hip", "u256.h",
+           os.path.join("..", "..", "include", "pathfeas.h"),
+           os.path.join("..", "..", "include", "pf_bytecode.h")]
+
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-value"]
+
+
+def _stale() -> bool:
+    if not os.path.exists(OUT):
+        return True
+    t = os.path.getmtime(OUT)
+    return any(os.path.getmtime(os.path.join(CSRC, s)) > t for s in SOURCES)
+
+
+def build_library(force: bool = False, verbose: bool = False) -> str:
+    if not force and not _stale():
+        return OUT
+    cmd = [HIPCC, *FLAGS, "-o", OUT + ".tmp", os.path.join(CSRC, "pathfeas.hip")]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True, cwd=CSRC)
+    os.replace(OUT + ".tmp", OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build_library(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,424 @@
+// pathfeas.hip — host side of libpathfeas.so: the C ABI declared in include/pathfeas.h.
+//
+// Single translation unit: the kernels (pf_eval.hip, pf_keccak.hip) are included so the
+// launches need no relocatable device code.  All entry points serialise on one mutex and
+// re-select the device, because Mythril's query funnel calls in from a new worker thread
+// per query (mythril/support/model.py:99-117).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/pathfeas.h"
+#include "pf_eval.hip"
+#include "pf_keccak.hip"
+
+namespace {
+
+std::mutex g_mu;
+thread_local std::string g_err_tls;
+std::string g_err;
+int g_device = -1;
+hipStream_t g_stream = nullptr;
+hipEvent_t g_ev0 = nullptr, g_ev1 = nullptr;
+uint32_t* g_scratch_u32 = nullptr;  // small device scratch (counters, t0)
+int g_num_cus = 256;
+
+int fail(const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return -1;
+}
+
+#define HIPCHK(x)                                                                       \
+    do {                                                                                \
+        hipError_t e_ = (x);                                                            \
+        if (e_ != hipSuccess) return fail("%s failed: %s (%s:%d)", #x, hipGetErrorString(e_), \
+                                          __FILE__, __LINE__);                          \
+    } while (0)
+
+struct Batch {
+    int device;
+    size_t n_ins, n_const, n_vars, n_parents, n_sets;
+    uint32_t max_vars;
+    std::vector<pf_set_desc> h_descs;
+    pf_set_desc* d_descs = nullptr;
+    uint4* d_code = nullptr;
+    uint32_t* d_consts = nullptr;
+    uint4* d_schema = nullptr;
+    uint32_t* d_parents = nullptr;
+    uint32_t* d_found = nullptr;
+};
+
+int ensure_init_locked() {
+    if (g_device < 0) return fail("pf_init() has not been called");
+    HIPCHK(hipSetDevice(g_device));
+    return 0;
+}
+
+template <typename T>
+int upload(T** dst, const void* src, size_t bytes) {
+    size_t alloc = bytes ? bytes : 16;
+    HIPCHK(hipMalloc((void**)dst, alloc));
+    HIPCHK(hipMemset(*dst, 0, alloc));
+    if (bytes && src) HIPCHK(hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice));
+    return 0;
+}
+
+Batch* as_batch(uint64_t h) { return reinterpret_cast<Batch*>(static_cast<uintptr_t>(h)); }
+
+hipStream_t pick_stream(void* s) { return s ? reinterpret_cast<hipStream_t>(s) : g_stream; }
+
+// launch geometry for the search kernel: enough waves to fill 256 CUs several times over,
+// each wave walking >= 64 candidates of one set.
+void geometry(uint32_t n_sets, uint32_t budget, uint32_t* per_wave, uint32_t* slices) {
+    const uint64_t target_waves = (uint64_t)g_num_cus * 8u * 8u;
+    uint64_t groups = (budget + 63u) / 64u;  // 64-candidate groups per set
+    uint64_t sl = (target_waves + n_sets - 1) / std::max<uint32_t>(n_sets, 1u);
+    sl = std::max<uint64_t>(1, std::min<uint64_t>(sl, groups));
+    uint64_t gpw = (groups + sl - 1) / sl;  // groups per wave
+    *per_wave = (uint32_t)(gpw * 64u);
+    *slices = (uint32_t)((budget + *per_wave - 1) / *per_wave);
+    if (*slices == 0) *slices = 1;
+}
+
+int check_launch(Batch* B, uint64_t gseed, uint32_t budget, uint32_t flags, uint32_t timeout_ms,
+                 uint32_t* d_found, pf_stats* stats, hipStream_t st) {
+    unsigned long long* d_counters = reinterpret_cast<unsigned long long*>(g_scratch_u32);
+    uint64_t* d_t0 = reinterpret_cast<uint64_t*>(g_scratch_u32 + 8);
+    HIPCHK(hipMemsetAsync(g_scratch_u32, 0, 64, st));
+    HIPCHK(hipMemsetAsync(d_found, 0xff, B->n_sets * sizeof(uint32_t), st));
+    if (B->n_sets == 0 || budget == 0) {
+        if (stats) memset(stats, 0, sizeof(*stats));
+        return 0;
+    }
+    uint32_t per_wave, slices;
+    geometry((uint32_t)B->n_sets, budget, &per_wave, &slices);
+    const uint64_t waves = (uint64_t)B->n_sets * slices;
+    if (waves > 0xffffffffull) return fail("batch too large: %llu waves", (unsigned long long)waves);
+    const uint32_t blocks = (uint32_t)((waves + 3) / 4);
+    const uint64_t deadline = timeout_ms ? (uint64_t)timeout_ms * 100000ull : 0ull;  // 100 MHz
+    HIPCHK(hipEventRecord(g_ev0, st));
+    hipLaunchKernelGGL(pf_check_kernel, dim3(blocks), dim3(256), 0, st, B->d_descs,
+                       (uint32_t)B->n_sets, B->d_code, B->d_consts, B->d_schema, B->d_parents,
+                       gseed, budget, per_wave, slices, flags, deadline, d_t0, d_found, d_counters);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(g_ev1, st));
+    if (stats) {
+        unsigned long long h[3];
+        HIPCHK(hipMemcpyAsync(h, d_counters, sizeof(h), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, g_ev0, g_ev1));
+        stats->evals_full = h[0];
+        stats->cands_decided = h[1];
+        stats->ops = h[2];
+        stats->kernel_ms = ms;
+        stats->n_sat = 0;
+    }
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pf_version(void) { return 1; }
+
+const char* pf_last_error(void) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_err_tls = g_err;
+    return g_err_tls.c_str();
+}
+
+int pf_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int pf_init(int device) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    int n = 0;
+    HIPCHK(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n) return fail("pf_init: device %d out of range (%d devices)", device, n);
+    if (g_device == device) return 0;
+    if (g_device >= 0) return fail("pf_init: already initialised on device %d", g_device);
+    HIPCHK(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, device));
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail("pf_init: device %d is %s, this build targets gfx950", device, prop.gcnArchName);
+    g_num_cus = prop.multiProcessorCount;
+    HIPCHK(hipStreamCreateWithFlags(&g_stream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreate(&g_ev0));
+    HIPCHK(hipEventCreate(&g_ev1));
+    HIPCHK(hipMalloc((void**)&g_scratch_u32, 256));
+    g_device = device;
+    return 0;
+}
+
+int pf_shutdown(void) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_device < 0) return 0;
+    hipSetDevice(g_device);
+    hipStreamSynchronize(g_stream);
+    hipFree(g_scratch_u32);
+    hipEventDestroy(g_ev0);
+    hipEventDestroy(g_ev1);
+    hipStreamDestroy(g_stream);
+    g_scratch_u32 = nullptr;
+    g_stream = nullptr;
+    g_device = -1;
+    return 0;
+}
+
+int pf_batch_create(const uint32_t* code, size_t n_ins, const uint32_t* consts, size_t n_const,
+                    const uint32_t* schema, size_t n_vars, const uint32_t* parents,
+                    size_t n_parents, const pf_set_desc* descs, size_t n_sets,
+                    uint64_t* handle_out) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (ensure_init_locked()) return -1;
+    if (!handle_out) return fail("pf_batch_create: null handle_out");
+    // host-side shape checks: every kernel index is derived from these
+    uint32_t max_vars = 0;
+    for (size_t s = 0; s < n_sets; s++) {
+        const pf_set_desc& d = descs[s];
+        if ((uint64_t)d.code_off + d.n_ins > n_ins || d.n_ins == 0)
+            return fail("set %zu: code range [%u,+%u) outside %zu instructions", s, d.code_off, d.n_ins, n_ins);
+        if ((uint64_t)d.const_off + d.n_const > n_const)
+            return fail("set %zu: constant range outside pool", s);
+        if ((uint64_t)d.var_off + d.n_vars > n_vars) return fail("set %zu: schema range outside", s);
+        if ((code[4 * ((size_t)d.code_off + d.n_ins - 1)] & 0xffu) != PF_END)
+            return fail("set %zu: program does not end with PF_END", s);
+        for (uint32_t i = 0; i < d.n_ins; i++) {
+            const uint32_t* I = code + 4 * ((size_t)d.code_off + i);
+            uint32_t op = I[0] & 0xffu, w = (I[0] >> 8) & 0x3ffu;
+            if (op != PF_END && (w == 0 || w > PF_MAX_WIDTH))
+                return fail("set %zu ins %u: width %u out of range", s, i, w);
+            if ((op == PF_W_VAR || op == PF_B_VAR) && I[2] >= d.n_vars)
+                return fail("set %zu ins %u: variable %u >= %u", s, i, I[2], d.n_vars);
+            if (op == PF_W_CONST && I[2] >= d.n_const)
+                return fail("set %zu ins %u: constant %u >= %u", s, i, I[2], d.n_const);
+        }
+        for (uint32_t v = 0; v < d.n_vars; v++) {
+            const uint32_t* sc = schema + 4 * ((size_t)d.var_off + v);
+            uint32_t kind = sc[0] & 0xffu, w = (sc[0] >> 8) & 0x3ffu;
+            if (w == 0 || w > PF_MAX_WIDTH) return fail("set %zu var %u: width %u", s, v, w);
+            if (sc[3] != PF_NO_PARENT && sc[3] >= n_parents) return fail("set %zu var %u: parent slot", s, v);
+            if (kind == PF_VK_KECCAK && sc[1] >= d.n_const) return fail("set %zu var %u: keccak base", s, v);
+            if (kind == PF_VK_ACTOR && (sc[2] > 4 || sc[1] + sc[2] > d.n_const))
+                return fail("set %zu var %u: actor table", s, v);
+        }
+        max_vars = std::max(max_vars, d.n_vars);
+    }
+    Batch* B = new Batch();
+    B->device = g_device;
+    B->n_ins = n_ins;
+    B->n_const = n_const;
+    B->n_vars = n_vars;
+    B->n_parents = n_parents;
+    B->n_sets = n_sets;
+    B->max_vars = max_vars;
+    B->h_descs.assign(descs, descs + n_sets);
+    int rc = 0;
+    rc |= upload(&B->d_code, code, n_ins * 16);
+    rc |= upload(&B->d_consts, consts, n_const * 32);
+    rc |= upload(&B->d_schema, schema, n_vars * 16);
+    rc |= upload(&B->d_parents, parents, n_parents * 32);
+    rc |= upload(&B->d_descs, descs, n_sets * sizeof(pf_set_desc));
+    rc |= upload(&B->d_found, nullptr, n_sets * 4);
+    if (rc) {
+        delete B;
+        return -1;
+    }
+    *handle_out = (uint64_t)(uintptr_t)B;
+    return 0;
+}
+
+int pf_batch_free(uint64_t handle) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    Batch* B = as_batch(handle);
+    if (!B) return 0;
+    hipSetDevice(B->device);
+    hipStreamSynchronize(g_stream);
+    hipFree(B->d_code);
+    hipFree(B->d_consts);
+    hipFree(B->d_schema);
+    hipFree(B->d_parents);
+    hipFree(B->d_descs);
+    hipFree(B->d_found);
+    delete B;
+    return 0;
+}
+
+int pf_check_batch(uint64_t handle, uint64_t global_seed, uint32_t budget, uint32_t flags,
+                   uint32_t timeout_ms, uint32_t* found_out, uint8_t* sat_bitmap_out,
+                   pf_stats* stats) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (ensure_init_locked()) return -1;
+    Batch* B = as_batch(handle);
+    if (!B) return fail("pf_check_batch: null batch");
+    pf_stats local;
+    pf_stats* st = stats ? stats : &local;
+    if (check_launch(B, global_seed, budget, flags, timeout_ms, B->d_found, st, g_stream)) return -1;
+    std::vector<uint32_t> found(B->n_sets);
+    if (B->n_sets)
+        HIPCHK(hipMemcpyAsync(found.data(), B->d_found, B->n_sets * 4, hipMemcpyDeviceToHost, g_stream));
+    HIPCHK(hipStreamSynchronize(g_stream));
+    uint64_t nsat = 0;
+    if (sat_bitmap_out) memset(sat_bitmap_out, 0, (B->n_sets + 7) / 8);
+    for (size_t s = 0; s < B->n_sets; s++) {
+        if (found_out) found_out[s] = found[s];
+        if (found[s] != 0xffffffffu) {
+            nsat++;
+            if (sat_bitmap_out) sat_bitmap_out[s / 8] |= (uint8_t)(1u << (s % 8));
+        }
+    }
+    st->n_sat = nsat;
+    return 0;
+}
+
+int pf_check_batch_dev(uint64_t handle, uint64_t global_seed, uint32_t budget, uint32_t flags,
+                       uint32_t timeout_ms, uint32_t* d_found, pf_stats* stats, void* stream) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (ensure_init_locked()) return -1;
+    Batch* B = as_batch(handle);
+    if (!B) return fail("pf_check_batch_dev: null batch");
+    if (!d_found) return fail("pf_check_batch_dev: null d_found");
+    return check_launch(B, global_seed, budget, flags, timeout_ms, d_found, stats, pick_stream(stream));
+}
+
+int pf_materialize(uint64_t handle, uint64_t global_seed, const uint32_t* set_ids,
+                   const uint32_t* cand_ids, size_t n, uint32_t* values_out) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (ensure_init_locked()) return -1;
+    Batch* B = as_batch(handle);
+    if (!B) return fail("pf_materialize: null batch");
+    if (n == 0) return 0;
+    std::vector<uint32_t> off(n);
+    uint64_t total = 0;
+    for (size_t i = 0; i < n; i++) {
+        if (set_ids[i] >= B->n_sets) return fail("pf_materialize: set %u out of range", set_ids[i]);
+        off[i] = (uint32_t)total;
+        total += B->h_descs[set_ids[i]].n_vars;
+    }
+    if (total == 0) return 0;
+    uint32_t *d_sets, *d_cands, *d_off, *d_out;
+    HIPCHK(hipMalloc(&d_sets, n * 4));
+    HIPCHK(hipMalloc(&d_cands, n * 4));
+    HIPCHK(hipMalloc(&d_off, n * 4));
+    HIPCHK(hipMalloc(&d_out, total * 32));
+    HIPCHK(hipMemcpyAsync(d_sets, set_ids, n * 4, hipMemcpyHostToDevice, g_stream));
+    HIPCHK(hipMemcpyAsync(d_cands, cand_ids, n * 4, hipMemcpyHostToDevice, g_stream));
+    HIPCHK(hipMemcpyAsync(d_off, off.data(), n * 4, hipMemcpyHostToDevice, g_stream));
+    const uint32_t mv = std::max<uint32_t>(B->max_vars, 1u);
+    const uint64_t threads = (uint64_t)n * mv;
+    hipLaunchKernelGGL(pf_materialize_kernel, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0,
+                       g_stream, B->d_descs, B->d_code, B->d_consts, B->d_schema, B->d_parents,
+                       global_seed, d_sets, d_cands, d_off, (uint32_t)n, mv, d_out);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(values_out, d_out, total * 32, hipMemcpyDeviceToHost, g_stream));
+    HIPCHK(hipStreamSynchronize(g_stream));
+    hipFree(d_sets);
+    hipFree(d_cands);
+    hipFree(d_off);
+    hipFree(d_out);
+    return 0;
+}
+
+static int eval_launch(Batch* B, uint32_t set, const uint32_t* d_soa, uint32_t n_cand,
+                       uint8_t* d_out, hipStream_t st) {
+    if (set >= B->n_sets) return fail("eval: set %u out of range", set);
+    if (n_cand == 0) return 0;
+    hipLaunchKernelGGL(pf_eval_soa_kernel, dim3((n_cand + 255) / 256), dim3(256), 0, st, B->d_descs,
+                       set, B->d_code, B->d_consts, B->d_schema, B->d_parents, d_soa, n_cand, d_out);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int pf_eval_assignments(uint64_t handle, uint32_t set, const uint32_t* soa, uint32_t n_cand,
+                        uint8_t* sat_out) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (ensure_init_locked()) return -1;
+    Batch* B = as_batch(handle);
+    if (!B) return fail("pf_eval_assignments: null batch");
+    if (set >= B->n_sets) return fail("eval: set %u out of range", set);
+    if (n_cand == 0) return 0;
+    const size_t nv = std::max<uint32_t>(B->h_descs[set].n_vars, 1u);
+    const size_t bytes = nv * 8 * (size_t)n_cand * 4;
+    uint32_t* d_soa;
+    uint8_t* d_out;
+    HIPCHK(hipMalloc(&d_soa, bytes));
+    HIPCHK(hipMalloc(&d_out, n_cand));
+    HIPCHK(hipMemcpyAsync(d_soa, soa, bytes, hipMemcpyHostToDevice, g_stream));
+    if (eval_launch(B, set, d_soa, n_cand, d_out, g_stream)) return -1;
+    HIPCHK(hipMemcpyAsync(sat_out, d_out, n_cand, hipMemcpyDeviceToHost, g_stream));
+    HIPCHK(hipStreamSynchronize(g_stream));
+    hipFree(d_soa);
+    hipFree(d_out);
+    return 0;
+}
+
+int pf_eval_assignments_dev(uint64_t handle, uint32_t set, const uint32_t* d_soa,
+                            uint32_t n_cand, uint8_t* d_sat_out, void* stream) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (ensure_init_locked()) return -1;
+    Batch* B = as_batch(handle);
+    if (!B) return fail("pf_eval_assignments_dev: null batch");
+    return eval_launch(B, set, d_soa, n_cand, d_sat_out, pick_stream(stream));
+}
+
+int pf_keccak256_batch(const uint8_t* data, const uint64_t* offsets, size_t n, uint8_t* out32) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (ensure_init_locked()) return -1;
+    if (n == 0) return 0;
+    for (size_t i = 0; i < n; i++)
+        if (offsets[i + 1] < offsets[i]) return fail("keccak: offsets not monotone at %zu", i);
+    const uint64_t total = offsets[n];
+    uint8_t *d_data, *d_out;
+    uint64_t* d_off;
+    HIPCHK(hipMalloc(&d_data, total ? total : 8));
+    HIPCHK(hipMalloc(&d_off, (n + 1) * 8));
+    HIPCHK(hipMalloc(&d_out, n * 32));
+    if (total) HIPCHK(hipMemcpyAsync(d_data, data, total, hipMemcpyHostToDevice, g_stream));
+    HIPCHK(hipMemcpyAsync(d_off, offsets, (n + 1) * 8, hipMemcpyHostToDevice, g_stream));
+    hipLaunchKernelGGL(pf_keccak_var_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, g_stream,
+                       d_data, d_off, (uint64_t)n, d_out);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(out32, d_out, n * 32, hipMemcpyDeviceToHost, g_stream));
+    HIPCHK(hipStreamSynchronize(g_stream));
+    hipFree(d_data);
+    hipFree(d_off);
+    hipFree(d_out);
+    return 0;
+}
+
+int pf_keccak256_fixed_dev(const uint8_t* d_data, uint32_t len, size_t n, uint8_t* d_out32,
+                           float* kernel_ms, void* stream) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (ensure_init_locked()) return -1;
+    if (n == 0) return 0;
+    hipStream_t st = pick_stream(stream);
+    HIPCHK(hipEventRecord(g_ev0, st));
+    hipLaunchKernelGGL(pf_keccak_fixed_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st,
+                       d_data, len, (uint64_t)n, d_out32);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(g_ev1, st));
+    if (kernel_ms) {
+        HIPCHK(hipEventSynchronize(g_ev1));
+        HIPCHK(hipEventElapsedTime(kernel_ms, g_ev0, g_ev1));
+    }
+    return 0;
+}
+
+}  // extern "C"

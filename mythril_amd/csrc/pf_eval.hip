@@ -1,0 +1,580 @@
+// pf_eval.hip — gfx950 kernels of the batched path-feasibility engine.
+//
+// Execution model:
+//   * one wavefront lane = one candidate assignment; a wave evaluates one constraint set's
+//     bytecode for 64 candidates at a time.  The instruction stream is wave-uniform, so it
+//     is fetched with scalar loads (s_load_dwordx4) and dispatched with scalar branches.
+//   * the W register file is limb-sliced: bank k (an ext_vector of 16 dwords) holds limb k
+//     of all 16 registers, so reading register r is one s_set_gpr_idx_on + 8 v_mov (the
+//     index is an SGPR) — no scratch, no LDS.  Bool registers live in one 32-dword bank.
+//   * candidates are generated in-register from Philox4x32-10 (include/pf_bytecode.h
+//     contract); only (set, candidate index) ever leaves the kernel.
+//   * ballot early exit: a wave records the smallest satisfying candidate with atomicMin
+//     and stops; other waves of the set stop once a witness below their candidates exists.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/pf_bytecode.h"
+#include "u256.h"
+
+using pf::u256;
+
+typedef uint32_t v16u __attribute__((ext_vector_type(16)));
+typedef uint32_t v32u __attribute__((ext_vector_type(32)));
+
+namespace {
+
+// W bank k holds limb k of all 16 wide registers.  These are macros, not functions: taking
+// the bank array by reference defeats AMDGPUPromoteAlloca (the banks land in scratch), while
+// direct element accesses become one s_set_gpr_idx_on + 8 v_mov per operand.
+#define RD_W(dst, W, r)                                        \
+    do {                                                       \
+        _Pragma("unroll") for (int k_ = 0; k_ < 8; k_++) (dst).l[k_] = (W)[k_][(r)]; \
+    } while (0)
+#define WR_W(W, r, src)                                        \
+    do {                                                       \
+        _Pragma("unroll") for (int k_ = 0; k_ < 8; k_++) (W)[k_][(r)] = (src).l[k_]; \
+    } while (0)
+
+// per-limb mask for width w (w uniform -> scalar arithmetic)
+PF_INL uint32_t limb_mask(uint32_t w, int i) {
+    uint32_t lo = (uint32_t)i * 32u;
+    return w >= lo + 32u ? 0xffffffffu : (w <= lo ? 0u : ((1u << (w - lo)) - 1u));
+}
+
+PF_INL void maskw(u256& x, uint32_t w) {
+    if (w < 256u) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) x.l[i] &= limb_mask(w, i);
+    }
+}
+
+// sign-extend a w-bit value (bits >= w zero) to 256 bits
+PF_INL u256 sextw(const u256& x, uint32_t w) {
+    if (w >= 256u) return x;
+    uint32_t li = (w - 1u) >> 5, bi = (w - 1u) & 31u;
+    uint32_t word = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) word = ((uint32_t)i == li) ? x.l[i] : word;
+    uint32_t fill = 0u - ((word >> bi) & 1u);
+    u256 r;
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.l[i] = x.l[i] | (fill & ~limb_mask(w, i));
+    return r;
+}
+
+// value >= w (shift amounts)
+PF_INL uint32_t ge_width(const u256& b, uint32_t w) {
+    uint32_t hi = 0;
+#pragma unroll
+    for (int i = 1; i < 8; i++) hi |= b.l[i];
+    return (hi != 0u) || (b.l[0] >= w);
+}
+
+PF_INL u256 pow2(uint32_t k) {  // 2^k, k < 256 (per lane)
+    u256 r;
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.l[i] = ((k >> 5) == (uint32_t)i) ? (1u << (k & 31u)) : 0u;
+    return r;
+}
+
+PF_INL u256 pow2m1(uint32_t k) {  // 2^k - 1
+    u256 r;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        uint32_t li = k >> 5;
+        r.l[i] = ((uint32_t)i < li) ? 0xffffffffu : (((uint32_t)i == li) ? ((1u << (k & 31u)) - 1u) : 0u);
+    }
+    return r;
+}
+
+// signed division family on sign-extended 256-bit operands (SMT-LIB2 definitions)
+PF_INL u256 sdivrem(const u256& a, const u256& b, int which /*0 sdiv,1 srem,2 smod*/) {
+    uint32_t sa = a.l[7] >> 31, sb = b.l[7] >> 31;
+    u256 ua = sa ? pf::neg256(a) : a;
+    u256 ub = sb ? pf::neg256(b) : b;
+    u256 q, r;
+    pf::udivrem256(ua, ub, &q, &r);
+    if (which == 0) return (sa ^ sb) ? pf::neg256(q) : q;
+    if (which == 1) return sa ? pf::neg256(r) : r;
+    // smod: sign follows divisor
+    if (pf::iszero256(r)) return r;
+    if (!sa && !sb) return r;
+    if (sa && !sb) return pf::add256(pf::neg256(r), b);
+    if (!sa && sb) return pf::add256(r, b);
+    return pf::neg256(r);
+}
+
+PF_INL u256 expmod(const u256& a, const u256& b, uint32_t w) {
+    u256 r = pf::zero256();
+    r.l[0] = 1u;
+    u256 base = a, e = b;
+    for (uint32_t i = 0; i < w; i++) {  // fixed w square-and-multiply steps
+        u256 t = pf::mul256(r, base);
+        r = pf::sel256(e.l[0] & 1u, t, r);
+        base = pf::mul256(base, base);
+#pragma unroll
+        for (int k = 0; k < 7; k++) e.l[k] = (e.l[k] >> 1) | (e.l[k + 1] << 31);
+        e.l[7] >>= 1;
+    }
+    return r;
+}
+
+// ---- Philox4x32-10 -------------------------------------------------------------------
+PF_INL uint4 philox(uint4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        uint32_t hi0 = __umulhi(PF_PHILOX_M0, c.x), lo0 = PF_PHILOX_M0 * c.x;
+        uint32_t hi1 = __umulhi(PF_PHILOX_M1, c.z), lo1 = PF_PHILOX_M1 * c.z;
+        c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
+        k0 += PF_PHILOX_W0;
+        k1 += PF_PHILOX_W1;
+    }
+    return c;
+}
+
+struct SetCtx {
+    const uint4* code;    // instruction stream of this set
+    const uint32_t* consts;   // this set's constants (8 u32 each)
+    const uint4* schema;  // this set's variable schema
+    const uint32_t* parents;  // parent values base (global) or null
+    uint32_t n_ins, n_const, n_vars, seed;
+    uint32_t k0, k1;      // Philox key
+};
+
+// candidate value of variable v (include/pf_bytecode.h generator contract)
+PF_INL u256 gen_var(const SetCtx& S, uint32_t v, uint32_t cand) {
+    uint4 sc = S.schema[v];  // uniform -> scalar load
+    uint32_t kind = sc.x & 0xffu, w = (sc.x >> 8) & 0x3ffu;
+    uint32_t hint0 = sc.y, hint1 = sc.z, pslot = sc.w;
+    u256 out;
+    if (cand == 0u && pslot != PF_NO_PARENT) {
+        const uint32_t* p = S.parents + (size_t)pslot * 8u;
+#pragma unroll
+        for (int i = 0; i < 8; i++) out.l[i] = p[i];
+        maskw(out, w);
+        return out;
+    }
+    uint4 r0 = philox(make_uint4(cand, v, 0u, 0u), S.k0, S.k1);
+    uint4 r1 = philox(make_uint4(cand, v, 1u, 0u), S.k0, S.k1);
+    uint4 m = philox(make_uint4(cand, v, 2u, 0u), S.k0, S.k1);
+    u256 rv;
+    rv.l[0] = r0.x; rv.l[1] = r0.y; rv.l[2] = r0.z; rv.l[3] = r0.w;
+    rv.l[4] = r1.x; rv.l[5] = r1.y; rv.l[6] = r1.z; rv.l[7] = r1.w;
+    if (kind == PF_VK_KECCAK) {
+        const uint32_t* lo = S.consts + (size_t)hint0 * 8u;
+        u256 k = pf::zero256();
+        k.l[0] = r0.x << 6;
+        k.l[1] = (r0.y << 6) | (r0.x >> 26);
+        k.l[2] = (r0.z << 6) | (r0.y >> 26);
+        k.l[3] = ((r0.w & 0x1fffffu) << 6) | (r0.z >> 26);
+        u256 base;
+#pragma unroll
+        for (int i = 0; i < 8; i++) base.l[i] = lo[i];
+        out = pf::add256(base, k);
+        maskw(out, w);
+        return out;
+    }
+    if (kind == PF_VK_SMALL) {
+        out = pf::zero256();
+        out.l[0] = (hint0 == 0xffffffffu) ? r0.x : (r0.x % (hint0 + 1u));
+        maskw(out, w);
+        return out;
+    }
+    if (kind == PF_VK_BOOL) {
+        out = pf::zero256();
+        out.l[0] = r0.x & 1u;
+        return out;
+    }
+    if (kind == PF_VK_ACTOR && (m.y & 3u) < hint1) {
+        const uint32_t* a = S.consts + (size_t)(hint0 + (m.y & 3u)) * 8u;
+#pragma unroll
+        for (int i = 0; i < 8; i++) out.l[i] = a[i];
+        maskw(out, w);
+        return out;
+    }
+    uint32_t sel = m.x & 15u;
+    if (sel <= 4u) {
+        out = rv;
+    } else if (sel <= 8u) {
+        uint32_t j = m.y % 12u, k = m.z % w;
+        if (j < 4u) {
+            out = pf::zero256();
+            out.l[0] = j;
+        } else if (j == 4u) {
+            out = pf::ones256();
+        } else if (j == 5u) {
+            out = pf::ones256();
+            out.l[0] = 0xfffffffeu;
+            // masked below: (2^w - 1) - 1 = 2^w - 2 for w > 1; w == 1 -> 0 (Python: (1-1)&1 = 0)
+            if (w < 32u) out.l[0] = ((w == 32u) ? 0xffffffffu : ((1u << w) - 1u)) - 1u;
+        } else if (j == 6u) {
+            out = pow2(w - 1u);
+        } else if (j == 7u) {
+            out = pow2m1(w - 1u);
+        } else if (j == 8u) {
+            out = pow2(k);
+        } else if (j == 9u) {
+            out = pow2m1(k);
+        } else if (j == 10u) {
+            out = pf::add256(pow2(k), pf::zero256());
+            u256 one = pf::zero256();
+            one.l[0] = 1u;
+            out = pf::add256(out, one);
+        } else {
+            out = pow2m1(160u);
+        }
+    } else if (sel <= 11u) {
+        if (S.n_const > 0u) {
+            const uint32_t* c = S.consts + (size_t)(m.y % S.n_const) * 8u;
+#pragma unroll
+            for (int i = 0; i < 8; i++) out.l[i] = c[i];
+            uint32_t dsel = m.z % 3u;
+            u256 dlt = (dsel == 0u) ? pf::zero256() : ((dsel == 1u) ? pow2(0u) : pf::ones256());
+            out = pf::add256(out, dlt);
+        } else {
+            out = rv;
+        }
+    } else if (sel <= 13u) {
+        if (pslot != PF_NO_PARENT) {
+            const uint32_t* p = S.parents + (size_t)pslot * 8u;
+#pragma unroll
+            for (int i = 0; i < 8; i++) out.l[i] = p[i];
+            if ((m.y & 3u) == 0u) {
+                u256 f = pow2(m.z % w);
+#pragma unroll
+                for (int i = 0; i < 8; i++) out.l[i] ^= f.l[i];
+            }
+        } else {
+            out = pf::zero256();
+            out.l[0] = r0.x & 0xffu;
+        }
+    } else {
+        out = pf::zero256();
+        uint32_t nb = 1u + (m.y & 15u);
+        out.l[0] = r0.x & ((nb >= 32u) ? 0xffffffffu : ((1u << nb) - 1u));
+    }
+    maskw(out, w);
+    return out;
+}
+
+enum Mode { MODE_GEN = 0, MODE_SOA = 1 };
+
+// operand traffic per opcode: bit0 reads W[a], bit1 reads W[b], bit2 writes W[d].
+// One read-a, one read-b and one write site for the whole interpreter keeps the W banks
+// promotable to VGPRs (few extract/insert users) and the code small.
+#define RA 1u
+#define RB 2u
+#define WW 4u
+__constant__ uint8_t kOpTraffic[PF_NUM_OPCODES] = {
+    /*END*/ 0, /*CONST*/ WW, /*VAR*/ WW, /*MOV*/ RA | WW,
+    /*ADD..SMOD (4..11)*/ RA | RB | WW, RA | RB | WW, RA | RB | WW, RA | RB | WW, RA | RB | WW,
+    RA | RB | WW, RA | RB | WW, RA | RB | WW,
+    /*AND OR XOR (12..14)*/ RA | RB | WW, RA | RB | WW, RA | RB | WW,
+    /*NOT NEG*/ RA | WW, RA | WW,
+    /*SHL LSHR ASHR EXP (17..20)*/ RA | RB | WW, RA | RB | WW, RA | RB | WW, RA | RB | WW,
+    /*EXTRACT*/ RA | WW, /*CONCAT*/ RA | RB | WW, /*SEXT*/ RA | WW, /*ITE*/ RA | RB | WW,
+    /*25..39*/ 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+    /*B_CONST B_VAR*/ 0, 0,
+    /*EQ ULT ULE SLT SLE (42..46)*/ RA | RB, RA | RB, RA | RB, RA | RB, RA | RB,
+    /*B_AND B_OR B_XOR B_NOT B_ITE (47..51)*/ 0, 0, 0, 0, 0,
+    /*UADD_NOOVF UMUL_NOOVF*/ RA | RB, RA | RB,
+    /*54..63*/ 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+
+// Run one set's program for this lane's candidate.  Returns the lane's root (0/1);
+// *complete = 1 if the program ran to END (not short-circuited).  `ops` accumulates
+// aux1 (per-lane algorithmic cost) of every executed instruction.
+template <int MODE>
+PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_t flags,
+                            const uint32_t* __restrict__ soa, uint32_t soa_n,
+                            uint32_t* complete, uint64_t* ops) {
+    // element-wise init: a whole-vector store would defeat promote-alloca-to-vector
+    v16u W[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+#pragma unroll
+        for (int r = 0; r < 16; r++) W[k][r] = 0u;
+    // the 32 bool registers are the bits of one VGPR (bit r = B register r)
+    uint32_t Bk = 0u;
+#define BGET(r) ((Bk >> ((r) & 31u)) & 1u)
+    uint32_t root = 1u;
+    uint64_t cost = 0;
+    *complete = 0u;
+    for (uint32_t pc = 0; pc < S.n_ins; pc++) {
+        const uint4 I = S.code[pc];
+        const uint32_t op = I.x & 0xffu;
+        const uint32_t w = (I.x >> 8) & 0x3ffu;
+        const uint32_t d = I.y & 0xffu, a = (I.y >> 8) & 0xffu, b = (I.y >> 16) & 0xffu,
+                       c = (I.y >> 24) & 0xffu;
+        cost += I.w;
+        if (op == PF_END) {
+            *complete = 1u;
+            break;
+        }
+        const uint32_t tr = kOpTraffic[op & (PF_NUM_OPCODES - 1)];
+        u256 x, y, z;
+        if (tr & RA) RD_W(x, W, a & 15u);
+        if (tr & RB) RD_W(y, W, b & 15u);
+        uint32_t bres = 0;  // bool result for B ops
+        switch (op) {
+            case PF_W_ADD: z = pf::add256(x, y); break;
+            case PF_W_SUB: z = pf::sub256(x, y); break;
+            case PF_W_MUL: z = pf::mul256(x, y); break;
+            case PF_W_UDIV:
+            case PF_W_UREM: {
+                u256 q, r;
+                pf::udivrem256(x, y, &q, &r);
+                z = (op == PF_W_UDIV) ? q : r;
+                break;
+            }
+            case PF_W_SDIV: z = sdivrem(sextw(x, w), sextw(y, w), 0); break;
+            case PF_W_SREM: z = sdivrem(sextw(x, w), sextw(y, w), 1); break;
+            case PF_W_SMOD: z = sdivrem(sextw(x, w), sextw(y, w), 2); break;
+            case PF_W_AND:
+#pragma unroll
+                for (int i = 0; i < 8; i++) z.l[i] = x.l[i] & y.l[i];
+                break;
+            case PF_W_OR:
+#pragma unroll
+                for (int i = 0; i < 8; i++) z.l[i] = x.l[i] | y.l[i];
+                break;
+            case PF_W_XOR:
+#pragma unroll
+                for (int i = 0; i < 8; i++) z.l[i] = x.l[i] ^ y.l[i];
+                break;
+            case PF_W_SHL: z = pf::shl256(x, y.l[0], ge_width(y, w)); break;
+            case PF_W_LSHR: {
+                uint32_t big = ge_width(y, w);
+                z = pf::shr256(x, big ? 0u : y.l[0], 0u);
+                if (big) z = pf::zero256();
+                break;
+            }
+            case PF_W_ASHR: {
+                u256 sx = sextw(x, w);
+                uint32_t big = ge_width(y, w);
+                uint32_t f = 0u - (sx.l[7] >> 31);
+                z = pf::shr256(sx, big ? 255u : y.l[0], f);
+                break;
+            }
+            case PF_W_EXP: z = expmod(x, y, w); break;
+            case PF_W_CONST: {
+                const uint32_t* cp = S.consts + (size_t)I.z * 8u;
+#pragma unroll
+                for (int i = 0; i < 8; i++) z.l[i] = cp[i];
+                break;
+            }
+            case PF_W_VAR:
+                if (MODE == MODE_GEN) {
+                    z = gen_var(S, I.z, cand);
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 8; i++)
+                        z.l[i] = active ? soa[((size_t)I.z * 8u + i) * soa_n + cand] : 0u;
+                }
+                break;
+            case PF_W_MOV: z = x; break;
+            case PF_W_NOT: z = pf::not256(x); break;
+            case PF_W_NEG: z = pf::neg256(x); break;
+            case PF_W_EXTRACT: z = pf::shr256(x, I.z & 255u, 0u); break;
+            case PF_W_CONCAT: {
+                z = pf::shl256(x, I.z, I.z >= 256u);
+#pragma unroll
+                for (int i = 0; i < 8; i++) z.l[i] |= y.l[i];
+                break;
+            }
+            case PF_W_SEXT: z = sextw(x, I.z); break;
+            case PF_W_ITE: z = pf::sel256(BGET(c), x, y); break;
+            case PF_B_CONST: bres = I.z & 1u; break;
+            case PF_B_VAR:
+                if (MODE == MODE_GEN) {
+                    bres = gen_var(S, I.z, cand).l[0] & 1u;
+                } else {
+                    bres = active ? (soa[((size_t)I.z * 8u) * soa_n + cand] & 1u) : 0u;
+                }
+                break;
+            case PF_B_EQ: bres = pf::eq256(x, y); break;
+            case PF_B_ULT: bres = pf::ult256(x, y); break;
+            case PF_B_ULE: bres = pf::ult256(y, x) ^ 1u; break;
+            case PF_B_SLT:
+            case PF_B_SLE: {
+                u256 sx = sextw(x, w), sy = sextw(y, w);
+                sx.l[7] ^= 0x80000000u;
+                sy.l[7] ^= 0x80000000u;
+                bres = (op == PF_B_SLT) ? pf::ult256(sx, sy) : (pf::ult256(sy, sx) ^ 1u);
+                break;
+            }
+            case PF_B_UADD_NOOVF: {
+                uint32_t co;
+                u256 s = pf::add256c(x, y, &co);
+                u256 sm = s;
+                maskw(sm, w);  // no overflow iff the sum fits in w bits
+                bres = (co == 0u) && pf::eq256(sm, s);
+                break;
+            }
+            case PF_B_UMUL_NOOVF: {
+                uint32_t ov = pf::mul256_overflows(x, y);
+                u256 p = pf::mul256(x, y);
+                u256 pm = p;
+                maskw(pm, w);
+                bres = (ov == 0u) && pf::eq256(pm, p);
+                break;
+            }
+            case PF_B_AND: bres = BGET(a) & BGET(b); break;
+            case PF_B_OR: bres = BGET(a) | BGET(b); break;
+            case PF_B_XOR: bres = BGET(a) ^ BGET(b); break;
+            case PF_B_NOT: bres = BGET(a) ^ 1u; break;
+            case PF_B_ITE: bres = BGET(c) ? BGET(a) : BGET(b); break;
+            case PF_ASSERT:
+                root &= BGET(a);
+                if (flags & PF_FLAG_SHORTCIRCUIT) {
+                    if (__ballot(root && active) == 0ull) {
+                        *ops += cost;
+                        return 0u;
+                    }
+                }
+                break;
+            default: break;
+        }
+        {
+            // Unconditional write: ops without a W result write the sink register
+            // PF_W_SINK.  A conditional insert would make the loop-carried banks a phi of
+            // old/new values, which costs a full bank copy (~100 extra VGPRs, spills).
+            maskw(z, w);
+            const uint32_t dd = (tr & WW) ? (d & 15u) : (uint32_t)PF_W_SINK;
+            WR_W(W, dd, z);
+        }
+        if (op >= PF_B_CONST && op <= PF_B_UMUL_NOOVF) {
+            const uint32_t bit = 1u << (d & 31u);
+            Bk = (Bk & ~bit) | (bres ? bit : 0u);
+        }
+    }
+    *ops += cost;
+    return root;
+#undef BGET
+}
+
+PF_INL SetCtx make_ctx(const pf_set_desc* __restrict__ descs, uint32_t set,
+                       const uint4* __restrict__ code, const uint32_t* __restrict__ consts,
+                       const uint4* __restrict__ schema, const uint32_t* __restrict__ parents,
+                       uint64_t gseed) {
+    pf_set_desc D = descs[set];
+    SetCtx S;
+    S.code = code + D.code_off;
+    S.consts = consts + (size_t)D.const_off * 8u;
+    S.schema = schema + D.var_off;
+    S.parents = parents;
+    S.n_ins = D.n_ins;
+    S.n_const = D.n_const;
+    S.n_vars = D.n_vars;
+    S.seed = D.seed;
+    S.k0 = (uint32_t)gseed ^ D.seed;
+    S.k1 = (uint32_t)(gseed >> 32);
+    return S;
+}
+
+}  // namespace
+
+// ---- search kernel: generate + evaluate + ballot early exit ---------------------------
+// grid: one wave per (set, slice); a slice is `per_wave` consecutive candidates.
+extern "C" __global__ void __launch_bounds__(256, 2)
+pf_check_kernel(const pf_set_desc* __restrict__ descs, uint32_t n_sets,
+                const uint4* __restrict__ code, const uint32_t* __restrict__ consts,
+                const uint4* __restrict__ schema, const uint32_t* __restrict__ parents,
+                uint64_t gseed, uint32_t budget, uint32_t per_wave, uint32_t slices,
+                uint32_t flags, uint64_t deadline_ticks, uint64_t* __restrict__ t0_slot,
+                uint32_t* __restrict__ found, unsigned long long* __restrict__ counters) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+    if (wave >= n_sets * slices) return;
+    const uint32_t set = __builtin_amdgcn_readfirstlane(wave / slices);
+    const uint32_t slice = __builtin_amdgcn_readfirstlane(wave % slices);
+    const SetCtx S = make_ctx(descs, set, code, consts, schema, parents, gseed);
+
+    uint64_t t0 = 0;
+    if (deadline_ticks) {
+        uint64_t now = __builtin_amdgcn_s_memrealtime();
+        unsigned long long prev = atomicCAS((unsigned long long*)t0_slot, 0ull, (unsigned long long)now);
+        t0 = prev ? prev : now;
+    }
+    const uint32_t begin = slice * per_wave;
+    const uint32_t end = min(budget, begin + per_wave);
+    uint64_t evals_full = 0, decided = 0, ops = 0;
+    for (uint32_t base = begin; base < end; base += 64u) {
+        if (flags & PF_FLAG_EARLY_EXIT) {
+            uint32_t f = __hip_atomic_load(found + set, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (__builtin_amdgcn_readfirstlane(f) <= base) break;
+        }
+        if (deadline_ticks) {
+            uint64_t now = __builtin_amdgcn_s_memrealtime();
+            if (now - t0 > deadline_ticks) break;
+        }
+        const uint32_t cand = base + lane;
+        const bool active = cand < end;
+        uint32_t complete = 0;
+        uint64_t lane_ops = 0;
+        uint32_t sat = run_program<MODE_GEN>(S, cand, active, flags, nullptr, 0u, &complete, &lane_ops);
+        const uint64_t m_act = __ballot(active);
+        const uint64_t m_sat = __ballot(active && sat);
+        const uint64_t m_full = __ballot(active && complete);
+        decided += __popcll(m_act);
+        evals_full += __popcll(m_full);
+        ops += lane_ops * (uint64_t)__popcll(m_act);
+        if (m_sat) {
+            uint32_t first = base + (uint32_t)__builtin_ctzll(m_sat);
+            if (lane == 0) atomicMin(found + set, first);
+            if (flags & PF_FLAG_EARLY_EXIT) break;
+        }
+    }
+    if (lane == 0) {
+        atomicAdd(counters + 0, (unsigned long long)evals_full);
+        atomicAdd(counters + 1, (unsigned long long)decided);
+        if (flags & PF_FLAG_COUNT_OPS) atomicAdd(counters + 2, (unsigned long long)ops);
+    }
+}
+
+// ---- explicit-assignment evaluation (SoA [var][limb][cand]) --------------------------
+extern "C" __global__ void __launch_bounds__(256, 2)
+pf_eval_soa_kernel(const pf_set_desc* __restrict__ descs, uint32_t set,
+                   const uint4* __restrict__ code, const uint32_t* __restrict__ consts,
+                   const uint4* __restrict__ schema, const uint32_t* __restrict__ parents,
+                   const uint32_t* __restrict__ soa, uint32_t n_cand, uint8_t* __restrict__ out) {
+    const uint32_t cand = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool active = cand < n_cand;
+    const SetCtx S = make_ctx(descs, __builtin_amdgcn_readfirstlane(set), code, consts, schema, parents, 0ull);
+    uint32_t complete = 0;
+    uint64_t ops = 0;
+    uint32_t sat = run_program<MODE_SOA>(S, active ? cand : 0u, active, 0u, soa, n_cand, &complete, &ops);
+    if (active) out[cand] = (uint8_t)sat;
+}
+
+// ---- materialise witness assignments --------------------------------------------------
+// one thread per (request, variable); out offset per request given by req_off (in vars)
+extern "C" __global__ void __launch_bounds__(256)
+pf_materialize_kernel(const pf_set_desc* __restrict__ descs, const uint4* __restrict__ code,
+                      const uint32_t* __restrict__ consts, const uint4* __restrict__ schema,
+                      const uint32_t* __restrict__ parents, uint64_t gseed,
+                      const uint32_t* __restrict__ set_ids, const uint32_t* __restrict__ cand_ids,
+                      const uint32_t* __restrict__ req_off, uint32_t n_req, uint32_t max_vars,
+                      uint32_t* __restrict__ out) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t req = t / max_vars, v = t % max_vars;
+    if (req >= n_req) return;
+    const uint32_t set = set_ids[req];
+    pf_set_desc D = descs[set];
+    if (v >= D.n_vars) return;
+    SetCtx S;
+    S.code = code + D.code_off;
+    S.consts = consts + (size_t)D.const_off * 8u;
+    S.schema = schema + D.var_off;
+    S.parents = parents;
+    S.n_ins = D.n_ins;
+    S.n_const = D.n_const;
+    S.n_vars = D.n_vars;
+    S.seed = D.seed;
+    S.k0 = (uint32_t)gseed ^ D.seed;
+    S.k1 = (uint32_t)(gseed >> 32);
+    u256 x = gen_var(S, v, cand_ids[req]);
+    uint32_t* o = out + ((size_t)req_off[req] + v) * 8u;
+#pragma unroll
+    for (int i = 0; i < 8; i++) o[i] = x.l[i];
+}

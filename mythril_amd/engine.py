@@ -1,0 +1,149 @@
+"""Host-side driver of the batched path-feasibility engine (one process per GPU).
+
+This is the layer the SMT facade (mythril_amd.smt.solver) and the LASER plugin call.  It
+replaces the two CPU paths of the reference's query funnel with one GPU batch:
+
+* ``ModelCache.check_quick_sat`` — evaluate the conjunction under candidate models
+  (mythril/support/support_utils.py:57-71), here 65,536 generated candidates per set
+  instead of <= 100 cached z3 models;
+* the objective-free ``Optimize.check`` (mythril/support/model.py:37-59, :99-125) whenever a
+  witness is found; sets without a witness are left to z3 unchanged (soundness).
+"""
+
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from .ir import LIMBS, Batch, Program, from_limbs
+
+NOT_FOUND = 0xFFFFFFFF
+
+
+@dataclass
+class CheckResult:
+    found: np.ndarray        # [n_sets] uint32 smallest witness index or NOT_FOUND
+    evals_full: int
+    cands_decided: int
+    ops: int
+    kernel_ms: float
+
+    @property
+    def sat(self) -> np.ndarray:
+        return self.found != NOT_FOUND
+
+
+class DeviceBatch:
+    """A :class:`~mythril_amd.ir.Batch` resident in HBM (pf_batch_create)."""
+
+    def __init__(self, batch: Batch):
+        L = _lib.lib()
+        self.batch = batch
+        h = ctypes.c_uint64(0)
+        descs = np.ascontiguousarray(batch.descs, dtype=np.uint32)
+        code = np.ascontiguousarray(batch.code, dtype=np.uint32)
+        consts = np.ascontiguousarray(batch.consts, dtype=np.uint32)
+        schema = np.ascontiguousarray(batch.schema, dtype=np.uint32)
+        parents = np.ascontiguousarray(batch.parents, dtype=np.uint32)
+        _lib.check(L.pf_batch_create(
+            _lib.ptr_u32(code.reshape(-1)) if code.size else None, code.shape[0],
+            _lib.ptr_u32(consts.reshape(-1)) if consts.size else None, consts.shape[0],
+            _lib.ptr_u32(schema.reshape(-1)) if schema.size else None, schema.shape[0],
+            _lib.ptr_u32(parents.reshape(-1)) if parents.size else None, parents.shape[0],
+            _lib.ptr_u32(descs.reshape(-1)) if descs.size else None, descs.shape[0],
+            ctypes.byref(h)), "pf_batch_create")
+        self.handle = h.value
+
+    def __len__(self):
+        return len(self.batch)
+
+    def free(self):
+        if self.handle:
+            _lib.lib().pf_batch_free(self.handle)
+            self.handle = 0
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Engine:
+    """The per-process engine: one GPU, one library stream."""
+
+    def __init__(self, device: int = 0):
+        _lib.init(device)
+        self.device = device
+
+    # ---- search -------------------------------------------------------------------
+    def upload(self, programs: Sequence[Program] | Batch) -> DeviceBatch:
+        batch = programs if isinstance(programs, Batch) else Batch(programs)
+        return DeviceBatch(batch)
+
+    def check(self, db: DeviceBatch, budget: int = 65536, seed: int = 0, flags: int = 2,
+              timeout_ms: int = 0) -> CheckResult:
+        n = len(db)
+        found = np.full(max(n, 1), NOT_FOUND, dtype=np.uint32)
+        st = _lib.pf_stats()
+        _lib.check(_lib.lib().pf_check_batch(db.handle, seed, budget, flags, timeout_ms,
+                                            _lib.ptr_u32(found), None, ctypes.byref(st)),
+                   "pf_check_batch")
+        return CheckResult(found[:n], st.evals_full, st.cands_decided, st.ops, st.kernel_ms)
+
+    def materialize(self, db: DeviceBatch, set_ids: Sequence[int], cand_ids: Sequence[int],
+                    seed: int = 0) -> List[List[int]]:
+        """Concrete variable values of the given (set, candidate) pairs."""
+        set_ids = np.ascontiguousarray(set_ids, dtype=np.uint32)
+        cand_ids = np.ascontiguousarray(cand_ids, dtype=np.uint32)
+        nv = [int(db.batch.descs[s][5]) for s in set_ids]
+        total = sum(nv)
+        out = np.zeros(max(total, 1) * LIMBS, dtype=np.uint32)
+        if len(set_ids):
+            _lib.check(_lib.lib().pf_materialize(db.handle, seed, _lib.ptr_u32(set_ids),
+                                                _lib.ptr_u32(cand_ids), len(set_ids),
+                                                _lib.ptr_u32(out)), "pf_materialize")
+        res, off = [], 0
+        rows = out.reshape(-1, LIMBS)
+        for k in nv:
+            res.append([from_limbs(rows[off + i]) for i in range(k)])
+            off += k
+        return res
+
+    def eval_assignments(self, db: DeviceBatch, set_id: int, soa: np.ndarray) -> np.ndarray:
+        """SAT flag of each explicit candidate; soa is [var][limb][cand] uint32."""
+        soa = np.ascontiguousarray(soa, dtype=np.uint32)
+        n_cand = soa.shape[-1]
+        out = np.zeros(max(n_cand, 1), dtype=np.uint8)
+        _lib.check(_lib.lib().pf_eval_assignments(db.handle, set_id, _lib.ptr_u32(soa.reshape(-1)),
+                                                 n_cand, _lib.ptr_u8(out)), "pf_eval_assignments")
+        return out[:n_cand].astype(bool)
+
+    # ---- keccak -------------------------------------------------------------------
+    def keccak256(self, messages: Sequence[bytes]) -> List[bytes]:
+        n = len(messages)
+        if n == 0:
+            return []
+        offsets = np.zeros(n + 1, dtype=np.uint64)
+        offsets[1:] = np.cumsum([len(m) for m in messages], dtype=np.uint64)
+        data = np.frombuffer(b"".join(messages) or b"\0", dtype=np.uint8).copy()
+        out = np.zeros(32 * n, dtype=np.uint8)
+        _lib.check(_lib.lib().pf_keccak256_batch(_lib.ptr_u8(data), _lib.ptr_u64(offsets), n,
+                                                _lib.ptr_u8(out)), "pf_keccak256_batch")
+        return [out[32 * i:32 * i + 32].tobytes() for i in range(n)]
+
+
+_engine: Optional[Engine] = None
+
+
+def get_engine(device: Optional[int] = None) -> Engine:
+    global _engine
+    if _engine is None:
+        import os
+        dev = device if device is not None else int(os.environ.get("LOCAL_RANK", "0"))
+        _engine = Engine(dev)
+    return _engine

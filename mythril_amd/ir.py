@@ -1,0 +1,305 @@
+"""Flat register bytecode for batched path-feasibility (Python mirror of include/pf_bytecode.h).
+
+A :class:`Program` is one constraint set — the conjunction Mythril hands to
+``get_model`` (mythril/support/model.py:63-125) — lowered to 4-word instructions over
+two register classes (W: 256-bit, B: bool).  A :class:`Batch` concatenates many
+programs into the flat arrays the C ABI (include/pathfeas.h) consumes.
+
+The opcode numbers are checked against the C header by tests/test_abi.py.
+"""
+
+from __future__ import annotations
+
+import struct
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+NW = 15  # usable W registers; register 15 is the kernel's write sink
+NB = 32
+LIMBS = 8
+MAX_WIDTH = 256
+NO_PARENT = 0xFFFFFFFF
+
+# ---- opcodes (pf_bytecode.h enum pf_opcode) ------------------------------------
+END = 0
+W_CONST = 1
+W_VAR = 2
+W_MOV = 3
+W_ADD = 4
+W_SUB = 5
+W_MUL = 6
+W_UDIV = 7
+W_UREM = 8
+W_SDIV = 9
+W_SREM = 10
+W_SMOD = 11
+W_AND = 12
+W_OR = 13
+W_XOR = 14
+W_NOT = 15
+W_NEG = 16
+W_SHL = 17
+W_LSHR = 18
+W_ASHR = 19
+W_EXP = 20
+W_EXTRACT = 21
+W_CONCAT = 22
+W_SEXT = 23
+W_ITE = 24
+B_CONST = 40
+B_VAR = 41
+B_EQ = 42
+B_ULT = 43
+B_ULE = 44
+B_SLT = 45
+B_SLE = 46
+B_AND = 47
+B_OR = 48
+B_XOR = 49
+B_NOT = 50
+B_ITE = 51
+B_UADD_NOOVF = 52
+B_UMUL_NOOVF = 53
+ASSERT = 60
+
+OPNAMES = {v: k for k, v in dict(globals()).items()
+           if k.isupper() and isinstance(v, int) and (k.startswith(("W_", "B_")) or k in ("END", "ASSERT"))}
+
+# binary W -> W ops
+W_BINARY = (W_ADD, W_SUB, W_MUL, W_UDIV, W_UREM, W_SDIV, W_SREM, W_SMOD, W_AND, W_OR,
+            W_XOR, W_SHL, W_LSHR, W_ASHR, W_EXP)
+W_UNARY = (W_NOT, W_NEG, W_MOV)
+B_CMP = (B_EQ, B_ULT, B_ULE, B_SLT, B_SLE, B_UADD_NOOVF, B_UMUL_NOOVF)
+B_LOGIC = (B_AND, B_OR, B_XOR)
+
+# ---- variable kinds --------------------------------------------------------------
+VK_GENERIC = 0
+VK_ACTOR = 1
+VK_KECCAK = 2
+VK_SMALL = 3
+VK_BOOL = 4
+
+# ---- flags -----------------------------------------------------------------------
+FLAG_SHORTCIRCUIT = 1
+FLAG_EARLY_EXIT = 2
+FLAG_COUNT_OPS = 4
+
+# ---- algorithmic int32-op cost table -----------------------------
+# Ops not in the table (moves, constant loads, candidate generation) cost 0: they are
+# bookkeeping, not constraint arithmetic.  Width-generic ops scale by ceil(w/32)/8.
+_COST256 = {
+    W_ADD: 8, W_SUB: 8, W_NOT: 8, W_AND: 8, W_OR: 8, W_XOR: 8, W_NEG: 8,
+    W_ITE: 8, W_EXTRACT: 8, W_CONCAT: 8, W_SEXT: 8,
+    B_EQ: 8, B_ULT: 8, B_ULE: 8, B_SLT: 8, B_SLE: 8,
+    W_SHL: 16, W_LSHR: 16, W_ASHR: 16,
+    W_MUL: 72, B_UMUL_NOOVF: 72, B_UADD_NOOVF: 8,
+    W_UDIV: 256, W_UREM: 256, W_SDIV: 280, W_SREM: 280, W_SMOD: 280,
+    W_EXP: 512 * 72,
+}
+
+
+def op_cost(op: int, width: int) -> int:
+    """Algorithmic int32 ops of one node, scaled by width."""
+    c = _COST256.get(op)
+    if c is None:
+        return 0
+    nl = (max(1, width) + 31) // 32
+    return (c * nl + 7) // 8
+
+
+def mask(w: int) -> int:
+    return (1 << w) - 1
+
+
+def to_limbs(v: int, n: int = LIMBS) -> List[int]:
+    return [(v >> (32 * i)) & 0xFFFFFFFF for i in range(n)]
+
+
+def from_limbs(limbs: Sequence[int]) -> int:
+    v = 0
+    for i, x in enumerate(limbs):
+        v |= int(x) << (32 * i)
+    return v
+
+
+@dataclass
+class Var:
+    """One free symbol of a constraint set (candidate schema entry)."""
+
+    name: str
+    width: int
+    kind: int = VK_GENERIC
+    hint0: int = 0
+    hint1: int = 0
+    parent: Optional[int] = None  # parent-model value, if known
+
+
+@dataclass
+class Ins:
+    op: int
+    width: int = 256
+    dst: int = 0
+    a: int = 0
+    b: int = 0
+    c: int = 0
+    aux0: int = 0
+    aux1: int = 0
+    flags: int = 0
+
+    def words(self):
+        return (
+            (self.op & 0xFF) | ((self.width & 0x3FF) << 8) | ((self.flags & 0x3FFF) << 18),
+            (self.dst & 0xFF) | ((self.a & 0xFF) << 8) | ((self.b & 0xFF) << 16) | ((self.c & 0xFF) << 24),
+            self.aux0 & 0xFFFFFFFF,
+            self.aux1 & 0xFFFFFFFF,
+        )
+
+    def __repr__(self):
+        return (f"{OPNAMES.get(self.op, self.op)}/w{self.width} d={self.dst} a={self.a} "
+                f"b={self.b} c={self.c} x={self.aux0}")
+
+
+@dataclass
+class Program:
+    """One lowered constraint set."""
+
+    code: List[Ins] = field(default_factory=list)
+    consts: List[int] = field(default_factory=list)
+    vars: List[Var] = field(default_factory=list)
+    seed: int = 0
+    name: str = ""
+
+    def const_index(self, value: int) -> int:
+        value &= mask(MAX_WIDTH)
+        try:
+            return self.consts.index(value)
+        except ValueError:
+            self.consts.append(value)
+            return len(self.consts) - 1
+
+    def emit(self, *args, **kw) -> Ins:
+        ins = Ins(*args, **kw)
+        self.code.append(ins)
+        return ins
+
+    def finish(self) -> "Program":
+        if not self.code or self.code[-1].op != END:
+            self.code.append(Ins(END, 1))
+        return self
+
+    @property
+    def has_parent(self) -> bool:
+        return any(v.parent is not None for v in self.vars)
+
+    def node_cost(self) -> int:
+        return sum(op_cost(i.op, i.width) for i in self.code)
+
+    def validate(self) -> None:
+        """Host-side shape check run before anything is launched (kernel assumes these)."""
+        for i, ins in enumerate(self.code):
+            if ins.op not in OPNAMES:
+                raise ValueError(f"ins {i}: unknown opcode {ins.op}")
+            if ins.op != END and not (1 <= ins.width <= MAX_WIDTH):
+                raise ValueError(f"ins {i}: width {ins.width} out of range")
+            w_regs, b_regs = _reg_classes(ins.op)
+            for r in w_regs(ins):
+                if r >= NW:
+                    raise ValueError(f"ins {i}: W register {r} >= {NW}")
+            for r in b_regs(ins):
+                if r >= NB:
+                    raise ValueError(f"ins {i}: B register {r} >= {NB}")
+            if ins.op in (W_VAR, B_VAR) and ins.aux0 >= len(self.vars):
+                raise ValueError(f"ins {i}: variable {ins.aux0} out of range")
+            if ins.op == W_CONST and ins.aux0 >= len(self.consts):
+                raise ValueError(f"ins {i}: constant {ins.aux0} out of range")
+        if not self.code or self.code[-1].op != END:
+            raise ValueError("program must end with END")
+
+
+def _reg_classes(op):
+    """(W registers used, B registers used) of an instruction, as accessor functions."""
+    if op in (W_CONST, W_VAR):
+        return (lambda i: (i.dst,)), (lambda i: ())
+    if op in W_UNARY or op in (W_EXTRACT, W_SEXT):
+        return (lambda i: (i.dst, i.a)), (lambda i: ())
+    if op in W_BINARY or op == W_CONCAT:
+        return (lambda i: (i.dst, i.a, i.b)), (lambda i: ())
+    if op == W_ITE:
+        return (lambda i: (i.dst, i.a, i.b)), (lambda i: (i.c,))
+    if op in B_CMP:
+        return (lambda i: (i.a, i.b)), (lambda i: (i.dst,))
+    if op in (B_CONST, B_VAR):
+        return (lambda i: ()), (lambda i: (i.dst,))
+    if op in B_LOGIC:
+        return (lambda i: ()), (lambda i: (i.dst, i.a, i.b))
+    if op == B_NOT:
+        return (lambda i: ()), (lambda i: (i.dst, i.a))
+    if op == B_ITE:
+        return (lambda i: ()), (lambda i: (i.dst, i.a, i.b, i.c))
+    if op == ASSERT:
+        return (lambda i: ()), (lambda i: (i.a,))
+    return (lambda i: ()), (lambda i: ())
+
+
+class Batch:
+    """Many programs packed into the flat arrays of the C ABI (pf_set_desc et al.)."""
+
+    def __init__(self, programs: Sequence[Program]):
+        self.programs = list(programs)
+        code, consts, schema, parents, descs = [], [], [], [], []
+        for p in self.programs:
+            p.validate()
+            d_code = len(code)
+            for ins in p.code:
+                w0, w1, a0, _ = ins.words()
+                # aux1 carries the node's algorithmic int32-op cost (PF_FLAG_COUNT_OPS)
+                code.append((w0, w1, a0, op_cost(ins.op, ins.width) if ins.op != END else 0))
+            d_const = len(consts)
+            for c in p.consts:
+                consts.append(to_limbs(c))
+            d_var = len(schema)
+            has_par = p.has_parent
+            d_par = len(parents) if has_par else NO_PARENT
+            for v in p.vars:
+                slot = NO_PARENT
+                if has_par and v.parent is not None:
+                    slot = len(parents)
+                    parents.append(to_limbs(v.parent & mask(v.width)))
+                schema.append((v.kind | (v.width << 8), v.hint0 & 0xFFFFFFFF,
+                               v.hint1 & 0xFFFFFFFF, slot))
+            descs.append((d_code, len(p.code), d_const, len(p.consts), d_var, len(p.vars),
+                          p.seed & 0xFFFFFFFF, d_par))
+        self.code = np.asarray(code, dtype=np.uint32).reshape(-1, 4)
+        self.consts = np.asarray(consts, dtype=np.uint32).reshape(-1, LIMBS)
+        self.schema = np.asarray(schema, dtype=np.uint32).reshape(-1, 4)
+        self.parents = np.asarray(parents, dtype=np.uint32).reshape(-1, LIMBS)
+        self.descs = np.asarray(descs, dtype=np.uint32).reshape(-1, 8)
+
+    def __len__(self):
+        return len(self.programs)
+
+    def node_costs(self) -> np.ndarray:
+        return np.array([p.node_cost() for p in self.programs], dtype=np.int64)
+
+
+def pack_assignments(prog: Program, cands: Sequence[Sequence[int]]) -> np.ndarray:
+    """Explicit candidates -> SoA limbs [var][limb][cand] (coalesced on the GPU)."""
+    n = len(cands)
+    out = np.zeros((max(1, len(prog.vars)), LIMBS, n), dtype=np.uint32)
+    for c, vals in enumerate(cands):
+        for v, val in enumerate(vals):
+            val = int(val) & mask(prog.vars[v].width)
+            for l in range(LIMBS):
+                out[v, l, c] = (val >> (32 * l)) & 0xFFFFFFFF
+    return out
+
+
+def pack_assignments_np(limbs: np.ndarray) -> np.ndarray:
+    """[cand][var][limb] uint32 -> [var][limb][cand]."""
+    return np.ascontiguousarray(np.transpose(limbs, (1, 2, 0)))
+
+
+def u32_bytes(words: Sequence[int]) -> bytes:
+    return struct.pack(f"<{len(words)}I", *words)

@@ -1,0 +1,275 @@
+"""Lower a bit-vector DAG (a Mythril constraint set) to the flat register bytecode.
+
+Input is a :class:`Dag`: hash-consed nodes in topological order (leaves: variables and
+constants; interior nodes: one IR opcode each) plus the list of root Bool nodes whose
+conjunction is the query — exactly what ``get_model`` receives as ``constraints``
+(mythril/support/model.py:87-93) after ``Constraints.get_all_constraints`` appended the
+keccak conditions (mythril/laser/ethereum/state/constraints.py:132-133).
+
+Register allocation is a linear scan over an emission order that evaluates one root at a
+time (so PF_ASSERT can short-circuit a wave as early as possible).  Interior values stay
+resident until their last use; leaves (PF_W_VAR / PF_W_CONST / bool leaves) are
+rematerialised when registers run out (Belady: evict the leaf used farthest in the future).
+A set that would need more than PF_NW live interior values raises :class:`LoweringError`
+and is left to z3 (the engine never guesses).
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+from . import ir
+from .ir import Ins, Program, Var
+
+# node kinds beyond IR opcodes
+K_VAR = "var"       # aux = variable index      (W or B by width: width 0 => bool var)
+K_CONST = "const"   # aux = value
+K_BCONST = "bconst"  # aux = 0/1
+K_BVAR = "bvar"     # aux = variable index
+
+
+class LoweringError(ValueError):
+    """The set uses a shape the GPU bytecode does not cover; it falls back to z3."""
+
+
+@dataclass
+class Node:
+    kind: object          # IR opcode (int) or one of the K_* leaf kinds
+    width: int            # result width for W nodes, operand width for compares, 1 for bools
+    args: Tuple[int, ...] = ()
+    aux: int = 0
+    is_bool: bool = False
+
+
+@dataclass
+class Dag:
+    nodes: List[Node] = field(default_factory=list)
+    roots: List[int] = field(default_factory=list)
+    vars: List[Var] = field(default_factory=list)
+    _memo: Dict[tuple, int] = field(default_factory=dict)
+    _var_index: Dict[str, int] = field(default_factory=dict)
+
+    def add(self, kind, width, args=(), aux=0, is_bool=False) -> int:
+        key = (kind, width, tuple(args), aux, is_bool)
+        i = self._memo.get(key)
+        if i is None:
+            i = len(self.nodes)
+            self.nodes.append(Node(kind, width, tuple(args), aux, is_bool))
+            self._memo[key] = i
+        return i
+
+    # ---- leaves --------------------------------------------------------------------
+    def var(self, name: str, width: int, kind: int = ir.VK_GENERIC, hint0: int = 0,
+            hint1: int = 0, parent: Optional[int] = None) -> int:
+        idx = self._var_index.get(name)
+        if idx is None:
+            idx = len(self.vars)
+            self.vars.append(Var(name, width, kind, hint0, hint1, parent))
+            self._var_index[name] = idx
+        if width == 0 or kind == ir.VK_BOOL:
+            return self.add(K_BVAR, 1, (), idx, True)
+        return self.add(K_VAR, width, (), idx)
+
+    def const(self, value: int, width: int) -> int:
+        return self.add(K_CONST, width, (), value & ir.mask(width))
+
+    def bconst(self, value: bool) -> int:
+        return self.add(K_BCONST, 1, (), int(bool(value)), True)
+
+    # ---- interior ------------------------------------------------------------------
+    def op(self, opcode: int, width: int, *args: int, aux: int = 0) -> int:
+        is_bool = opcode >= ir.B_CONST
+        return self.add(opcode, width, args, aux, is_bool)
+
+    def assert_(self, b: int) -> None:
+        if not self.nodes[b].is_bool:
+            raise LoweringError("root is not a Bool")
+        self.roots.append(b)
+
+    def width(self, i: int) -> int:
+        return self.nodes[i].width
+
+
+_LEAF_KINDS = (K_VAR, K_CONST, K_BCONST, K_BVAR)
+
+
+def _emission_order(dag: Dag) -> List[Tuple[str, int]]:
+    """Post-order per root (roots in order); ('node', i) and ('assert', i) events."""
+    seen = set()
+    events: List[Tuple[str, int]] = []
+    for r in dag.roots:
+        stack = [(r, False)]
+        while stack:
+            i, done = stack.pop()
+            n = dag.nodes[i]
+            if n.kind in _LEAF_KINDS:
+                continue
+            if done:
+                if i not in seen:
+                    seen.add(i)
+                    events.append(("node", i))
+                continue
+            if i in seen:
+                continue
+            stack.append((i, True))
+            for a in reversed(n.args):
+                if dag.nodes[a].kind not in _LEAF_KINDS and a not in seen:
+                    stack.append((a, False))
+        events.append(("assert", r))
+    return events
+
+
+class _RegFile:
+    def __init__(self, n: int, cls: str):
+        self.n = n
+        self.cls = cls
+        self.free = list(range(n - 1, -1, -1))
+        self.holder: Dict[int, int] = {}   # reg -> node
+        self.where: Dict[int, int] = {}    # node -> reg
+
+    def alloc(self, node: int, evict_rank, pinned) -> int:
+        """Take a free register, else evict the cheapest-to-restore value (evict_rank)."""
+        if self.free:
+            r = self.free.pop()
+        else:
+            cands = [(evict_rank(nd), rg) for rg, nd in self.holder.items() if rg not in pinned]
+            cands = [c for c in cands if c[0] is not None]
+            if not cands:
+                raise LoweringError(f"more than {self.n} live {self.cls} values")
+            _, r = min(cands)
+            old = self.holder.pop(r)
+            del self.where[old]
+        self.holder[r] = node
+        self.where[node] = r
+        return r
+
+    def release(self, node: int) -> None:
+        r = self.where.pop(node, None)
+        if r is not None:
+            del self.holder[r]
+            self.free.append(r)
+
+
+_REMAT_MAX = 6     # nodes re-emitted to restore one evicted interior value
+_REMAT_OPCOST = 16  # only cheap ops (compare/ite/logic/extract/concat) are recomputed
+
+
+def lower(dag: Dag, seed: int = 0, name: str = "") -> Program:
+    prog = Program(vars=list(dag.vars), seed=seed, name=name)
+    events = _emission_order(dag)
+    uses: Dict[int, List[int]] = {}
+    for t, (kind, i) in enumerate(events):
+        if kind == "node":
+            for a in dag.nodes[i].args:
+                uses.setdefault(a, []).append(t)
+        else:
+            uses.setdefault(i, []).append(t)
+
+    def next_use(nd: int, now: int) -> int:
+        lst = uses.get(nd, [])
+        lo, hi = 0, len(lst)
+        while lo < hi:  # first use > now
+            mid = (lo + hi) // 2
+            if lst[mid] <= now:
+                lo = mid + 1
+            else:
+                hi = mid
+        return lst[lo] if lo < len(lst) else 1 << 30
+
+    remat_memo: Dict[int, Optional[int]] = {}
+
+    def remat_size(nd: int) -> Optional[int]:
+        """Nodes to re-emit to restore nd (None = must stay resident)."""
+        if nd in remat_memo:
+            return remat_memo[nd]
+        n = dag.nodes[nd]
+        if n.kind in _LEAF_KINDS:
+            res: Optional[int] = 1
+        elif ir.op_cost(n.kind, n.width) > _REMAT_OPCOST or n.kind == ir.W_EXP:
+            res = None
+        else:
+            tot = 1
+            for a in n.args:
+                sa = remat_size(a)
+                if sa is None:
+                    tot = None
+                    break
+                tot += sa
+            res = tot if tot is not None and tot <= _REMAT_MAX else None
+        remat_memo[nd] = res
+        return res
+
+    W = _RegFile(ir.NW, "W")
+    B = _RegFile(ir.NB, "B")
+
+    def rank(t):
+        def f(nd):
+            sz = remat_size(nd)
+            if sz is None:
+                return None
+            # cheapest restore first, then farthest next use (Belady)
+            return (sz, -next_use(nd, t))
+        return f
+
+    def regfile(nd):
+        return B if dag.nodes[nd].is_bool else W
+
+    def emit_node(i: int, t: int, pinned_w: set, pinned_b: set) -> int:
+        n = dag.nodes[i]
+        rf = regfile(i)
+        if n.kind in _LEAF_KINDS:
+            r = rf.alloc(i, rank(t), pinned_b if n.is_bool else pinned_w)
+            if n.kind == K_VAR:
+                prog.emit(ir.W_VAR, n.width, dst=r, aux0=n.aux)
+            elif n.kind == K_CONST:
+                prog.emit(ir.W_CONST, n.width, dst=r, aux0=prog.const_index(n.aux))
+            elif n.kind == K_BCONST:
+                prog.emit(ir.B_CONST, 1, dst=r, aux0=n.aux)
+            else:
+                prog.emit(ir.B_VAR, 1, dst=r, aux0=n.aux)
+            return r
+        pw, pb = set(pinned_w), set(pinned_b)
+        regs = []
+        for a in n.args:
+            r = materialize(a, t, pw, pb)
+            (pb if dag.nodes[a].is_bool else pw).add(r)
+            regs.append(r)
+        # operands whose last use is this node may be reused as destination
+        for a in set(n.args):
+            if next_use(a, t) >= (1 << 30):
+                regfile(a).release(a)
+                (pb if dag.nodes[a].is_bool else pw).discard(regs[n.args.index(a)])
+        dst = rf.alloc(i, rank(t), pb if n.is_bool else pw)
+        op = n.kind
+        if op in (ir.W_ITE, ir.B_ITE):      # args: cond(B), then, else
+            prog.emit(op, n.width if op == ir.W_ITE else 1, dst=dst, a=regs[1], b=regs[2], c=regs[0])
+        else:
+            a = regs[0] if len(regs) > 0 else 0
+            b = regs[1] if len(regs) > 1 else 0
+            prog.emit(op, n.width, dst=dst, a=a, b=b, aux0=n.aux)
+        return dst
+
+    def materialize(nd: int, t: int, pinned_w: set, pinned_b: set) -> int:
+        rf = regfile(nd)
+        if nd in rf.where:
+            return rf.where[nd]
+        if dag.nodes[nd].kind not in _LEAF_KINDS and remat_size(nd) is None:
+            raise LoweringError("non-rematerialisable value was evicted")
+        return emit_node(nd, t, pinned_w, pinned_b)
+
+    for t, (kind, i) in enumerate(events):
+        if kind == "assert":
+            rb = materialize(i, t, set(), set())
+            prog.emit(ir.ASSERT, 1, a=rb)
+            if next_use(i, t) >= (1 << 30):
+                B.release(i)
+            continue
+        if i in regfile(i).where:
+            continue  # already (re)computed as an operand of an earlier node
+        emit_node(i, t, set(), set())
+        if next_use(i, t) >= (1 << 30):
+            regfile(i).release(i)
+    prog.finish()
+    prog.validate()
+    return prog

@@ -1,0 +1,29 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (run on the GPU box)")
+
+
+@pytest.fixture(scope="session")
+def engine():
+    from mythril_amd.engine import get_engine
+
+    return get_engine(0)
+
+
+def load_golden(name):
+    import json
+
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)

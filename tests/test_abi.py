@@ -1,0 +1,59 @@
+"""CPU: the C ABI and its Python mirror agree; the library loads and exports every symbol."""
+
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from mythril_amd import _lib, ir
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _header_enum():
+    src = open(os.path.join(ROOT, "include", "pf_bytecode.h")).read()
+    return {m.group(1): int(m.group(2)) for m in re.finditer(r"\bPF_([A-Z0-9_]+)\s*=\s*(\d+)", src)}
+
+
+def test_opcodes_match_header():
+    h = _header_enum()
+    for name, val in h.items():
+        if name in ("NUM_OPCODES",) or name.startswith("VK_"):
+            continue
+        assert getattr(ir, name) == val, name
+    for k in ("GENERIC", "ACTOR", "KECCAK", "SMALL", "BOOL"):
+        assert getattr(ir, "VK_" + k) == h["VK_" + k]
+
+
+def test_register_counts_match_header():
+    src = open(os.path.join(ROOT, "include", "pf_bytecode.h")).read()
+    assert int(re.search(r"#define PF_NW (\d+)", src).group(1)) == ir.NW
+    assert int(re.search(r"#define PF_NB (\d+)", src).group(1)) == ir.NB
+
+
+def _declared_symbols():
+    src = open(os.path.join(ROOT, "include", "pathfeas.h")).read()
+    return set(re.findall(r"^\s*(?:int|const char\*)\s+(pf_[a-z0-9_]+)\(", src, re.M))
+
+
+def test_ctypes_table_covers_header():
+    assert _declared_symbols() == set(_lib.SIGNATURES)
+
+
+def test_library_loads_and_exports():
+    if not os.path.exists(_lib.LIB_PATH):
+        from mythril_amd.build import build_library
+        build_library()
+    L = _lib.load_library()
+    for name in _declared_symbols():
+        assert hasattr(L, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
+                         text=True).stdout
+    for name in _declared_symbols():
+        assert re.search(rf"\bT {name}\b", out), name
+
+
+def test_set_desc_layout():
+    assert ctypes.sizeof(_lib.pf_stats) == 40

@@ -1,0 +1,185 @@
+"""GPU parity: the gfx950 kernels against the oracle (oracle/pyoracle.py), bit-exact.
+
+Every check goes through the C ABI (libpathfeas.so via ctypes).  Integer/byte work: the bar
+is bit-exact equality, no tolerance.
+"""
+
+import numpy as np
+import pyoracle as O
+import pytest
+from conftest import load_golden
+
+import evm_to_ir
+from mythril_amd import ir, synth
+from mythril_amd.lower import Dag, lower
+
+pytestmark = pytest.mark.gpu
+
+_OPS = {
+    "add": ir.W_ADD, "sub": ir.W_SUB, "mul": ir.W_MUL, "udiv": ir.W_UDIV, "urem": ir.W_UREM,
+    "sdiv": ir.W_SDIV, "srem": ir.W_SREM, "smod": ir.W_SMOD, "shl": ir.W_SHL,
+    "lshr": ir.W_LSHR, "ashr": ir.W_ASHR, "exp": ir.W_EXP,
+}
+_CMPS = {"ult": ir.B_ULT, "ule": ir.B_ULE, "slt": ir.B_SLT, "sle": ir.B_SLE,
+         "uadd_noovf": ir.B_UADD_NOOVF, "umul_noovf": ir.B_UMUL_NOOVF}
+
+
+def _op_program(name, w):
+    """vars a, b, e (width w or 1): assert op(a, b) == e."""
+    dag = Dag()
+    a, b = dag.var("a", w), dag.var("b", w)
+    if name in _OPS:
+        e = dag.var("e", w)
+        r = dag.op(_OPS[name], w, a, b)
+        dag.assert_(dag.op(ir.B_EQ, w, r, e))
+    else:
+        e = dag.var("e", 1, ir.VK_BOOL)
+        r = dag.op(_CMPS[name], w, a, b)
+        dag.assert_(dag.op(ir.B_NOT, 1, dag.op(ir.B_XOR, 1, r, e)))
+    return lower(dag)
+
+
+def test_ops_golden_vectors(engine):
+    vecs = load_golden("ops.json")
+    groups = {}
+    for v in vecs:
+        groups.setdefault((v["op"], v["w"]), []).append(v)
+    progs, keys = [], []
+    for (name, w) in sorted(groups):
+        progs.append(_op_program(name, w))
+        keys.append((name, w))
+    db = engine.upload(progs)
+    for s, key in enumerate(keys):
+        rows = groups[key]
+        cands = []
+        for v in rows:
+            r = v["r"] if isinstance(v["r"], int) else int(v["r"], 16)
+            cands.append([int(v["a"], 16), int(v["b"], 16), r])
+            # a corrupted expectation must evaluate to false
+            cands.append([int(v["a"], 16), int(v["b"], 16), (r ^ 1) & ir.mask(key[1] if key[0] in _OPS else 1)])
+        soa = ir.pack_assignments(progs[s], cands)
+        got = engine.eval_assignments(db, s, soa)
+        want = np.array([i % 2 == 0 for i in range(len(cands))])
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, (key, [cands[i] for i in bad[:4]])
+
+
+def test_eip145_shifts(engine):
+    progs, cands = [], []
+    for case in load_golden("eip145.json"):
+        dag = Dag()
+        v, s = dag.var("v", 256), dag.var("s", 256)
+        op = {"shl": ir.W_SHL, "shr": ir.W_LSHR, "sar": ir.W_ASHR}[case["op"]]
+        dag.assert_(dag.op(ir.B_EQ, 256, dag.op(op, 256, v, s), dag.const(int(case["expected"], 16), 256)))
+        progs.append(lower(dag))
+        cands.append([int(case["value"], 16), int(case["shift"], 16)])
+    db = engine.upload(progs)
+    for i, p in enumerate(progs):
+        assert engine.eval_assignments(db, i, ir.pack_assignments(p, [cands[i]]))[0], i
+
+
+def test_vmtests_post_storage(engine):
+    progs, names = [], []
+    for c in load_golden("vmtests.json"):
+        try:
+            progs.append(lower(evm_to_ir.build(c["code"], c["storage"])))
+            names.append(c["name"])
+        except evm_to_ir.Unsupported:
+            pass
+    assert len(progs) >= 200
+    db = engine.upload(progs)
+    failed = [names[i] for i, p in enumerate(progs)
+              if not engine.eval_assignments(db, i, ir.pack_assignments(p, [[]]))[0]]
+    assert not failed, failed
+
+
+def _oracle_first(prog, budget, seed):
+    sv = O.SetView.from_batch(ir.Batch([prog]), 0)
+    first, _ = sv.check(budget, seed)
+    return first
+
+
+@pytest.mark.parametrize("flags", [0, ir.FLAG_EARLY_EXIT, ir.FLAG_EARLY_EXIT | ir.FLAG_SHORTCIRCUIT])
+def test_search_matches_oracle(engine, flags):
+    """Generated candidates: the smallest witness index equals the oracle's, per set."""
+    budget, seed = 512, 0x1234_5678_9ABC
+    progs = []
+    for i in range(10):
+        progs.append(synth.random_dag_set(100 + i, plant=False)[0])
+        progs.append(synth.random_dag_set(200 + i, plant=True)[0])
+    progs += [synth.mythril_like_set(i) for i in range(2)]
+    db = engine.upload(progs)
+    res = engine.check(db, budget=budget, seed=seed, flags=flags)
+    for i, p in enumerate(progs):
+        want = _oracle_first(p, budget, seed)
+        got = None if res.found[i] == 0xFFFFFFFF else int(res.found[i])
+        assert got == want, (i, p.name, got, want)
+    assert res.cands_decided > 0
+
+
+def test_planted_witness_found_at_candidate_zero(engine):
+    progs = [synth.random_dag_set(300 + i, plant=True)[0] for i in range(16)]
+    db = engine.upload(progs)
+    res = engine.check(db, budget=4096, seed=99, flags=ir.FLAG_EARLY_EXIT)
+    assert (res.found == 0).all()
+
+
+def test_materialize_matches_generator(engine):
+    progs = [synth.random_dag_set(400 + i, plant=(i % 2 == 0))[0] for i in range(6)]
+    progs.append(synth.mythril_like_set(5))
+    db = engine.upload(progs)
+    seed = 0xDEAD_BEEF_0001
+    sets, cands = [], []
+    for s in range(len(progs)):
+        for c in (0, 1, 7, 63, 64, 1000, 65535):
+            sets.append(s)
+            cands.append(c)
+    vals = engine.materialize(db, sets, cands, seed=seed)
+    b = ir.Batch(progs)
+    for k, (s, c) in enumerate(zip(sets, cands)):
+        sv = O.SetView.from_batch(b, s)
+        assert vals[k] == sv.gen_assignments(np.array([c], dtype=np.uint64), seed)[0], (s, c)
+
+
+def test_witness_rechecks_on_oracle(engine):
+    """The model handed back for a GPU witness satisfies the set under the oracle."""
+    progs = [synth.random_dag_set(500 + i, plant=False)[0] for i in range(12)]
+    db = engine.upload(progs)
+    seed = 7
+    res = engine.check(db, budget=8192, seed=seed, flags=ir.FLAG_EARLY_EXIT | ir.FLAG_SHORTCIRCUIT)
+    sat = [i for i in range(len(progs)) if res.found[i] != 0xFFFFFFFF]
+    assert sat, "no generated witness at all"
+    vals = engine.materialize(db, sat, [int(res.found[i]) for i in sat], seed=seed)
+    b = ir.Batch(progs)
+    for k, s in enumerate(sat):
+        assert O.SetView.from_batch(b, s).evaluate(vals[k])
+
+
+def test_keccak_vmsha3_and_random(engine):
+    msgs = [bytes(c["size"]) for c in load_golden("vmsha3.json")]
+    want = [c["digest"].lower() for c in load_golden("vmsha3.json")]
+    got = engine.keccak256(msgs)
+    assert ["0x" + g.hex() for g in got] == want
+    rng = np.random.default_rng(3)
+    msgs = [rng.bytes(n) for n in list(range(0, 300)) + [64] * 50 + [1000, 4096]]
+    got = engine.keccak256(msgs)
+    for m, g in zip(msgs, got):
+        assert g == O.keccak256(m)
+
+
+def test_keccak_fixed_dev_matches(engine):
+    torch = pytest.importorskip("torch")
+    from mythril_amd import _lib
+    import ctypes
+    n, ln = 4096, 64
+    host = np.random.default_rng(5).integers(0, 256, size=n * ln, dtype=np.uint8)
+    d_in = torch.from_numpy(host).to("cuda")
+    d_out = torch.zeros(n * 32, dtype=torch.uint8, device="cuda")
+    ms = ctypes.c_float(0)
+    stream = torch.cuda.current_stream().cuda_stream  # same stream as the tensors' producers
+    _lib.check(_lib.lib().pf_keccak256_fixed_dev(d_in.data_ptr(), ln, n, d_out.data_ptr(),
+                                                 ctypes.byref(ms), stream), "keccak fixed")
+    torch.cuda.synchronize()
+    out = d_out.cpu().numpy()
+    for i in range(0, n, 97):
+        assert out[32 * i:32 * i + 32].tobytes() == O.keccak256(host[ln * i:ln * i + ln].tobytes())
