@@ -61,6 +61,9 @@ enum pf_opcode {
     PF_W_CONCAT = 22, /* dst <- (a << aux0) | b   where aux0 = width(b)               */
     PF_W_SEXT = 23,   /* dst <- sign_extend(a) from aux0 bits to width                 */
     PF_W_ITE = 24,    /* dst <- B[c] ? a : b                                           */
+    PF_W_HASH = 25,   /* dst <- H_aux0(a): keyed 256-bit mix of a (two Philox4x32-10
+                         blocks, see below) — the by-construction interpretation of
+                         uninterpreted functions (keccak256_<n>, unknown UFs)          */
     /* B results */
     PF_B_CONST = 40,  /* dst <- aux0 & 1                                               */
     PF_B_VAR = 41,    /* dst <- candidate value of Bool variable aux0                  */
@@ -120,6 +123,12 @@ typedef struct pf_set_desc {
  * PF_VK_KECCAK: const[hint0] + ((r[0..3] & (2^117 - 1)) << 6).
  * PF_VK_SMALL: r[0] % (hint0 + 1).   PF_VK_BOOL: r[0] & 1.
  * All results are masked to the variable's width.                                  */
+/* PF_W_HASH with salt s of value x (limbs x0..x7):
+ *   h = Philox(ctr=(x0,x1,x2,x3), key=(s, 0x5BD1E995)),
+ *   g = Philox(ctr=(x4^h0, x5^h1, x6^h2, x7^h3), key=(s, 0x27D4EB2F)),
+ *   H = limbs (h0,h1,h2,h3,g0,g1,g2,g3) masked to width.                              */
+#define PF_HASH_K1A 0x5BD1E995u
+#define PF_HASH_K1B 0x27D4EB2Fu
 #define PF_PHILOX_M0 0xD2511F53u
 #define PF_PHILOX_M1 0xCD9E8D57u
 #define PF_PHILOX_W0 0x9E3779B9u

@@ -274,7 +274,8 @@ __constant__ uint8_t kOpTraffic[PF_NUM_OPCODES] = {
     /*NOT NEG*/ RA | WW, RA | WW,
     /*SHL LSHR ASHR EXP (17..20)*/ RA | RB | WW, RA | RB | WW, RA | RB | WW, RA | RB | WW,
     /*EXTRACT*/ RA | WW, /*CONCAT*/ RA | RB | WW, /*SEXT*/ RA | WW, /*ITE*/ RA | RB | WW,
-    /*25..39*/ 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+    /*HASH*/ RA | WW,
+    /*26..39*/ 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
     /*B_CONST B_VAR*/ 0, 0,
     /*EQ ULT ULE SLT SLE (42..46)*/ RA | RB, RA | RB, RA | RB, RA | RB, RA | RB,
     /*B_AND B_OR B_XOR B_NOT B_ITE (47..51)*/ 0, 0, 0, 0, 0,
@@ -384,6 +385,15 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
             }
             case PF_W_SEXT: z = sextw(x, I.z); break;
             case PF_W_ITE: z = pf::sel256(BGET(c), x, y); break;
+            case PF_W_HASH: {
+                const uint32_t salt = I.z;
+                uint4 h = philox(make_uint4(x.l[0], x.l[1], x.l[2], x.l[3]), salt, PF_HASH_K1A);
+                uint4 g = philox(make_uint4(x.l[4] ^ h.x, x.l[5] ^ h.y, x.l[6] ^ h.z, x.l[7] ^ h.w),
+                                 salt, PF_HASH_K1B);
+                z.l[0] = h.x; z.l[1] = h.y; z.l[2] = h.z; z.l[3] = h.w;
+                z.l[4] = g.x; z.l[5] = g.y; z.l[6] = g.z; z.l[7] = g.w;
+                break;
+            }
             case PF_B_CONST: bres = I.z & 1u; break;
             case PF_B_VAR:
                 if (MODE == MODE_GEN) {

@@ -48,6 +48,7 @@ W_EXTRACT = 21
 W_CONCAT = 22
 W_SEXT = 23
 W_ITE = 24
+W_HASH = 25
 B_CONST = 40
 B_VAR = 41
 B_EQ = 42
@@ -70,7 +71,7 @@ OPNAMES = {v: k for k, v in dict(globals()).items()
 # binary W -> W ops
 W_BINARY = (W_ADD, W_SUB, W_MUL, W_UDIV, W_UREM, W_SDIV, W_SREM, W_SMOD, W_AND, W_OR,
             W_XOR, W_SHL, W_LSHR, W_ASHR, W_EXP)
-W_UNARY = (W_NOT, W_NEG, W_MOV)
+W_UNARY = (W_NOT, W_NEG, W_MOV, W_HASH)
 B_CMP = (B_EQ, B_ULT, B_ULE, B_SLT, B_SLE, B_UADD_NOOVF, B_UMUL_NOOVF)
 B_LOGIC = (B_AND, B_OR, B_XOR)
 
@@ -91,7 +92,7 @@ FLAG_COUNT_OPS = 4
 # bookkeeping, not constraint arithmetic.  Width-generic ops scale by ceil(w/32)/8.
 _COST256 = {
     W_ADD: 8, W_SUB: 8, W_NOT: 8, W_AND: 8, W_OR: 8, W_XOR: 8, W_NEG: 8,
-    W_ITE: 8, W_EXTRACT: 8, W_CONCAT: 8, W_SEXT: 8,
+    W_ITE: 8, W_EXTRACT: 8, W_CONCAT: 8, W_SEXT: 8, W_HASH: 0,
     B_EQ: 8, B_ULT: 8, B_ULE: 8, B_SLT: 8, B_SLE: 8,
     W_SHL: 16, W_LSHR: 16, W_ASHR: 16,
     W_MUL: 72, B_UMUL_NOOVF: 72, B_UADD_NOOVF: 8,

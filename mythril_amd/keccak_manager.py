@@ -1,0 +1,131 @@
+"""Keccak hash modelling for the GPU path — mirror of KeccakFunctionManager
+(mythril/laser/ethereum/function_managers/keccak_function_manager.py:25-182).
+
+Same UF names (``keccak256_<n>``, ``keccak256_<n>-1``), interval constants and conditions,
+so the constraint sets it emits are the ones LASER emits.  Two things differ:
+* concrete hashes (``find_concrete_keccak``, :57-69) are computed by the batched Keccak-256
+  kernel (pf_keccak256_batch) instead of eth_hash;
+* every interval / concrete pair is registered in the UF registry that the lowering uses to
+  interpret ``keccak256_<n>`` by construction (mythril_amd/smt/to_dag.py).
+"""
+
+from __future__ import annotations
+
+from typing import Dict, List, Tuple
+
+from .smt import And, BitVec, Function, Or, ULE, ULT, URem, symbol_factory
+from .smt import Bool
+from .smt.to_dag import DEFAULT_REGISTRY, KeccakSpec, UFRegistry
+
+TOTAL_PARTS = 10 ** 40
+PART = (2 ** 256 - 1) // TOTAL_PARTS
+INTERVAL_DIFFERENCE = 10 ** 30
+EMPTY_KECCAK = 89477152217924674838424037953991966239322087453347756267410168184682657981552
+
+
+def keccak256_bytes(data: bytes) -> bytes:
+    from .engine import get_engine
+
+    return get_engine().keccak256([data])[0]
+
+
+class KeccakFunctionManager:
+    def __init__(self, registry: UFRegistry = DEFAULT_REGISTRY):
+        self.registry = registry
+        self.reset()
+
+    def reset(self):
+        self.store_function: Dict[int, Tuple[Function, Function]] = {}
+        self.interval_hook_for_size: Dict[int, int] = {}
+        self._index_counter = TOTAL_PARTS - 34534
+        self.hash_result_store: Dict[int, List[BitVec]] = {}
+        self.quick_inverse: Dict[BitVec, BitVec] = {}
+        self.concrete_hashes: Dict[BitVec, BitVec] = {}
+        self.symbolic_inputs: Dict[int, List[BitVec]] = {}
+        self.registry.keccak.clear()
+
+    @staticmethod
+    def find_concrete_keccak(data: BitVec) -> BitVec:
+        digest = keccak256_bytes(data.value.to_bytes(data.size() // 8, byteorder="big"))
+        return symbol_factory.BitVecVal(int.from_bytes(digest, "big"), 256)
+
+    def get_function(self, length: int) -> Tuple[Function, Function]:
+        try:
+            return self.store_function[length]
+        except KeyError:
+            func = Function(f"keccak256_{length}", [length], 256)
+            inverse = Function(f"keccak256_{length}-1", [256], length)
+            self.store_function[length] = (func, inverse)
+            self.hash_result_store[length] = []
+            return func, inverse
+
+    @staticmethod
+    def get_empty_keccak_hash() -> BitVec:
+        return symbol_factory.BitVecVal(EMPTY_KECCAK, 256)
+
+    def create_keccak(self, data: BitVec) -> BitVec:
+        length = data.size()
+        func, _ = self.get_function(length)
+        if data.symbolic is False:
+            concrete_hash = self.find_concrete_keccak(data)
+            self.concrete_hashes[data] = concrete_hash
+            self._spec(length).concrete[data.value] = concrete_hash.value
+            return concrete_hash
+        self.symbolic_inputs.setdefault(length, []).append(data)
+        self.hash_result_store[length].append(func(data))
+        self._interval(length)
+        return func(data)
+
+    def _spec(self, length: int) -> KeccakSpec:
+        # concrete hashes do not claim an interval (the reference assigns intervals only in
+        # _create_condition, i.e. for symbolic inputs): lo stays None until one does
+        spec = self.registry.keccak.get(length)
+        if spec is None:
+            spec = KeccakSpec(lo=None)
+            self.registry.keccak[length] = spec
+        return spec
+
+    def _interval(self, length: int) -> int:
+        try:
+            index = self.interval_hook_for_size[length]
+        except KeyError:
+            self.interval_hook_for_size[length] = self._index_counter
+            index = self._index_counter
+            self._index_counter -= INTERVAL_DIFFERENCE
+        spec = self._spec(length)
+        if spec.lo is None:
+            spec.lo = index * PART
+        return index
+
+    def create_conditions(self) -> Bool:
+        condition = symbol_factory.Bool(True)
+        for inputs_list in self.symbolic_inputs.values():
+            for symbolic_input in inputs_list:
+                condition = And(condition, self._create_condition(func_input=symbolic_input))
+        for concrete_input, concrete_hash in self.concrete_hashes.items():
+            func, inverse = self.get_function(concrete_input.size())
+            condition = And(condition, func(concrete_input) == concrete_hash,
+                            inverse(func(concrete_input)) == concrete_input)
+        return condition
+
+    def _create_condition(self, func_input: BitVec) -> Bool:
+        length = func_input.size()
+        func, inv = self.get_function(length)
+        index = self._interval(length)
+        lower_bound = index * PART
+        upper_bound = lower_bound + PART
+        cond = And(
+            inv(func(func_input)) == func_input,
+            ULE(symbol_factory.BitVecVal(lower_bound, 256), func(func_input)),
+            ULT(func(func_input), symbol_factory.BitVecVal(upper_bound, 256)),
+            URem(func(func_input), symbol_factory.BitVecVal(64, 256)) == 0,
+        )
+        concrete_cond = symbol_factory.Bool(False)
+        for key, keccak in self.concrete_hashes.items():
+            if key.size() == func_input.size():
+                hash_eq = And(func(func_input) == keccak, key == func_input)
+                concrete_cond = Or(concrete_cond, hash_eq)
+        return And(inv(func(func_input)) == func_input, Or(cond, concrete_cond))
+
+
+keccak_function_manager = KeccakFunctionManager()

@@ -47,8 +47,15 @@ class Dag:
     nodes: List[Node] = field(default_factory=list)
     roots: List[int] = field(default_factory=list)
     vars: List[Var] = field(default_factory=list)
+    forced: List[int] = field(default_factory=list)  # constants pinned at pool index 0..
     _memo: Dict[tuple, int] = field(default_factory=dict)
     _var_index: Dict[str, int] = field(default_factory=dict)
+
+    def force_consts(self, values) -> int:
+        """Pin constants at known pool indices (schema hints refer to them)."""
+        start = len(self.forced)
+        self.forced.extend(int(v) & ir.mask(ir.MAX_WIDTH) for v in values)
+        return start
 
     def add(self, kind, width, args=(), aux=0, is_bool=False) -> int:
         key = (kind, width, tuple(args), aux, is_bool)
@@ -67,7 +74,7 @@ class Dag:
             idx = len(self.vars)
             self.vars.append(Var(name, width, kind, hint0, hint1, parent))
             self._var_index[name] = idx
-        if width == 0 or kind == ir.VK_BOOL:
+        if kind == ir.VK_BOOL:
             return self.add(K_BVAR, 1, (), idx, True)
         return self.add(K_VAR, width, (), idx)
 
@@ -157,6 +164,7 @@ _REMAT_OPCOST = 16  # only cheap ops (compare/ite/logic/extract/concat) are reco
 
 def lower(dag: Dag, seed: int = 0, name: str = "") -> Program:
     prog = Program(vars=list(dag.vars), seed=seed, name=name)
+    prog.consts.extend(dag.forced)  # schema hints index these (actor tables, keccak bases)
     events = _emission_order(dag)
     uses: Dict[int, List[int]] = {}
     for t, (kind, i) in enumerate(events):

@@ -1,0 +1,209 @@
+"""Host-side term evaluation under a GPU witness — the ``Model.eval`` of this engine.
+
+The reference's callers evaluate expressions with ``model.eval(expr, model_completion=True)``
+(mythril/laser/smt/model.py:45-59; e.g. analysis/solver.py:185-214 concretises calldata,
+callvalue and caller).  A witness found on the GPU is a (set, candidate) index; after
+``pf_materialize`` returns the candidate's variable values, this module evaluates any term
+under exactly the interpretation the kernel used (same arrays rule, same keccak/UF
+interpretation, PF_W_HASH restated below), so host and device agree bit for bit.
+"""
+
+from __future__ import annotations
+
+import re
+from typing import Dict, List, Optional, Tuple
+
+from . import terms as T
+from .to_dag import KECCAK_MASK_BITS, Lowered, UFRegistry, salt_of
+
+_KECCAK_RE = re.compile(r"^keccak256_(\d+)(-1)?$")
+_M32 = 0xFFFFFFFF
+
+
+def _philox(c, k0, k1):
+    c0, c1, c2, c3 = c
+    for _ in range(10):
+        p0 = 0xD2511F53 * c0
+        p1 = 0xCD9E8D57 * c2
+        c0, c1, c2, c3 = ((p1 >> 32) ^ c1 ^ k0) & _M32, p1 & _M32, ((p0 >> 32) ^ c3 ^ k1) & _M32, p0 & _M32
+        k0 = (k0 + 0x9E3779B9) & _M32
+        k1 = (k1 + 0xBB67AE85) & _M32
+    return c0, c1, c2, c3
+
+
+def uf_hash(x: int, salt: int) -> int:
+    """PF_W_HASH (include/pf_bytecode.h)."""
+    xs = [(x >> (32 * i)) & _M32 for i in range(8)]
+    h = _philox(tuple(xs[:4]), salt, 0x5BD1E995)
+    g = _philox(tuple(xs[4 + i] ^ h[i] for i in range(4)), salt, 0x27D4EB2F)
+    return sum(v << (32 * i) for i, v in enumerate(h + g))
+
+
+def _sgn(x, w):
+    return x - (1 << w) if x >> (w - 1) else x
+
+
+def _chunks(v: int, w: int) -> List[int]:
+    out = []
+    while w > 0:
+        out.append(v & T.M(min(w, 256)))
+        v >>= 256
+        w -= 256
+    return out
+
+
+class Witness:
+    """One satisfying assignment plus the interpretation state to evaluate any term."""
+
+    def __init__(self, lowered: Lowered, values: List[int], registry: UFRegistry):
+        self.reg = registry
+        self.vars: Dict[str, int] = {}
+        self.bools: Dict[str, bool] = {}
+        self.reads: Dict[T.Term, int] = {}      # select / inverse-app terms -> their own var value
+        for term, val in zip(lowered.var_terms, values):
+            if term.op == "var":
+                self.vars[term.val] = val
+            elif term.op == "bvar":
+                self.bools[term.val] = bool(val & 1)
+            else:
+                self.reads[term] = val
+        self.array_reads = lowered.array_reads
+        self.uf_apps = lowered.uf_apps
+        self._memo: Dict[T.Term, object] = {}
+        self._tables: Optional[Dict[str, Dict[int, int]]] = None
+        self._keccak_tables: Dict[int, List[Tuple[int, int]]] = {}
+
+    # ---- array interpretation: first earlier index with an equal value ------------------
+    def tables(self) -> Dict[str, Dict[int, int]]:
+        if self._tables is None:
+            self._tables = {}
+            for name, reads in self.array_reads.items():
+                tab: Dict[int, int] = {}
+                for it, sel in reads:
+                    iv = self.ev(it)
+                    if iv not in tab:
+                        tab[iv] = self.reads.get(sel, 0)
+                self._tables[name] = tab
+        return self._tables
+
+    def _select(self, arr: T.Term, iv: int) -> int:
+        if arr.op == "store":
+            if self.ev(arr.args[1]) == iv:
+                return self.ev(arr.args[2])
+            return self._select(arr.args[0], iv)
+        if arr.op == "K":
+            return self.ev(arr.args[0])
+        if arr.op == "ite":
+            return self._select(arr.args[1] if self.ev(arr.args[0]) else arr.args[2], iv)
+        if arr.op == "array":
+            return self.tables().get(arr.val, {}).get(iv, 0)  # model completion: 0
+        raise ValueError(f"select over {arr.op}")
+
+    # ---- UFs ----------------------------------------------------------------------------
+    def _keccak(self, n: int, x: int) -> int:
+        spec = self.reg.keccak_for(n)
+        if spec is not None and x in spec.concrete:
+            return spec.concrete[x]
+        h = None
+        for c in _chunks(x, n):
+            h = uf_hash(c if h is None else h ^ c, salt_of(f"keccak256_{n}"))
+        if spec is None or spec.lo is None:
+            return h
+        return (spec.base + ((h & T.M(KECCAK_MASK_BITS)) << 6)) & T.M(256)
+
+    def _keccak_inv(self, n: int, y: int, term: T.Term) -> int:
+        # same lookup order as the lowering: f-applications lowered before this inverse
+        # application first, then earlier inverse applications that own a variable
+        before = []
+        for (fname, args, app) in self.uf_apps:
+            if app is term:
+                break
+            before.append((fname, args, app))
+        for (fname, args, app) in before:
+            if fname == f"keccak256_{n}":
+                x = self.ev(args[0])
+                if self._keccak(n, x) == y:
+                    return x
+        for (fname, args, app) in before:
+            if fname == f"keccak256_{n}-1" and app in self.reads and self.ev(args[0]) == y:
+                return self.reads[app]
+        return self.reads.get(term, 0)
+
+    def _apply(self, t: T.Term) -> int:
+        fname = t.val[0]
+        m = _KECCAK_RE.match(fname)
+        if m:
+            n = int(m.group(1))
+            a = t.args[0]
+            if m.group(2) is not None and a.op == "apply" and a.val[0] == f"keccak256_{n}":
+                return self.ev(a.args[0])  # inv(f(x)) = x, as substituted by the lowering
+            x = self.ev(a)
+            return self._keccak(n, x) if m.group(2) is None else self._keccak_inv(n, x, t)
+        if fname == "Power" and len(t.args) == 2:
+            return pow(self.ev(t.args[0]), self.ev(t.args[1]), 1 << 256)
+        h = None
+        for a in t.args:
+            for c in _chunks(self.ev(a), a.width):
+                h = uf_hash(c if h is None else h ^ c, salt_of(fname))
+        return h & T.M(t.width)
+
+    # ---- evaluator ------------------------------------------------------------------------
+    def ev(self, t: T.Term):
+        r = self._memo.get(t)
+        if r is not None:
+            return r
+        r = self._ev(t)
+        self._memo[t] = r
+        return r
+
+    def _ev(self, t: T.Term):
+        op = t.op
+        if op == "bv":
+            return t.val
+        if op == "true":
+            return True
+        if op == "false":
+            return False
+        if op == "var":
+            return self.vars.get(t.val, 0)          # model completion: 0
+        if op == "bvar":
+            return self.bools.get(t.val, False)
+        w = t.width
+        if op in T._FOLD2:
+            return T._FOLD2[op](self.ev(t.args[0]), self.ev(t.args[1]), w)
+        if op in T._CMP:
+            a = t.args[0]
+            return bool(T._CMP[op](self.ev(a), self.ev(t.args[1]), a.width))
+        if op == "bvnot":
+            return ~self.ev(t.args[0]) & T.M(w)
+        if op == "bvneg":
+            return -self.ev(t.args[0]) & T.M(w)
+        if op == "extract":
+            hi, lo = t.val
+            return (self.ev(t.args[0]) >> lo) & T.M(hi - lo + 1)
+        if op == "concat":
+            v = 0
+            for a in t.args:
+                v = (v << a.width) | self.ev(a)
+            return v
+        if op == "zero_extend":
+            return self.ev(t.args[0])
+        if op == "ite":
+            return self.ev(t.args[1]) if self.ev(t.args[0]) else self.ev(t.args[2])
+        if op == "select":
+            return self._select(t.args[0], self.ev(t.args[1]))
+        if op == "apply":
+            return self._apply(t)
+        if op == "=":
+            return self.ev(t.args[0]) == self.ev(t.args[1])
+        if op == "iff":
+            return bool(self.ev(t.args[0])) == bool(self.ev(t.args[1]))
+        if op == "and":
+            return all(self.ev(a) for a in t.args)
+        if op == "or":
+            return any(self.ev(a) for a in t.args)
+        if op == "not":
+            return not self.ev(t.args[0])
+        if op == "xor":
+            return bool(self.ev(t.args[0])) != bool(self.ev(t.args[1]))
+        raise ValueError(f"cannot evaluate {op}")

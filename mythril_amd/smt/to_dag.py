@@ -1,0 +1,467 @@
+"""Constraint terms -> bytecode DAG (mythril_amd.lower.Dag), with arrays and UFs interpreted
+by construction.
+
+The conjunction handed to ``get_model`` (mythril/support/model.py:87-93) is lowered so that
+every GPU candidate *is* a complete model:
+
+* free BitVec/Bool symbols become candidate variables (schema kind from the LASER naming
+  scheme: ``sender_*`` -> actor set, ``*_calldatasize`` -> small sizes, see
+  mythril/laser/ethereum/transaction/symbolic.py:122-139, state/calldata.py:229-230);
+* ``select`` over ``store``/``K``/``ite`` chains is resolved structurally; a base array
+  becomes one variable per distinct index term, and a later index term reads the value of
+  the first earlier index that evaluates equal (``ite`` chain) — a total, consistent array
+  interpretation for every candidate (no Ackermann side constraints needed);
+* ``keccak256_<n>`` (keccak_function_manager.py:71-84) is interpreted as
+  ``c_i -> keccak(c_i)`` for the registered concrete hashes and
+  ``x -> lo_n + 64 * (H(x) mod 2^117)`` otherwise (H = PF_W_HASH), which satisfies the
+  interval / ``% 64`` / concrete-equality conditions of ``_create_condition`` (:150-179) by
+  construction; ``keccak256_<n>-1`` is substituted through ``inv(f(t)) = t`` and otherwise
+  looked up among the set's f-applications, with the injectivity of f on the set added as
+  side constraints (f(a) = f(b) -> a = b) so the interpretation stays a function;
+* ``Power`` (exponent_function_manager.py:29-68) is interpreted as real modular EXP;
+  any other UF as a keyed hash of its arguments.
+Values wider than 256 bits (keccak256_512 inputs, zero-padded ``==``, bitvec.py:16-22) are
+carried as 256-bit chunks.  Anything else raises LoweringError -> the query goes to z3.
+"""
+
+from __future__ import annotations
+
+import re
+import zlib
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+from .. import ir
+from ..lower import Dag, LoweringError
+from . import terms as T
+
+_KECCAK_RE = re.compile(r"^keccak256_(\d+)(-1)?$")
+
+ACTORS = (
+    0xAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFE,  # CREATOR  (transaction/symbolic.py:26-37)
+    0xDEADBEEFDEADBEEFDEADBEEFDEADBEEFDEADBEEF,  # ATTACKER
+    0xAAAAAAABBBBBBBBBCCCCCCCCCCCCCCCCCCCCCCCC,  # SOMEGUY
+)
+KECCAK_MASK_BITS = 117
+
+
+@dataclass
+class KeccakSpec:
+    lo: Optional[int]                         # interval start (keccak_function_manager.py:165);
+                                              # None while the width has only concrete hashes
+    concrete: Dict[int, int] = field(default_factory=dict)   # input value -> keccak
+
+    @property
+    def base(self) -> int:
+        """First multiple of 64 in the interval: base + 64*k stays inside [lo, lo + PART)
+        for k < 2^117 (PART = (2^256-1) // 10^40 > 2^123 + 64) and satisfies ``% 64 == 0``."""
+        return (self.lo + 63) & ~63
+
+
+class UFRegistry:
+    """Per-width keccak interpretation data, mirrored from the KeccakFunctionManager."""
+
+    def __init__(self):
+        self.keccak: Dict[int, KeccakSpec] = {}
+        self.actors: Tuple[int, ...] = ACTORS
+
+    def keccak_for(self, n: int) -> Optional[KeccakSpec]:
+        return self.keccak.get(n)
+
+
+DEFAULT_REGISTRY = UFRegistry()
+
+
+def salt_of(name: str) -> int:
+    return zlib.crc32(name.encode()) & 0xFFFFFFFF
+
+
+def var_kind(name: str, w: int):
+    """Candidate-generator kind for a LASER symbol name."""
+    if name.startswith("sender_") and w == 256:
+        return ir.VK_ACTOR
+    if name.endswith("_calldatasize"):
+        return ir.VK_SMALL
+    return ir.VK_GENERIC
+
+
+@dataclass
+class Lowered:
+    dag: Dag
+    var_terms: List[T.Term]                    # candidate variable i <-> term (var / select / apply)
+    uf_apps: List[Tuple[str, tuple, T.Term]]   # (name, arg terms, app term) for model tables
+    array_reads: Dict[str, List[Tuple[T.Term, T.Term]]]  # array -> (index, select term) in lookup order
+
+
+class TermLowering:
+    def __init__(self, registry: Optional[UFRegistry] = None, parent: Optional[dict] = None):
+        self.reg = registry or DEFAULT_REGISTRY
+        self.dag = Dag()
+        self.parent = parent or {}
+        self.memo: Dict[T.Term, object] = {}
+        self.var_terms: List[T.Term] = []
+        # base array name -> [(idx term, select term, idx node, value node)] in lookup order
+        self.arrays: Dict[str, List[Tuple[T.Term, T.Term, int, object]]] = {}
+        self.keccak_apps: Dict[int, List[Tuple[T.Term, object, object]]] = {}  # n -> [(arg term, arg val, f node)]
+        self.inv_apps: Dict[int, List[Tuple[object, object]]] = {}  # n -> [(key node, value node)]
+        self.uf_apps: List[Tuple[str, tuple, T.Term]] = []
+        self.side: List[int] = []
+        self._actor_consts: Optional[int] = None
+
+    # ---- leaves -----------------------------------------------------------------------
+    def _var(self, name: str, w: int, term: T.Term) -> int:
+        kind = var_kind(name, w)
+        hint0 = hint1 = 0
+        if kind == ir.VK_ACTOR:
+            hint0, hint1 = self._actor_table()
+        elif kind == ir.VK_SMALL:
+            hint0 = 4 + 32 * 8
+        before = len(self.dag.vars)
+        node = self.dag.var(name, w, kind, hint0, hint1, self.parent.get(name))
+        if len(self.dag.vars) > before:
+            self.var_terms.append(term)
+        return node
+
+    def _actor_table(self):
+        if self._actor_consts is None:
+            self._actor_consts = self.dag.force_consts(self.reg.actors)
+        return self._actor_consts, len(self.reg.actors)
+
+    # ---- generic lowering ---------------------------------------------------------------
+    def w(self, t: T.Term):
+        """Lower a BitVec term: a node (width <= 256) or a chunk list for wider values."""
+        r = self.memo.get(t)
+        if r is None:
+            r = self._lower_bv(t)
+            self.memo[t] = r
+        return r
+
+    def node(self, t: T.Term) -> int:
+        r = self.w(t)
+        if isinstance(r, list):
+            raise LoweringError(f"{t.width}-bit value used where <= 256 bits are required")
+        return r
+
+    def b(self, t: T.Term) -> int:
+        r = self.memo.get(t)
+        if r is None:
+            r = self._lower_bool(t)
+            self.memo[t] = r
+        return r
+
+    def chunks(self, t: T.Term) -> List[Tuple[int, int]]:
+        """Little-endian 256-bit-aligned chunks (node, width) of a value of any width."""
+        pieces = self._pieces(t)
+        out: List[Tuple[int, int]] = []
+        cur: List[Tuple[int, int]] = []   # pieces of the current chunk (LSB first)
+        fill = 0
+        for node, wd in pieces:
+            off = 0
+            while off < wd:
+                take = min(256 - fill, wd - off)
+                if off == 0 and take == wd:
+                    part = node
+                else:
+                    part = self.dag.op(ir.W_EXTRACT, take, node, aux=off)
+                cur.append((part, take))
+                fill += take
+                off += take
+                if fill == 256:
+                    out.append(self._join(cur))
+                    cur, fill = [], 0
+        if cur:
+            out.append(self._join(cur))
+        return out
+
+    def _join(self, cur):
+        # cur is LSB-first; concat high..low
+        node, wd = cur[-1]
+        for part, pw in reversed(cur[:-1]):
+            node = self.dag.op(ir.W_CONCAT, wd + pw, node, part, aux=pw)
+            wd += pw
+        return node, wd
+
+    def _pieces(self, t: T.Term) -> List[Tuple[int, int]]:
+        if t.width <= 256:
+            return [(self.node(t), t.width)]
+        if t.op == "concat":
+            out = []
+            for p in reversed(t.args):
+                out.extend(self._pieces(p))
+            return out
+        if t.op == "zero_extend":
+            out = self._pieces(t.args[0])
+            rest = t.val
+            while rest > 0:
+                k = min(rest, 256)
+                out.append((self.dag.const(0, k), k))
+                rest -= k
+            return out
+        if t.op == "bv":
+            out, v, rest = [], t.val, t.width
+            while rest > 0:
+                k = min(rest, 256)
+                out.append((self.dag.const(v & ir.mask(k), k), k))
+                v >>= k
+                rest -= k
+            return out
+        r = self.w(t)
+        if isinstance(r, list):
+            return r
+        raise LoweringError(f"wide op {t.op}")
+
+    def _lower_bv(self, t: T.Term):
+        op, wd = t.op, t.width
+        if wd > 256:
+            if op in ("concat", "zero_extend", "bv"):
+                return self.chunks(t)
+            if op == "apply":
+                return self._apply(t)
+            if op == "ite":
+                c = self.b(t.args[0])
+                a, b = self.chunks(t.args[1]), self.chunks(t.args[2])
+                return [(self.dag.op(ir.W_ITE, x[1], c, x[0], y[0]), x[1]) for x, y in zip(a, b)]
+            raise LoweringError(f"{wd}-bit {op}")
+        if op == "bv":
+            return self.dag.const(t.val, wd)
+        if op == "var":
+            return self._var(t.val, wd, t)
+        if op in _WBIN:
+            return self.dag.op(_WBIN[op], wd, self.node(t.args[0]), self.node(t.args[1]))
+        if op == "bvnot":
+            return self.dag.op(ir.W_NOT, wd, self.node(t.args[0]))
+        if op == "bvneg":
+            return self.dag.op(ir.W_NEG, wd, self.node(t.args[0]))
+        if op == "extract":
+            hi, lo = t.val
+            src = t.args[0]
+            if src.width <= 256:
+                return self.dag.op(ir.W_EXTRACT, wd, self.node(src), aux=lo)
+            for (base, cwid), cnode in self._chunk_offsets(src):
+                if base <= lo and hi < base + cwid:
+                    return self.dag.op(ir.W_EXTRACT, wd, cnode, aux=lo - base)
+            raise LoweringError("extract across a 256-bit chunk boundary")
+        if op == "concat":
+            parts = t.args
+            node, acc = self.node(parts[0]), parts[0].width
+            for p in parts[1:]:
+                node = self.dag.op(ir.W_CONCAT, acc + p.width, node, self.node(p), aux=p.width)
+                acc += p.width
+            return node
+        if op == "zero_extend":
+            return self.dag.op(ir.W_MOV, wd, self.node(t.args[0]))
+        if op == "ite":
+            return self.dag.op(ir.W_ITE, wd, self.b(t.args[0]), self.node(t.args[1]), self.node(t.args[2]))
+        if op == "select":
+            return self._select(t.args[0], t.args[1], t)
+        if op == "apply":
+            return self._apply(t)
+        raise LoweringError(f"unsupported bit-vector op {op}")
+
+    def _chunk_offsets(self, t):
+        off = 0
+        for node, cw in self.chunks(t):
+            yield (off, cw), node
+            off += cw
+
+    def _lower_bool(self, t: T.Term) -> int:
+        op = t.op
+        d = self.dag
+        if op == "true":
+            return d.bconst(True)
+        if op == "false":
+            return d.bconst(False)
+        if op == "bvar":
+            return self._bvar(t)
+        if op == "not":
+            return d.op(ir.B_NOT, 1, self.b(t.args[0]))
+        if op in ("and", "or"):
+            opc = ir.B_AND if op == "and" else ir.B_OR
+            acc = self.b(t.args[0])
+            for a in t.args[1:]:
+                acc = d.op(opc, 1, acc, self.b(a))
+            return acc
+        if op == "xor":
+            return d.op(ir.B_XOR, 1, self.b(t.args[0]), self.b(t.args[1]))
+        if op == "iff":
+            return d.op(ir.B_NOT, 1, d.op(ir.B_XOR, 1, self.b(t.args[0]), self.b(t.args[1])))
+        if op == "ite":
+            return d.op(ir.B_ITE, 1, self.b(t.args[0]), self.b(t.args[1]), self.b(t.args[2]))
+        if op == "=":
+            a, b = t.args
+            if a.width > 256 or b.width > 256:
+                ca, cb = self.chunks(a), self.chunks(b)
+                acc = None
+                for (x, wx), (y, wy) in zip(ca, cb):
+                    e = d.op(ir.B_EQ, wx, x, y)
+                    acc = e if acc is None else d.op(ir.B_AND, 1, acc, e)
+                return acc
+            return d.op(ir.B_EQ, a.width, self.node(a), self.node(b))
+        if op in _BCMP:
+            a, b = t.args
+            return d.op(_BCMP[op], a.width, self.node(a), self.node(b))
+        raise LoweringError(f"unsupported bool op {op}")
+
+    def _bvar(self, t: T.Term) -> int:
+        before = len(self.dag.vars)
+        node = self.dag.var(t.val, 1, ir.VK_BOOL, parent=self.parent.get(t.val))
+        if len(self.dag.vars) > before:
+            self.var_terms.append(t)
+        return node
+
+    # ---- arrays ---------------------------------------------------------------------------
+    def _select(self, arr: T.Term, idx: T.Term, term: T.Term) -> int:
+        d = self.dag
+        if arr.op == "store":
+            base, k, v = arr.args
+            if k is idx:
+                return self.node(v)
+            if k.op == "bv" and idx.op == "bv":
+                return self._select(base, idx, term) if k.val != idx.val else self.node(v)
+            rest = self._select(base, idx, T.select(base, idx))
+            c = d.op(ir.B_EQ, idx.width, self.node(idx), self.node(k))
+            return d.op(ir.W_ITE, arr.sort[2], c, self.node(v), rest)
+        if arr.op == "K":
+            return self.node(arr.args[0])
+        if arr.op == "ite":
+            c = self.b(arr.args[0])
+            a = self._select(arr.args[1], idx, T.select(arr.args[1], idx))
+            b = self._select(arr.args[2], idx, T.select(arr.args[2], idx))
+            return d.op(ir.W_ITE, arr.sort[2], c, a, b)
+        if arr.op != "array":
+            raise LoweringError(f"select over {arr.op}")
+        name, rng = arr.val, arr.sort[2]
+        if idx.width > 256:
+            raise LoweringError("array index wider than 256 bits")
+        entries = self.arrays.setdefault(name, [])
+        for (it, _, _, val) in entries:
+            if it is idx:
+                return val
+        inode = self.node(idx)
+        if idx.op == "bv":
+            vname = f"{name}[{idx.val}]"
+        else:
+            vname = f"{name}@{len(entries)}"
+        sel_term = T.select(arr, idx)
+        val = self._var(vname, rng, sel_term)
+        # first earlier index with an equal value wins (consistent array interpretation)
+        for (it, _, inn, v) in reversed(entries):
+            if it.op == "bv" and idx.op == "bv":
+                continue  # distinct constants never alias
+            val = d.op(ir.W_ITE, rng, d.op(ir.B_EQ, idx.width, inode, inn), v, val)
+        entries.append((idx, sel_term, inode, val))
+        return val
+
+    # ---- uninterpreted functions --------------------------------------------------------
+    def _hash_args(self, args, salt) -> int:
+        d = self.dag
+        h = None
+        for a in args:
+            for node, wd in self.chunks(a):
+                x = node if wd == 256 else d.op(ir.W_MOV, 256, node)
+                h = d.op(ir.W_HASH, 256, x if h is None else d.op(ir.W_XOR, 256, h, x), aux=salt)
+        return h
+
+    def _apply(self, t: T.Term):
+        d = self.dag
+        fname, _ = t.val
+        args = t.args
+        m = _KECCAK_RE.match(fname)
+        if m:
+            n = int(m.group(1))
+            if m.group(2) is None:
+                return self._keccak(n, args[0], t)
+            return self._keccak_inv(n, args[0], t)
+        self.uf_apps.append((fname, args, t))
+        if fname == "Power" and len(args) == 2:
+            return d.op(ir.W_EXP, 256, self.node(args[0]), self.node(args[1]))
+        h = self._hash_args(args, salt_of(fname))
+        return h if t.width == 256 else d.op(ir.W_EXTRACT, t.width, h, aux=0)
+
+    def _keccak(self, n: int, arg: T.Term, t: T.Term) -> int:
+        d = self.dag
+        apps = self.keccak_apps.setdefault(n, [])
+        for (a, _, node) in apps:
+            if a is arg:
+                return node
+        spec = self.reg.keccak_for(n)
+        h = self._hash_args([arg], salt_of(f"keccak256_{n}"))
+        if spec is not None:
+            if spec.lo is not None:
+                k = d.op(ir.W_AND, 256, h, d.const(ir.mask(KECCAK_MASK_BITS), 256))
+                val = d.op(ir.W_ADD, 256, d.const(spec.base, 256),
+                           d.op(ir.W_SHL, 256, k, d.const(6, 256)))
+            else:
+                val = h
+            for c, kv in spec.concrete.items():
+                eqs = self._eq_value(arg, c)
+                if eqs is not None:
+                    val = d.op(ir.W_ITE, 256, eqs, d.const(kv, 256), val)
+        else:
+            val = h
+        # injectivity on the set: f(a) = f(b) -> a = b
+        for (a, _, node) in apps:
+            same_f = d.op(ir.B_EQ, 256, val, node)
+            same_x = self._eq_terms(arg, a)
+            self.side.append(d.op(ir.B_OR, 1, d.op(ir.B_NOT, 1, same_f), same_x))
+        apps.append((arg, None, val))
+        self.uf_apps.append((f"keccak256_{n}", (arg,), t))  # registration order = lookup order
+        return val
+
+    def _keccak_inv(self, n: int, y: T.Term, t: T.Term):
+        d = self.dag
+        if y.op == "apply" and y.val[0] == f"keccak256_{n}":
+            self.w(y)  # make sure f(x) is registered (injectivity constraints)
+            return self.w(y.args[0])
+        if n > 256:
+            raise LoweringError("inverse keccak of a wide input on a non-application")
+        ynode = self.node(y)
+        val = self._var(f"keccak256_{n}-1@{len(self.inv_apps.get(n, []))}", n, t)
+        entries = self.inv_apps.setdefault(n, [])
+        for (knode, vnode) in reversed(entries):
+            val = d.op(ir.W_ITE, n, d.op(ir.B_EQ, 256, ynode, knode), vnode, val)
+        for (a, _, fnode) in reversed(self.keccak_apps.get(n, [])):
+            val = d.op(ir.W_ITE, n, d.op(ir.B_EQ, 256, ynode, fnode), self.node(a), val)
+        entries.append((ynode, val))
+        self.uf_apps.append((f"keccak256_{n}-1", (y,), t))
+        return val
+
+    def _eq_value(self, t: T.Term, c: int) -> Optional[int]:
+        return self._eq_terms(t, T.const(c, t.width))
+
+    def _eq_terms(self, a: T.Term, b: T.Term) -> int:
+        d = self.dag
+        if a.width != b.width:
+            return d.bconst(False)
+        if a.width <= 256:
+            return d.op(ir.B_EQ, a.width, self.node(a), self.node(b))
+        acc = None
+        for (x, wx), (y, _) in zip(self.chunks(a), self.chunks(b)):
+            e = d.op(ir.B_EQ, wx, x, y)
+            acc = e if acc is None else d.op(ir.B_AND, 1, acc, e)
+        return acc
+
+    # ---- driver ---------------------------------------------------------------------------
+    def lower(self, constraints: List[T.Term]) -> Lowered:
+        for c in constraints:
+            if not c.is_bool:
+                raise LoweringError("constraint is not a Bool")
+            if c is T.TRUE:
+                continue
+            self.dag.assert_(self.b(c))
+        for s in self.side:
+            self.dag.assert_(s)
+        arrays = {k: [(it, st) for (it, st, _, _) in v] for k, v in self.arrays.items()}
+        return Lowered(self.dag, self.var_terms, self.uf_apps, arrays)
+
+
+_WBIN = {
+    "bvadd": ir.W_ADD, "bvsub": ir.W_SUB, "bvmul": ir.W_MUL, "bvudiv": ir.W_UDIV,
+    "bvurem": ir.W_UREM, "bvsdiv": ir.W_SDIV, "bvsrem": ir.W_SREM, "bvsmod": ir.W_SMOD,
+    "bvand": ir.W_AND, "bvor": ir.W_OR, "bvxor": ir.W_XOR, "bvshl": ir.W_SHL,
+    "bvlshr": ir.W_LSHR, "bvashr": ir.W_ASHR, "bvexp": ir.W_EXP,
+}
+_BCMP = {
+    "bvult": ir.B_ULT, "bvule": ir.B_ULE, "bvslt": ir.B_SLT, "bvsle": ir.B_SLE,
+    "bvuadd_noovfl": ir.B_UADD_NOOVF, "bvumul_noovfl": ir.B_UMUL_NOOVF,
+}

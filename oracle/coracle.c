@@ -243,6 +243,17 @@ static int eval_one(const SetV* S, const v256* values, uint32_t cand, uint64_t g
             case 22: W[d] = andv(orv(shlv(x, I[2]), y), M); break;
             case 23: W[d] = sext(x, I[2], w); break;
             case 24: W[d] = B[c & 31] ? x : y; break;
+            case 25: {
+                uint32_t xs[8], h[4], g[4];
+                for (int k = 0; k < 4; k++) { xs[2 * k] = (uint32_t)x.w[k]; xs[2 * k + 1] = (uint32_t)(x.w[k] >> 32); }
+                memcpy(h, xs, 16);
+                philox(h, I[2], 0x5BD1E995u);
+                for (int k = 0; k < 4; k++) g[k] = xs[4 + k] ^ h[k];
+                philox(g, I[2], 0x27D4EB2Fu);
+                uint32_t o[8] = {h[0], h[1], h[2], h[3], g[0], g[1], g[2], g[3]};
+                W[d] = andv(from32(o), M);
+                break;
+            }
             case 40: B[d] = I[2] & 1; break;
             case 41: B[d] = (uint8_t)((values ? values[I[2]] : gen(S, I[2], cand, gseed)).w[0] & 1); break;
             case 42: B[d] = eqv(x, y); break;

@@ -253,6 +253,15 @@ def philox4x32(ctr: Sequence[np.ndarray], key: Sequence[int]):
 VK_GENERIC, VK_ACTOR, VK_KECCAK, VK_SMALL, VK_BOOL = 0, 1, 2, 3, 4
 
 
+def uf_hash(x: int, salt: int) -> int:
+    """PF_W_HASH (include/pf_bytecode.h): keyed 256-bit mix of x (restated)."""
+    xs = [(x >> (32 * i)) & 0xFFFFFFFF for i in range(8)]
+    h = [int(v[0]) for v in philox4x32([[xs[0]], [xs[1]], [xs[2]], [xs[3]]], (salt, 0x5BD1E995))]
+    g = [int(v[0]) for v in philox4x32([[xs[4] ^ h[0]], [xs[5] ^ h[1]], [xs[6] ^ h[2]], [xs[7] ^ h[3]]],
+                                       (salt, 0x27D4EB2F))]
+    return sum(v << (32 * i) for i, v in enumerate(h + g))
+
+
 def _boundary(j: int, k: int, w: int) -> int:
     m = M(w)
     table = (0, 1, 2, 3, m, m - 1, 1 << (w - 1), (1 << (w - 1)) - 1,
@@ -322,7 +331,7 @@ def gen_values(cands: np.ndarray, var_index: int, schema: Sequence[int], consts:
 OP = dict(END=0, W_CONST=1, W_VAR=2, W_MOV=3, W_ADD=4, W_SUB=5, W_MUL=6, W_UDIV=7, W_UREM=8,
           W_SDIV=9, W_SREM=10, W_SMOD=11, W_AND=12, W_OR=13, W_XOR=14, W_NOT=15, W_NEG=16,
           W_SHL=17, W_LSHR=18, W_ASHR=19, W_EXP=20, W_EXTRACT=21, W_CONCAT=22, W_SEXT=23,
-          W_ITE=24, B_CONST=40, B_VAR=41, B_EQ=42, B_ULT=43, B_ULE=44, B_SLT=45, B_SLE=46,
+          W_ITE=24, W_HASH=25, B_CONST=40, B_VAR=41, B_EQ=42, B_ULT=43, B_ULE=44, B_SLT=45, B_SLE=46,
           B_AND=47, B_OR=48, B_XOR=49, B_NOT=50, B_ITE=51, B_UADD_NOOVF=52, B_UMUL_NOOVF=53,
           ASSERT=60)
 
@@ -403,6 +412,8 @@ class SetView:
                 W[d] = sign_extend(W[a], aux0, w)
             elif op == OP["W_ITE"]:
                 W[d] = W[a] if B[c] else W[b]
+            elif op == OP["W_HASH"]:
+                W[d] = uf_hash(W[a], aux0) & M(w)
             elif op == OP["B_CONST"]:
                 B[d] = bool(aux0 & 1)
             elif op == OP["B_VAR"]:

@@ -36,6 +36,8 @@ def eval_dag(dag, values):
             v = bool(values[n.aux] & 1)
         elif k in _W:
             v = _W[k](val[n.args[0]], val[n.args[1]], w)
+        elif k == ir.W_HASH:
+            v = O.uf_hash(val[n.args[0]], n.aux) & O.M(w)
         elif k == ir.W_NOT:
             v = O.bvnot(val[n.args[0]], w)
         elif k == ir.W_NEG:
@@ -66,3 +68,4 @@ def eval_dag(dag, values):
             raise ValueError(k)
         val[i] = v
     return all(val[r] for r in dag.roots)
+

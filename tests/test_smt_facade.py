@@ -1,0 +1,156 @@
+"""CPU: the mythril.laser.smt mirror — operator semantics, constant folding, lowering, and the
+host model evaluator agreeing with the bytecode (oracle) on random assignments."""
+
+import random
+
+import numpy as np
+import pyoracle as O
+import pytest
+
+from mythril_amd import ir
+from mythril_amd.lower import lower
+from mythril_amd.smt import (UGE, UGT, ULE, ULT, And, Array, BVAddNoOverflow, BVMulNoOverflow,
+                             BVSubNoUnderflow, Concat, Extract, Function, If, K, LShR, Not, Or,
+                             SRem, UDiv, URem, symbol_factory)
+from mythril_amd.smt import terms as T
+from mythril_amd.smt.interp import Witness, uf_hash
+from mythril_amd.smt.to_dag import KeccakSpec, TermLowering, UFRegistry
+
+BVV = symbol_factory.BitVecVal
+BV = symbol_factory.BitVecSym
+
+
+def test_signed_operators_match_reference_semantics():
+    # bitvec.py:138-180: < > <= >= are signed; / is sdiv; >> is ashr
+    a, b = BVV(-1, 256), BVV(1, 256)
+    assert (a < b).is_true and (b > a).is_true and (a <= b).is_true and (b >= a).is_true
+    assert ULT(b, a).is_true and UGT(a, b).is_true
+    assert (BVV(-7, 256) / BVV(2, 256)).value == (-3) % (1 << 256)
+    assert (BVV(-8, 256) >> BVV(1, 256)).value == (-4) % (1 << 256)
+    assert LShR(BVV(-8, 256), BVV(1, 256)).value == ((1 << 256) - 8) >> 1
+    assert UDiv(BVV(7, 256), BVV(0, 256)).value == (1 << 256) - 1
+    assert URem(BVV(7, 256), BVV(0, 256)).value == 7
+    assert SRem(BVV(-7, 256), BVV(2, 256)).value == (-1) % (1 << 256)
+
+
+def test_ule_uge_are_or_forms():
+    x, y = BV("x", 256), BV("y", 256)
+    assert ULE(x, y).raw.op == "or" and UGE(x, y).raw.op == "or"
+
+
+def test_padded_equality():
+    # bitvec.py:16-22: == between different widths zero-pads the narrower operand
+    a = Concat(BV("k", 256), BV("s", 256))
+    e = (a == BV("z", 256))
+    assert e.raw.args[1].op == "zero_extend" and e.raw.args[1].width == 512
+    assert (BVV(100, 8) == BVV(100, 16)).is_true
+
+
+def test_noovf_predicates_fold():
+    m = (1 << 256) - 1
+    assert BVAddNoOverflow(BVV(m, 256), BVV(1, 256), False).is_false
+    assert BVAddNoOverflow(BVV(m - 1, 256), BVV(1, 256), False).is_true
+    assert BVMulNoOverflow(BVV(1 << 128, 256), BVV(1 << 128, 256), False).is_false
+    assert BVSubNoUnderflow(BVV(3, 256), BVV(4, 256), False).is_false
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_constant_folding_matches_oracle(seed):
+    rng = random.Random(seed)
+    ops = [("bvadd", O.bvadd), ("bvsub", O.bvsub), ("bvmul", O.bvmul), ("bvudiv", O.bvudiv),
+           ("bvurem", O.bvurem), ("bvsdiv", O.bvsdiv), ("bvsrem", O.bvsrem), ("bvsmod", O.bvsmod),
+           ("bvshl", O.bvshl), ("bvlshr", O.bvlshr), ("bvashr", O.bvashr)]
+    for w in (8, 160, 256):
+        for _ in range(50):
+            a = rng.choice([0, 1, (1 << w) - 1, 1 << (w - 1), rng.getrandbits(w)])
+            b = rng.choice([0, 1, 3, w, (1 << w) - 1, rng.getrandbits(w)])
+            for name, fn in ops:
+                assert T.binop(name, T.const(a, w), T.const(b, w)).val == fn(a, b, w), (name, a, b, w)
+
+
+def _random_constraints(rng, registry):
+    x, y = BV("x", 256), BV("y", 256)
+    s = BV("sender_1", 256)
+    size = BV("1_calldatasize", 256)
+    b = symbol_factory.BoolSym("flag")
+    cd = Array("1_calldata", 256, 8)
+    st = K(256, 256, 0)
+    st[BVV(5, 256)] = x
+    st[y] = BVV(9, 256)
+    keccak = Function("keccak256_512", [512], 256)
+    inv = Function("keccak256_512-1", [256], 512)
+    power = Function("Power", [256, 256], 256)
+    other = Function("blockhash_x", [256], 256)
+    word = Concat([If(BVV(i, 256) < size, cd[BVV(i, 256)], BVV(0, 8)) for i in range(4, 8)])
+    key = Concat(x, y)
+    h = keccak(key)
+    cs = [
+        ULT(x, BVV(rng.getrandbits(256), 256)) if rng.random() < 0.5 else (x > y),
+        Or(s == BVV(0xDEADBEEFDEADBEEFDEADBEEFDEADBEEFDEADBEEF, 256), b),
+        UGE(st[y], BVV(rng.getrandbits(4), 256)),
+        Not(word == BVV(rng.getrandbits(32), 32)),
+        inv(h) == key,
+        ULE(BVV(registry.keccak[512].lo, 256), h),
+        URem(h, BVV(64, 256)) == 0,
+        cd[x] == cd[BVV(4, 256)],
+        Extract(7, 0, other(y)) != BVV(3, 8),
+        power(BVV(256, 256), y) > 0,
+        BVAddNoOverflow(x, y, False),
+        If(b, x, y) != BVV(0, 256),
+    ]
+    rng.shuffle(cs)
+    return [c.raw for c in cs[: rng.randint(4, len(cs))]]
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_host_model_eval_matches_bytecode(seed):
+    """Witness.ev (host Model.eval) == oracle evaluation of the lowered program."""
+    rng = random.Random(seed)
+    reg = UFRegistry()
+    reg.keccak[512] = KeccakSpec(lo=(10 ** 40 - 34534) * ((2 ** 256 - 1) // 10 ** 40))
+    reg.keccak[512].concrete[(7 << 256) | 9] = rng.getrandbits(256)
+    cs = _random_constraints(rng, reg)
+    lo = TermLowering(reg).lower(cs)
+    prog = lower(lo.dag)
+    sv = O.SetView.from_batch(ir.Batch([prog]), 0)
+    agree = 0
+    for trial in range(40):
+        vals = []
+        for v in prog.vars:
+            choice = rng.random()
+            if v.name in ("x", "y") and choice < 0.3:
+                vals.append(rng.choice([0, 1, 5, 7, 9]))
+            else:
+                vals.append(rng.getrandbits(v.width))
+        w = Witness(lo, vals, reg)
+        host = all(w.ev(c) for c in cs)
+        dev = sv.evaluate(vals)
+        assert host == dev, (seed, trial)
+        agree += 1
+    assert agree == 40
+
+
+def test_uf_hash_matches_oracle():
+    rng = random.Random(1)
+    for _ in range(20):
+        x, salt = rng.getrandbits(256), rng.getrandbits(32)
+        assert uf_hash(x, salt) == O.uf_hash(x, salt)
+
+
+def test_keccak_interpretation_satisfies_conditions_by_construction():
+    """Any candidate: inv(f(k)) == k, interval and %64 hold (keccak_function_manager.py:150-179)."""
+    reg = UFRegistry()
+    lo_idx = 10 ** 40 - 34534
+    part = (2 ** 256 - 1) // 10 ** 40
+    reg.keccak[256] = KeccakSpec(lo=lo_idx * part)
+    f = Function("keccak256_256", [256], 256)
+    inv = Function("keccak256_256-1", [256], 256)
+    n = BV("n", 256)
+    cond = And(inv(f(n)) == n, ULE(BVV(lo_idx * part, 256), f(n)),
+               ULT(f(n), BVV(lo_idx * part + part, 256)), URem(f(n), BVV(64, 256)) == 0)
+    lo = TermLowering(reg).lower([cond.raw])
+    prog = lower(lo.dag)
+    sv = O.SetView.from_batch(ir.Batch([prog]), 0)
+    rng = np.random.default_rng(0)
+    for _ in range(32):
+        assert sv.evaluate([int.from_bytes(rng.bytes(32), "little")])
