@@ -158,7 +158,7 @@ class BaseSolver:
         return self._model
 
     def sexpr(self) -> str:
-        lines = []
+        lines = T.declarations(self.constraints + self._minimize + self._maximize)
         for c in self.constraints:
             lines.append(f"(assert {T.to_sexpr(c)})")
         for e in self._minimize:

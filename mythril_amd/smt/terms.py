@@ -306,7 +306,7 @@ def to_sexpr(t: Term, _memo: Optional[dict] = None) -> str:
     if t.op in ("true", "false"):
         return t.op
     if t.op in ("var", "bvar", "array"):
-        return f"|{t.val}|" if not str(t.val).isidentifier() else str(t.val)
+        return _q(t.val)
     if t.op == "extract":
         return f"((_ extract {t.val[0]} {t.val[1]}) {to_sexpr(t.args[0])})"
     if t.op == "zero_extend":
@@ -314,7 +314,42 @@ def to_sexpr(t: Term, _memo: Optional[dict] = None) -> str:
     if t.op == "K":
         return f"((as const (Array (_ BitVec {t.sort[1]}) (_ BitVec {t.sort[2]}))) {to_sexpr(t.args[0])})"
     if t.op == "apply":
-        name = t.val[0]
-        return f"(|{name}| " + " ".join(to_sexpr(a) for a in t.args) + ")"
+        return f"({_q(t.val[0])} " + " ".join(to_sexpr(a) for a in t.args) + ")"
     name = {"iff": "=", "bvexp": "bvexp"}.get(t.op, t.op)
     return f"({name} " + " ".join(to_sexpr(a) for a in t.args) + ")"
+
+
+def _sort_str(sort: tuple) -> str:
+    if sort == BOOL:
+        return "Bool"
+    if sort[0] == "bv":
+        return f"(_ BitVec {sort[1]})"
+    return f"(Array (_ BitVec {sort[1]}) (_ BitVec {sort[2]}))"
+
+
+def _q(name: str) -> str:
+    return name if str(name).isidentifier() else f"|{name}|"
+
+
+def declarations(roots) -> list:
+    """``declare-fun`` lines for every free symbol / UF reachable from ``roots`` (z3 order:
+    first occurrence)."""
+    out, seen, done = [], set(), set()
+    stack = list(reversed(list(roots)))
+    while stack:
+        t = stack.pop()
+        if t in done:
+            continue
+        done.add(t)
+        if t.op in ("var", "bvar", "array"):
+            if t.val not in seen:
+                seen.add(t.val)
+                out.append(f"(declare-fun {_q(t.val)} () {_sort_str(t.sort)})")
+        elif t.op == "apply":
+            name, doms = t.val
+            if name not in seen:
+                seen.add(name)
+                d = " ".join(f"(_ BitVec {w})" for w in doms)
+                out.append(f"(declare-fun {_q(name)} ({d}) (_ BitVec {t.width}))")
+        stack.extend(reversed(t.args))
+    return out
