@@ -11,8 +11,11 @@
  * restatement that pins them is oracle/pyoracle.py.
  *
  * Instruction = 4 x uint32:
- *   w0 = op | (width << 8) | (flags << 18)      width = result width (W ops) or the
- *                                               operand width (compare ops), 1..256
+ *   w0 = op | (width << 8) | (traffic << 18)    width = result width (W ops) or the
+ *           | (unit << 21)                      operand width (compare ops), 1..256;
+ *                                               traffic = PF_TR_* bits and unit =
+ *                                               PF_U_* datapath, both recomputed from
+ *                                               the opcode by pf_batch_create
  *   w1 = dst | (a << 8) | (b << 16) | (c << 24) register indices
  *   w2 = aux0, w3 = aux1                        op specific
  *
@@ -83,6 +86,51 @@ enum pf_opcode {
                          false stops evaluating the set here                           */
     PF_NUM_OPCODES = 64
 };
+
+/* operand traffic bits (w0 >> 18): reads W[a], reads W[b], writes W[d] */
+#define PF_TR_RA 1u
+#define PF_TR_RB 2u
+#define PF_TR_WW 4u
+
+/* datapath unit of each opcode (w0 >> 21): the kernel dispatches on it first */
+enum pf_unit {
+    PF_U_ALU = 0,   /* W add/sub/logic/const/mov/not/neg/sext/ite/hash */
+    PF_U_MUL = 1,   /* MUL, EXP                                        */
+    PF_U_DIV = 2,   /* UDIV..SMOD, UMUL_NOOVF                          */
+    PF_U_SHIFT = 3, /* SHL/LSHR/ASHR/EXTRACT/CONCAT                    */
+    PF_U_GEN = 4,   /* W_VAR, B_VAR (candidate generator)             */
+    PF_U_CMP = 5,   /* B_EQ..B_SLE, UADD_NOOVF                         */
+    PF_U_BOOL = 6,  /* B_CONST, B_AND..B_ITE, ASSERT                   */
+    PF_U_END = 7
+};
+
+#ifdef __cplusplus
+static inline uint32_t pf_op_unit(uint32_t op) {
+    if (op == PF_W_MUL || op == PF_W_EXP) return PF_U_MUL;
+    if ((op >= PF_W_UDIV && op <= PF_W_SMOD) || op == PF_B_UMUL_NOOVF) return PF_U_DIV;
+    if ((op >= PF_W_SHL && op <= PF_W_ASHR) || op == PF_W_EXTRACT || op == PF_W_CONCAT) return PF_U_SHIFT;
+    if (op == PF_W_VAR || op == PF_B_VAR) return PF_U_GEN;
+    if ((op >= PF_B_EQ && op <= PF_B_SLE) || op == PF_B_UADD_NOOVF) return PF_U_CMP;
+    if (op == PF_B_CONST || (op >= PF_B_AND && op <= PF_B_ITE) || op == PF_ASSERT) return PF_U_BOOL;
+    if (op == PF_END || op >= PF_NUM_OPCODES) return PF_U_END;
+    return PF_U_ALU;
+}
+
+/* traffic of each opcode (host side; the kernel reads the bits from the instruction) */
+static inline uint32_t pf_op_traffic(uint32_t op) {
+    const uint32_t rab_w = PF_TR_RA | PF_TR_RB | PF_TR_WW, ra_w = PF_TR_RA | PF_TR_WW;
+    if (op == PF_W_CONST || op == PF_W_VAR) return PF_TR_WW;
+    if (op == PF_W_MOV || op == PF_W_NOT || op == PF_W_NEG || op == PF_W_EXTRACT ||
+        op == PF_W_SEXT || op == PF_W_HASH)
+        return ra_w;
+    if ((op >= PF_W_ADD && op <= PF_W_SMOD) || (op >= PF_W_AND && op <= PF_W_XOR) ||
+        (op >= PF_W_SHL && op <= PF_W_EXP) || op == PF_W_CONCAT || op == PF_W_ITE)
+        return rab_w;
+    if ((op >= PF_B_EQ && op <= PF_B_SLE) || op == PF_B_UADD_NOOVF || op == PF_B_UMUL_NOOVF)
+        return PF_TR_RA | PF_TR_RB;
+    return 0u;
+}
+#endif
 
 /* ---- variable schema (4 x uint32 per variable) -------------------------------- */
 /* s0 = kind | (width << 8); s1 = hint0; s2 = hint1; s3 = parent slot (or PF_NO_PARENT) */

@@ -221,6 +221,33 @@ int pf_batch_create(const uint32_t* code, size_t n_ins, const uint32_t* consts, 
         }
         max_vars = std::max(max_vars, d.n_vars);
     }
+    // traffic bits and register def-before-use, recomputed here so the kernel can trust
+    // them whatever the caller packed (w0 bits 18..23)
+    std::vector<uint32_t> code_fixed(code, code + 4 * n_ins);
+    for (size_t s = 0; s < n_sets; s++) {
+        const pf_set_desc& d = descs[s];
+        uint32_t wdef = 1u << PF_W_SINK, bdef = 0u;
+        for (uint32_t i = 0; i < d.n_ins; i++) {
+            uint32_t* I = code_fixed.data() + 4 * ((size_t)d.code_off + i);
+            const uint32_t op = I[0] & 0xffu, tr = pf_op_traffic(op);
+            I[0] = (I[0] & 0x3ffffu) | (tr << 18) | (pf_op_unit(op) << 21);
+            const uint32_t rd = I[1] & 0xffu, ra = (I[1] >> 8) & 0xffu, rb = (I[1] >> 16) & 0xffu,
+                           rc = (I[1] >> 24) & 0xffu;
+            if ((tr & PF_TR_WW) && rd >= PF_NW) return fail("set %zu ins %u: W dst %u", s, i, rd);
+            if (((tr & PF_TR_RA) && !(wdef >> (ra & 15u) & 1u)) || ((tr & PF_TR_RB) && !(wdef >> (rb & 15u) & 1u)))
+                return fail("set %zu ins %u: W register read before write", s, i);
+            const bool bres = op >= PF_B_CONST && op <= PF_B_UMUL_NOOVF;
+            const bool breads_ab = op >= PF_B_AND && op <= PF_B_XOR;
+            if ((breads_ab && (!(bdef >> (ra & 31u) & 1u) || !(bdef >> (rb & 31u) & 1u))) ||
+                ((op == PF_B_NOT || op == PF_ASSERT) && !(bdef >> (ra & 31u) & 1u)) ||
+                ((op == PF_W_ITE || op == PF_B_ITE) && !(bdef >> (rc & 31u) & 1u)) ||
+                (op == PF_B_ITE && (!(bdef >> (ra & 31u) & 1u) || !(bdef >> (rb & 31u) & 1u))))
+                return fail("set %zu ins %u: B register read before write", s, i);
+            if (tr & PF_TR_WW) wdef |= 1u << rd;
+            if (bres) bdef |= 1u << (rd & 31u);
+        }
+    }
+    code = code_fixed.data();
     Batch* B = new Batch();
     B->device = g_device;
     B->n_ins = n_ins;

@@ -88,38 +88,6 @@ PF_INL u256 pow2m1(uint32_t k) {  // 2^k - 1
     return r;
 }
 
-// signed division family on sign-extended 256-bit operands (SMT-LIB2 definitions)
-PF_INL u256 sdivrem(const u256& a, const u256& b, int which /*0 sdiv,1 srem,2 smod*/) {
-    uint32_t sa = a.l[7] >> 31, sb = b.l[7] >> 31;
-    u256 ua = sa ? pf::neg256(a) : a;
-    u256 ub = sb ? pf::neg256(b) : b;
-    u256 q, r;
-    pf::udivrem256(ua, ub, &q, &r);
-    if (which == 0) return (sa ^ sb) ? pf::neg256(q) : q;
-    if (which == 1) return sa ? pf::neg256(r) : r;
-    // smod: sign follows divisor
-    if (pf::iszero256(r)) return r;
-    if (!sa && !sb) return r;
-    if (sa && !sb) return pf::add256(pf::neg256(r), b);
-    if (!sa && sb) return pf::add256(r, b);
-    return pf::neg256(r);
-}
-
-PF_INL u256 expmod(const u256& a, const u256& b, uint32_t w) {
-    u256 r = pf::zero256();
-    r.l[0] = 1u;
-    u256 base = a, e = b;
-    for (uint32_t i = 0; i < w; i++) {  // fixed w square-and-multiply steps
-        u256 t = pf::mul256(r, base);
-        r = pf::sel256(e.l[0] & 1u, t, r);
-        base = pf::mul256(base, base);
-#pragma unroll
-        for (int k = 0; k < 7; k++) e.l[k] = (e.l[k] >> 1) | (e.l[k + 1] << 31);
-        e.l[7] >>= 1;
-    }
-    return r;
-}
-
 // ---- Philox4x32-10 -------------------------------------------------------------------
 PF_INL uint4 philox(uint4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
@@ -260,28 +228,6 @@ PF_INL u256 gen_var(const SetCtx& S, uint32_t v, uint32_t cand) {
 
 enum Mode { MODE_GEN = 0, MODE_SOA = 1 };
 
-// operand traffic per opcode: bit0 reads W[a], bit1 reads W[b], bit2 writes W[d].
-// One read-a, one read-b and one write site for the whole interpreter keeps the W banks
-// promotable to VGPRs (few extract/insert users) and the code small.
-#define RA 1u
-#define RB 2u
-#define WW 4u
-__constant__ uint8_t kOpTraffic[PF_NUM_OPCODES] = {
-    /*END*/ 0, /*CONST*/ WW, /*VAR*/ WW, /*MOV*/ RA | WW,
-    /*ADD..SMOD (4..11)*/ RA | RB | WW, RA | RB | WW, RA | RB | WW, RA | RB | WW, RA | RB | WW,
-    RA | RB | WW, RA | RB | WW, RA | RB | WW,
-    /*AND OR XOR (12..14)*/ RA | RB | WW, RA | RB | WW, RA | RB | WW,
-    /*NOT NEG*/ RA | WW, RA | WW,
-    /*SHL LSHR ASHR EXP (17..20)*/ RA | RB | WW, RA | RB | WW, RA | RB | WW, RA | RB | WW,
-    /*EXTRACT*/ RA | WW, /*CONCAT*/ RA | RB | WW, /*SEXT*/ RA | WW, /*ITE*/ RA | RB | WW,
-    /*HASH*/ RA | WW,
-    /*26..39*/ 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
-    /*B_CONST B_VAR*/ 0, 0,
-    /*EQ ULT ULE SLT SLE (42..46)*/ RA | RB, RA | RB, RA | RB, RA | RB, RA | RB,
-    /*B_AND B_OR B_XOR B_NOT B_ITE (47..51)*/ 0, 0, 0, 0, 0,
-    /*UADD_NOOVF UMUL_NOOVF*/ RA | RB, RA | RB,
-    /*54..63*/ 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-
 // Run one set's program for this lane's candidate.  Returns the lane's root (0/1);
 // *complete = 1 if the program ran to END (not short-circuited).  `ops` accumulates
 // aux1 (per-lane algorithmic cost) of every executed instruction.
@@ -289,168 +235,198 @@ template <int MODE>
 PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_t flags,
                             const uint32_t* __restrict__ soa, uint32_t soa_n,
                             uint32_t* complete, uint64_t* ops) {
-    // element-wise init: a whole-vector store would defeat promote-alloca-to-vector
+    // No initialisation: pf_batch_create rejects programs that read a register before
+    // writing it, so the banks never leak values between candidates.
     v16u W[8];
-#pragma unroll
-    for (int k = 0; k < 8; k++)
-#pragma unroll
-        for (int r = 0; r < 16; r++) W[k][r] = 0u;
     // the 32 bool registers are the bits of one VGPR (bit r = B register r)
     uint32_t Bk = 0u;
 #define BGET(r) ((Bk >> ((r) & 31u)) & 1u)
     uint32_t root = 1u;
     uint64_t cost = 0;
     *complete = 0u;
-    for (uint32_t pc = 0; pc < S.n_ins; pc++) {
-        const uint4 I = S.code[pc];
+    // Software-pipelined fetch: the scalar load of instruction pc+1 is issued while
+    // instruction pc executes (the last slot re-reads END, never past the program).
+    uint4 In = S.code[0];
+    uint32_t pc = 0;
+    while (pc < S.n_ins) {
+        const uint4 I = In;
         const uint32_t op = I.x & 0xffu;
         const uint32_t w = (I.x >> 8) & 0x3ffu;
+        const uint32_t tr = (I.x >> 18) & 7u;
+        const uint32_t unit = (I.x >> 21) & 7u;
         const uint32_t d = I.y & 0xffu, a = (I.y >> 8) & 0xffu, b = (I.y >> 16) & 0xffu,
                        c = (I.y >> 24) & 0xffu;
+        const uint32_t aux = I.z;
         cost += I.w;
-        if (op == PF_END) {
+        // Issue the next fetch only after this instruction's words are decoded: scalar
+        // loads return out of order, so a fetch issued before the decode would be waited
+        // for together with the one being consumed (lgkmcnt(0)).
+        __builtin_amdgcn_sched_barrier(0);
+        In = S.code[min(pc + 1u, S.n_ins - 1u)];
+        pc++;
+        if (unit == PF_U_END) {
             *complete = 1u;
             break;
         }
-        const uint32_t tr = kOpTraffic[op & (PF_NUM_OPCODES - 1)];
         u256 x, y, z;
-        if (tr & RA) RD_W(x, W, a & 15u);
-        if (tr & RB) RD_W(y, W, b & 15u);
+        if (tr & PF_TR_RA) RD_W(x, W, a & 15u);
+        if (tr & PF_TR_RB) RD_W(y, W, b & 15u);
         uint32_t bres = 0;  // bool result for B ops
-        switch (op) {
-            case PF_W_ADD: z = pf::add256(x, y); break;
-            case PF_W_SUB: z = pf::sub256(x, y); break;
-            case PF_W_MUL: z = pf::mul256(x, y); break;
-            case PF_W_UDIV:
-            case PF_W_UREM: {
-                u256 q, r;
-                pf::udivrem256(x, y, &q, &r);
-                z = (op == PF_W_UDIV) ? q : r;
+        // Dispatch on the datapath unit (w0 bits 21..23) first.  The heavy datapaths exist
+        // once each (multiplier, divider, shifter, generator) and are shared by every
+        // opcode that needs them: the kernel's code must stay small enough for the
+        // instruction cache, since consecutive bytecode instructions jump between units.
+        switch (unit) {
+            case PF_U_MUL:
+                // ---- multiplier: MUL = one product; EXP = 2-bit-window square-and-multiply
+                // over the wave's largest exponent bit length (pf::exp256)
+                if (op == PF_W_MUL) {
+                    z = pf::mul256(x, y);
+                } else {
+                    uint32_t nb = 256u - pf::clz256(y);
+#pragma unroll
+                    for (int o = 32; o >= 1; o >>= 1) nb = max(nb, (uint32_t)__shfl_xor((int)nb, o));
+                    nb = min(__builtin_amdgcn_readfirstlane(nb), 256u);
+                    z = pf::exp256(x, y, nb);
+                }
+                break;
+            case PF_U_DIV: {
+                // ---- divider: bvudiv/bvurem/bvsdiv/bvsrem/bvsmod (SMT-LIB2 definitions on
+                // magnitudes) and bvumul_noovfl (a*b < 2^w  <=>  b == 0 || a <= (2^w-1)/b)
+                const bool sgn = op >= PF_W_SDIV && op <= PF_W_SMOD;
+                const bool ovf = op == PF_B_UMUL_NOOVF;
+                const u256 xs = sgn ? sextw(x, w) : x;
+                const u256 ys = sgn ? sextw(y, w) : y;
+                const uint32_t sa = sgn ? (xs.l[7] >> 31) : 0u, sb = sgn ? (ys.l[7] >> 31) : 0u;
+                u256 ua = sa ? pf::neg256(xs) : xs;
+                if (ovf) {
+                    ua = pf::ones256();
+                    maskw(ua, w);
+                }
+                const u256 ub = sb ? pf::neg256(ys) : ys;
+                u256 q, rr;
+                pf::udivrem256(ua, ub, &q, &rr);
+                const bool want_q = op == PF_W_UDIV || op == PF_W_SDIV;
+                const u256 v = want_q ? q : rr;
+                const uint32_t neg = want_q ? (sa ^ sb) : sa;
+                z = neg ? pf::neg256(v) : v;
+                if (op == PF_W_SMOD && !pf::iszero256(rr) && (sa ^ sb)) z = pf::add256(z, ys);
+                bres = pf::iszero256(y) || !pf::ult256(q, x);
                 break;
             }
-            case PF_W_SDIV: z = sdivrem(sextw(x, w), sextw(y, w), 0); break;
-            case PF_W_SREM: z = sdivrem(sextw(x, w), sextw(y, w), 1); break;
-            case PF_W_SMOD: z = sdivrem(sextw(x, w), sextw(y, w), 2); break;
-            case PF_W_AND:
+            case PF_U_SHIFT: {
+                const bool by_reg = op <= PF_W_ASHR;
+                const uint32_t big = by_reg ? ge_width(y, w) : (aux >= 256u);
+                const uint32_t amt = by_reg ? y.l[0] : aux;
+                if (op == PF_W_SHL || op == PF_W_CONCAT) {
+                    z = pf::shl256(x, big ? 0u : amt, big);
+                    if (op == PF_W_CONCAT) {
 #pragma unroll
-                for (int i = 0; i < 8; i++) z.l[i] = x.l[i] & y.l[i];
-                break;
-            case PF_W_OR:
-#pragma unroll
-                for (int i = 0; i < 8; i++) z.l[i] = x.l[i] | y.l[i];
-                break;
-            case PF_W_XOR:
-#pragma unroll
-                for (int i = 0; i < 8; i++) z.l[i] = x.l[i] ^ y.l[i];
-                break;
-            case PF_W_SHL: z = pf::shl256(x, y.l[0], ge_width(y, w)); break;
-            case PF_W_LSHR: {
-                uint32_t big = ge_width(y, w);
-                z = pf::shr256(x, big ? 0u : y.l[0], 0u);
-                if (big) z = pf::zero256();
+                        for (int i = 0; i < 8; i++) z.l[i] |= y.l[i];
+                    }
+                } else {
+                    const bool ar = op == PF_W_ASHR;
+                    const u256 src = ar ? sextw(x, w) : x;
+                    const uint32_t f = ar ? 0u - (src.l[7] >> 31) : 0u;
+                    z = pf::shr256(src, big ? (ar ? 255u : 0u) : (amt & 255u), f);
+                    if (big && !ar) z = pf::zero256();
+                }
                 break;
             }
-            case PF_W_ASHR: {
-                u256 sx = sextw(x, w);
-                uint32_t big = ge_width(y, w);
-                uint32_t f = 0u - (sx.l[7] >> 31);
-                z = pf::shr256(sx, big ? 255u : y.l[0], f);
-                break;
-            }
-            case PF_W_EXP: z = expmod(x, y, w); break;
-            case PF_W_CONST: {
-                const uint32_t* cp = S.consts + (size_t)I.z * 8u;
-#pragma unroll
-                for (int i = 0; i < 8; i++) z.l[i] = cp[i];
-                break;
-            }
-            case PF_W_VAR:
+            case PF_U_GEN:
+                // ---- candidate generator (one site for W and B variables)
                 if (MODE == MODE_GEN) {
-                    z = gen_var(S, I.z, cand);
+                    z = gen_var(S, aux, cand);
                 } else {
 #pragma unroll
                     for (int i = 0; i < 8; i++)
-                        z.l[i] = active ? soa[((size_t)I.z * 8u + i) * soa_n + cand] : 0u;
+                        z.l[i] = active ? soa[((size_t)aux * 8u + i) * soa_n + cand] : 0u;
                 }
+                bres = z.l[0] & 1u;
                 break;
-            case PF_W_MOV: z = x; break;
-            case PF_W_NOT: z = pf::not256(x); break;
-            case PF_W_NEG: z = pf::neg256(x); break;
-            case PF_W_EXTRACT: z = pf::shr256(x, I.z & 255u, 0u); break;
-            case PF_W_CONCAT: {
-                z = pf::shl256(x, I.z, I.z >= 256u);
-#pragma unroll
-                for (int i = 0; i < 8; i++) z.l[i] |= y.l[i];
-                break;
-            }
-            case PF_W_SEXT: z = sextw(x, I.z); break;
-            case PF_W_ITE: z = pf::sel256(BGET(c), x, y); break;
-            case PF_W_HASH: {
-                const uint32_t salt = I.z;
-                uint4 h = philox(make_uint4(x.l[0], x.l[1], x.l[2], x.l[3]), salt, PF_HASH_K1A);
-                uint4 g = philox(make_uint4(x.l[4] ^ h.x, x.l[5] ^ h.y, x.l[6] ^ h.z, x.l[7] ^ h.w),
-                                 salt, PF_HASH_K1B);
-                z.l[0] = h.x; z.l[1] = h.y; z.l[2] = h.z; z.l[3] = h.w;
-                z.l[4] = g.x; z.l[5] = g.y; z.l[6] = g.z; z.l[7] = g.w;
-                break;
-            }
-            case PF_B_CONST: bres = I.z & 1u; break;
-            case PF_B_VAR:
-                if (MODE == MODE_GEN) {
-                    bres = gen_var(S, I.z, cand).l[0] & 1u;
-                } else {
-                    bres = active ? (soa[((size_t)I.z * 8u) * soa_n + cand] & 1u) : 0u;
-                }
-                break;
-            case PF_B_EQ: bres = pf::eq256(x, y); break;
-            case PF_B_ULT: bres = pf::ult256(x, y); break;
-            case PF_B_ULE: bres = pf::ult256(y, x) ^ 1u; break;
-            case PF_B_SLT:
-            case PF_B_SLE: {
-                u256 sx = sextw(x, w), sy = sextw(y, w);
-                sx.l[7] ^= 0x80000000u;
-                sy.l[7] ^= 0x80000000u;
-                bres = (op == PF_B_SLT) ? pf::ult256(sx, sy) : (pf::ult256(sy, sx) ^ 1u);
-                break;
-            }
-            case PF_B_UADD_NOOVF: {
-                uint32_t co;
-                u256 s = pf::add256c(x, y, &co);
-                u256 sm = s;
-                maskw(sm, w);  // no overflow iff the sum fits in w bits
-                bres = (co == 0u) && pf::eq256(sm, s);
-                break;
-            }
-            case PF_B_UMUL_NOOVF: {
-                uint32_t ov = pf::mul256_overflows(x, y);
-                u256 p = pf::mul256(x, y);
-                u256 pm = p;
-                maskw(pm, w);
-                bres = (ov == 0u) && pf::eq256(pm, p);
-                break;
-            }
-            case PF_B_AND: bres = BGET(a) & BGET(b); break;
-            case PF_B_OR: bres = BGET(a) | BGET(b); break;
-            case PF_B_XOR: bres = BGET(a) ^ BGET(b); break;
-            case PF_B_NOT: bres = BGET(a) ^ 1u; break;
-            case PF_B_ITE: bres = BGET(c) ? BGET(a) : BGET(b); break;
-            case PF_ASSERT:
-                root &= BGET(a);
-                if (flags & PF_FLAG_SHORTCIRCUIT) {
-                    if (__ballot(root && active) == 0ull) {
-                        *ops += cost;
-                        return 0u;
+            case PF_U_CMP:
+                switch (op) {
+                    case PF_B_EQ: bres = pf::eq256(x, y); break;
+                    case PF_B_ULT: bres = pf::ult256(x, y); break;
+                    case PF_B_ULE: bres = pf::ult256(y, x) ^ 1u; break;
+                    case PF_B_SLT:
+                    case PF_B_SLE: {
+                        u256 sx = sextw(x, w), sy = sextw(y, w);
+                        sx.l[7] ^= 0x80000000u;
+                        sy.l[7] ^= 0x80000000u;
+                        bres = (op == PF_B_SLT) ? pf::ult256(sx, sy) : (pf::ult256(sy, sx) ^ 1u);
+                        break;
+                    }
+                    default: {  // PF_B_UADD_NOOVF
+                        uint32_t co;
+                        u256 sm = pf::add256c(x, y, &co);
+                        u256 s2 = sm;
+                        maskw(s2, w);  // no overflow iff the sum fits in w bits
+                        bres = (co == 0u) && pf::eq256(sm, s2);
+                        break;
                     }
                 }
                 break;
-            default: break;
+            case PF_U_BOOL:
+                switch (op) {
+                    case PF_B_CONST: bres = aux & 1u; break;
+                    case PF_B_AND: bres = BGET(a) & BGET(b); break;
+                    case PF_B_OR: bres = BGET(a) | BGET(b); break;
+                    case PF_B_XOR: bres = BGET(a) ^ BGET(b); break;
+                    case PF_B_NOT: bres = BGET(a) ^ 1u; break;
+                    case PF_B_ITE: bres = BGET(c) ? BGET(a) : BGET(b); break;
+                    default:  // PF_ASSERT
+                        root &= BGET(a);
+                        if ((flags & PF_FLAG_SHORTCIRCUIT) && __ballot(root && active) == 0ull)
+                            pc = S.n_ins;  // every lane of the wave is decided: leave the program
+                        break;
+                }
+                break;
+            default:  // PF_U_ALU
+                switch (op) {
+                    case PF_W_ADD: z = pf::add256(x, y); break;
+                    case PF_W_SUB: z = pf::sub256(x, y); break;
+                    case PF_W_AND:
+#pragma unroll
+                        for (int i = 0; i < 8; i++) z.l[i] = x.l[i] & y.l[i];
+                        break;
+                    case PF_W_OR:
+#pragma unroll
+                        for (int i = 0; i < 8; i++) z.l[i] = x.l[i] | y.l[i];
+                        break;
+                    case PF_W_XOR:
+#pragma unroll
+                        for (int i = 0; i < 8; i++) z.l[i] = x.l[i] ^ y.l[i];
+                        break;
+                    case PF_W_CONST: {
+                        const uint32_t* cp = S.consts + (size_t)aux * 8u;
+#pragma unroll
+                        for (int i = 0; i < 8; i++) z.l[i] = cp[i];
+                        break;
+                    }
+                    case PF_W_MOV: z = x; break;
+                    case PF_W_NOT: z = pf::not256(x); break;
+                    case PF_W_NEG: z = pf::neg256(x); break;
+                    case PF_W_SEXT: z = sextw(x, aux); break;
+                    case PF_W_ITE: z = pf::sel256(BGET(c), x, y); break;
+                    case PF_W_HASH: {
+                        uint4 h = philox(make_uint4(x.l[0], x.l[1], x.l[2], x.l[3]), aux, PF_HASH_K1A);
+                        uint4 g = philox(make_uint4(x.l[4] ^ h.x, x.l[5] ^ h.y, x.l[6] ^ h.z, x.l[7] ^ h.w),
+                                         aux, PF_HASH_K1B);
+                        z.l[0] = h.x; z.l[1] = h.y; z.l[2] = h.z; z.l[3] = h.w;
+                        z.l[4] = g.x; z.l[5] = g.y; z.l[6] = g.z; z.l[7] = g.w;
+                        break;
+                    }
+                    default: break;
+                }
+                break;
         }
         {
             // Unconditional write: ops without a W result write the sink register
             // PF_W_SINK.  A conditional insert would make the loop-carried banks a phi of
             // old/new values, which costs a full bank copy (~100 extra VGPRs, spills).
             maskw(z, w);
-            const uint32_t dd = (tr & WW) ? (d & 15u) : (uint32_t)PF_W_SINK;
+            const uint32_t dd = (tr & PF_TR_WW) ? (d & 15u) : (uint32_t)PF_W_SINK;
             WR_W(W, dd, z);
         }
         if (op >= PF_B_CONST && op <= PF_B_UMUL_NOOVF) {

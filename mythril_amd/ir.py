@@ -75,6 +75,16 @@ W_UNARY = (W_NOT, W_NEG, W_MOV, W_HASH)
 B_CMP = (B_EQ, B_ULT, B_ULE, B_SLT, B_SLE, B_UADD_NOOVF, B_UMUL_NOOVF)
 B_LOGIC = (B_AND, B_OR, B_XOR)
 
+# ---- datapath units (w0 bits 21..23, set by pf_batch_create from the opcode) --------
+U_ALU = 0
+U_MUL = 1
+U_DIV = 2
+U_SHIFT = 3
+U_GEN = 4
+U_CMP = 5
+U_BOOL = 6
+U_END = 7
+
 # ---- variable kinds --------------------------------------------------------------
 VK_GENERIC = 0
 VK_ACTOR = 1
