@@ -228,13 +228,20 @@ PF_INL u256 gen_var(const SetCtx& S, uint32_t v, uint32_t cand) {
 
 enum Mode { MODE_GEN = 0, MODE_SOA = 1 };
 
+// LDS for EXP's window table (pf::exp256): 8 entries x 4 limb pairs per lane, 64 lanes,
+// 4 waves per 256-thread workgroup = 64 KiB; two workgroups per CU fit in 160 KiB.
+#define PF_EXP_LDS_U2 (4 * 8 * 4 * 64)
+PF_INL uint2* exp_tbl_of(uint2* lds) {
+    return lds + (threadIdx.x >> 6) * (8 * 4 * 64) + (threadIdx.x & 63u);
+}
+
 // Run one set's program for this lane's candidate.  Returns the lane's root (0/1);
 // *complete = 1 if the program ran to END (not short-circuited).  `ops` accumulates
 // aux1 (per-lane algorithmic cost) of every executed instruction.
 template <int MODE>
 PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_t flags,
                             const uint32_t* __restrict__ soa, uint32_t soa_n,
-                            uint32_t* complete, uint64_t* ops) {
+                            uint2* exp_tbl, uint32_t* complete, uint64_t* ops) {
     // No initialisation: pf_batch_create rejects programs that read a register before
     // writing it, so the banks never leak values between candidates.
     v16u W[8];
@@ -287,7 +294,7 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
 #pragma unroll
                     for (int o = 32; o >= 1; o >>= 1) nb = max(nb, (uint32_t)__shfl_xor((int)nb, o));
                     nb = min(__builtin_amdgcn_readfirstlane(nb), 256u);
-                    z = pf::exp256(x, y, nb);
+                    z = pf::exp256(x, y, nb, exp_tbl, 64u);
                 }
                 break;
             case PF_U_DIV: {
@@ -475,6 +482,8 @@ pf_check_kernel(const pf_set_desc* __restrict__ descs, uint32_t n_sets,
     const uint32_t set = __builtin_amdgcn_readfirstlane(wave / slices);
     const uint32_t slice = __builtin_amdgcn_readfirstlane(wave % slices);
     const SetCtx S = make_ctx(descs, set, code, consts, schema, parents, gseed);
+    __shared__ uint2 pf_exp_lds[PF_EXP_LDS_U2];
+    uint2* exp_tbl = exp_tbl_of(pf_exp_lds);
 
     uint64_t t0 = 0;
     if (deadline_ticks) {
@@ -498,7 +507,7 @@ pf_check_kernel(const pf_set_desc* __restrict__ descs, uint32_t n_sets,
         const bool active = cand < end;
         uint32_t complete = 0;
         uint64_t lane_ops = 0;
-        uint32_t sat = run_program<MODE_GEN>(S, cand, active, flags, nullptr, 0u, &complete, &lane_ops);
+        uint32_t sat = run_program<MODE_GEN>(S, cand, active, flags, nullptr, 0u, exp_tbl, &complete, &lane_ops);
         const uint64_t m_act = __ballot(active);
         const uint64_t m_sat = __ballot(active && sat);
         const uint64_t m_full = __ballot(active && complete);
@@ -527,9 +536,11 @@ pf_eval_soa_kernel(const pf_set_desc* __restrict__ descs, uint32_t set,
     const uint32_t cand = blockIdx.x * blockDim.x + threadIdx.x;
     const bool active = cand < n_cand;
     const SetCtx S = make_ctx(descs, __builtin_amdgcn_readfirstlane(set), code, consts, schema, parents, 0ull);
+    __shared__ uint2 pf_exp_lds[PF_EXP_LDS_U2];
     uint32_t complete = 0;
     uint64_t ops = 0;
-    uint32_t sat = run_program<MODE_SOA>(S, active ? cand : 0u, active, 0u, soa, n_cand, &complete, &ops);
+    uint32_t sat = run_program<MODE_SOA>(S, active ? cand : 0u, active, 0u, soa, n_cand,
+                                         exp_tbl_of(pf_exp_lds), &complete, &ops);
     if (active) out[cand] = (uint8_t)sat;
 }
 

@@ -183,3 +183,39 @@ def test_keccak_fixed_dev_matches(engine):
     out = d_out.cpu().numpy()
     for i in range(0, n, 97):
         assert out[32 * i:32 * i + 32].tobytes() == O.keccak256(host[ln * i:ln * i + ln].tobytes())
+
+
+def _rand_operand(rng, w):
+    k = int(rng.integers(0, 6))
+    M = ir.mask(w)
+    if k == 0:
+        return [0, 1, 2, M, M - 1, 1 << (w - 1), (1 << (w - 1)) - 1][int(rng.integers(0, 7))] & M
+    if k == 1:
+        return int.from_bytes(rng.bytes(32), "little") & ((1 << int(rng.integers(1, w + 1))) - 1)
+    if k == 2:
+        return ((1 << int(rng.integers(0, w))) + int(rng.integers(-1, 2))) & M
+    return int.from_bytes(rng.bytes(32), "little") & M
+
+
+@pytest.mark.parametrize("name", sorted(_OPS))
+def test_random_arith_bulk(engine, name):
+    """4,096 seeded operand pairs per op (w = 256 and an odd width), GPU vs the oracle."""
+    fn = {"add": O.bvadd, "sub": O.bvsub, "mul": O.bvmul, "udiv": O.bvudiv, "urem": O.bvurem,
+          "sdiv": O.bvsdiv, "srem": O.bvsrem, "smod": O.bvsmod, "shl": O.bvshl,
+          "lshr": O.bvlshr, "ashr": O.bvashr, "exp": O.bvexp}[name]
+    rng = np.random.default_rng(0xA11CE + len(name))
+    for w in (256, 173):
+        prog = _op_program(name, w)
+        db = engine.upload([prog])
+        cands = []
+        for _ in range(2048):
+            a, b = _rand_operand(rng, w), _rand_operand(rng, w)
+            if name in ("shl", "lshr", "ashr") and rng.random() < 0.7:
+                b = int(rng.integers(0, w + 2))
+            r = fn(a, b, w)
+            cands.append([a, b, r])
+            cands.append([a, b, r ^ (1 << int(rng.integers(0, w)))])
+        got = engine.eval_assignments(db, 0, ir.pack_assignments(prog, cands))
+        want = np.array([i % 2 == 0 for i in range(len(cands))])
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, (name, w, [[hex(v) for v in cands[i]] for i in bad[:3]])

@@ -6,6 +6,9 @@
 #define __device__
 #define __forceinline__ inline
 static inline unsigned long long __ballot(int p) { return p ? 1ull : 0ull; }
+struct uint2 { uint32_t x, y; };
+static inline uint2 make_uint2(uint32_t x, uint32_t y) { return uint2{x, y}; }
+#define PF_HOST_MAC
 #include "../mythril_amd/csrc/u256.h"
 using pf::u256;
 int main() {
@@ -21,7 +24,8 @@ int main() {
         pf::udivrem256(a, b, &q, &r);
         u256 m = pf::mul256(a, b);
         u256 sq = pf::sqr256(a);
-        u256 ex = pf::exp256(a, b, 256u - pf::clz256(b));
+        uint2 tbl[32];
+        u256 ex = pf::exp256(a, b, (a.l[0] & 1u) ? 256u : 256u - pf::clz256(b), tbl, 1u);
         for (int i = 7; i >= 0; i--) printf("%08x", q.l[i]); printf(" ");
         for (int i = 7; i >= 0; i--) printf("%08x", r.l[i]); printf(" ");
         for (int i = 7; i >= 0; i--) printf("%08x", m.l[i]); printf(" ");
