@@ -76,6 +76,21 @@ def cpu_baseline(programs, budget, seed, target_s):
             "sample": f"python oracle, {s} sets x 64 candidates ({err[:60]})"}
 
 
+def pmc_traffic(args):
+    """HBM bytes per launch of pf_check_kernel from the newest committed PMC summary
+    (profiles/*_pmc.json, written by tools/pmc_summary.py from separate rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE passes of this same default command) — None for other configs."""
+    if (args.sets, args.budget, args.mode) != (1024, 65536, "full"):
+        return None, None
+    import glob
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "*_pmc.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    return d.get("traffic_bytes"), os.path.relpath(files[-1], os.path.dirname(os.path.abspath(__file__)))
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -136,11 +151,13 @@ def main():
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         tot_evals, max_dt = float(ev.item()), float(mx.item())
         # the path's one collective: all-gather the per-set SAT verdicts
-        sat = torch.from_numpy(np.concatenate(founds).astype(np.int64)).to("cuda")
-        gathered = [torch.empty_like(sat) for _ in range(world)]
-        dist.all_gather(gathered, sat)
+        from mythril_amd.dist import gather_found
+
+        local = np.concatenate(founds)
+        gather_found(local, rank * len(local), world * len(local))
 
     if rank == 0:
+        traffic, traffic_src = pmc_traffic(args)
         kernel_s = sum(kms) / 1e3
         achieved = ops / kernel_s if kernel_s > 0 else 0.0
         line = {
@@ -161,9 +178,11 @@ def main():
                        "mode": args.mode, "parallelism": f"sets sharded over {world} GPU(s)"},
             "roofline": {"bound": "valu", "achieved": achieved / 1e12,
                          "peak": INT32_PEAK_OPS / 1e12, "unit": "Tops/s (int32)",
-                         "frac": achieved / INT32_PEAK_OPS, "traffic": None,
+                         "frac": achieved / INT32_PEAK_OPS, "traffic": traffic,
+                         "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
                          "kernel": "pf_check_kernel", "kernel_ms_avg": float(np.mean(kms))},
-            "node_evals_note": "ops counted with the SURVEY.md §8(d) per-op int32 table",
+            "node_evals_note": "ops counted with the SURVEY.md §8(d) per-op int32 table (EXP priced "
+                               "at 512 products; the kernel's windowed EXP needs ~340, DESIGN.md §4)",
             "gen_upload_s": t_gen,
         }
         if world == 1 and not args.no_cpu_baseline:
