@@ -40,7 +40,7 @@ _KECCAK_RE = re.compile(r"^keccak256_(\d+)(-1)?$")
 ACTORS = (
     0xAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFE,  # CREATOR  (transaction/symbolic.py:26-37)
     0xDEADBEEFDEADBEEFDEADBEEFDEADBEEFDEADBEEF,  # ATTACKER
-    0xAAAAAAABBBBBBBBBCCCCCCCCCCCCCCCCCCCCCCCC,  # SOMEGUY
+    0xAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAA,  # SOMEGUY
 )
 KECCAK_MASK_BITS = 117
 

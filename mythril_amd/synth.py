@@ -191,7 +191,7 @@ def random_dag_batch(first_id: int, n: int, **kw) -> List[Program]:
 # ---- Mythril-shaped sets ------------------------------------------------------------
 CREATOR = 0xAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFE
 ATTACKER = 0xDEADBEEFDEADBEEFDEADBEEFDEADBEEFDEADBEEF
-SOMEGUY = 0xAAAAAAAABBBBBBBBCCCCCCCCDDDDDDDDEEEEEEEE
+SOMEGUY = 0xAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAA
 
 
 def calldata_word(dag: Dag, tx: int, offset: int, size_node: int) -> int:
