@@ -35,6 +35,7 @@
 #define PF_NB 32          /* bool registers                                          */
 #define PF_LIMBS 8        /* 8 x 32-bit limbs = 256 bits, little-endian limb order   */
 #define PF_MAX_WIDTH 256
+#define PF_MAX_SPILL 64   /* spill slots per lane (8 x u32 each, private scratch)       */
 
 /* ---- opcodes ------------------------------------------------------------------ */
 enum pf_opcode {
@@ -67,6 +68,8 @@ enum pf_opcode {
     PF_W_HASH = 25,   /* dst <- H_aux0(a): keyed 256-bit mix of a (two Philox4x32-10
                          blocks, see below) — the by-construction interpretation of
                          uninterpreted functions (keccak256_<n>, unknown UFs)          */
+    PF_W_SPILL = 26,  /* spill slot aux0 <- W a      (register pressure; no W result)       */
+    PF_W_FILL = 27,   /* dst <- spill slot aux0                                          */
     /* B results */
     PF_B_CONST = 40,  /* dst <- aux0 & 1                                               */
     PF_B_VAR = 41,    /* dst <- candidate value of Bool variable aux0                  */
@@ -82,6 +85,8 @@ enum pf_opcode {
     PF_B_ITE = 51,    /* B[c] ? B a : B b                                              */
     PF_B_UADD_NOOVF = 52, /* a + b < 2^w   (z3 BVAddNoOverflow(a, b, False))          */
     PF_B_UMUL_NOOVF = 53, /* a * b < 2^w   (z3 BVMulNoOverflow(a, b, False), bvumul_noovfl) */
+    PF_B_FILL = 54,   /* dst <- limb 0 of spill slot aux0 (a spilled B value)              */
+    PF_B_SPILL = 55,  /* limb 0 of spill slot aux0 <- B a                                  */
     PF_ASSERT = 60,   /* root &= B a; with PF_FLAG_SHORTCIRCUIT a wave whose lanes are all
                          false stops evaluating the set here                           */
     PF_NUM_OPCODES = 64
@@ -111,7 +116,9 @@ static inline uint32_t pf_op_unit(uint32_t op) {
     if ((op >= PF_W_SHL && op <= PF_W_ASHR) || op == PF_W_EXTRACT || op == PF_W_CONCAT) return PF_U_SHIFT;
     if (op == PF_W_VAR || op == PF_B_VAR) return PF_U_GEN;
     if ((op >= PF_B_EQ && op <= PF_B_SLE) || op == PF_B_UADD_NOOVF) return PF_U_CMP;
-    if (op == PF_B_CONST || (op >= PF_B_AND && op <= PF_B_ITE) || op == PF_ASSERT) return PF_U_BOOL;
+    if (op == PF_B_CONST || (op >= PF_B_AND && op <= PF_B_ITE) || op == PF_ASSERT || op == PF_B_FILL ||
+        op == PF_B_SPILL)
+        return PF_U_BOOL;
     if (op == PF_END || op >= PF_NUM_OPCODES) return PF_U_END;
     return PF_U_ALU;
 }
@@ -119,7 +126,8 @@ static inline uint32_t pf_op_unit(uint32_t op) {
 /* traffic of each opcode (host side; the kernel reads the bits from the instruction) */
 static inline uint32_t pf_op_traffic(uint32_t op) {
     const uint32_t rab_w = PF_TR_RA | PF_TR_RB | PF_TR_WW, ra_w = PF_TR_RA | PF_TR_WW;
-    if (op == PF_W_CONST || op == PF_W_VAR) return PF_TR_WW;
+    if (op == PF_W_CONST || op == PF_W_VAR || op == PF_W_FILL) return PF_TR_WW;
+    if (op == PF_W_SPILL) return PF_TR_RA;
     if (op == PF_W_MOV || op == PF_W_NOT || op == PF_W_NEG || op == PF_W_EXTRACT ||
         op == PF_W_SEXT || op == PF_W_HASH)
         return ra_w;
@@ -131,6 +139,9 @@ static inline uint32_t pf_op_traffic(uint32_t op) {
     return 0u;
 }
 #endif
+
+/* B results are the opcodes PF_B_CONST..PF_B_FILL (a B destination register is written) */
+#define PF_OP_WRITES_B(op) ((op) >= PF_B_CONST && (op) <= PF_B_FILL)
 
 /* ---- variable schema (4 x uint32 per variable) -------------------------------- */
 /* s0 = kind | (width << 8); s1 = hint0; s2 = hint1; s3 = parent slot (or PF_NO_PARENT) */
@@ -167,6 +178,10 @@ typedef struct pf_set_desc {
  *    12,13 parent value (bit m[2] % w flipped when (m[1] & 3) == 0), else r[0] & 0xff
  *    14,15 small: r[0] & (2^(1 + m[1] % 16) - 1)
  * Candidate 0 is the exact parent value for every variable that has one.
+ * Neighbourhood candidates: for an odd candidate c, a variable with a parent value keeps
+ * it exactly when (m[3] & ((4 << ((c >> 1) & 3)) - 1)) != 0 — probability 3/4, 7/8, 15/16
+ * or 31/32 by (c >> 1) & 3 — and is generated by its kind's rule below otherwise, so half
+ * of the candidates are few-variable mutations of the parent (hint) model.
  * PF_VK_ACTOR: m[1] % 4 < hint1 -> const[hint0 + m[1] % 4], else generic.
  * PF_VK_KECCAK: const[hint0] + ((r[0..3] & (2^117 - 1)) << 6).
  * PF_VK_SMALL: r[0] % (hint0 + 1).   PF_VK_BOOL: r[0] & 1.

@@ -227,6 +227,7 @@ int pf_batch_create(const uint32_t* code, size_t n_ins, const uint32_t* consts, 
     for (size_t s = 0; s < n_sets; s++) {
         const pf_set_desc& d = descs[s];
         uint32_t wdef = 1u << PF_W_SINK, bdef = 0u;
+        uint64_t sdef = 0ull;
         for (uint32_t i = 0; i < d.n_ins; i++) {
             uint32_t* I = code_fixed.data() + 4 * ((size_t)d.code_off + i);
             const uint32_t op = I[0] & 0xffu, tr = pf_op_traffic(op);
@@ -236,13 +237,19 @@ int pf_batch_create(const uint32_t* code, size_t n_ins, const uint32_t* consts, 
             if ((tr & PF_TR_WW) && rd >= PF_NW) return fail("set %zu ins %u: W dst %u", s, i, rd);
             if (((tr & PF_TR_RA) && !(wdef >> (ra & 15u) & 1u)) || ((tr & PF_TR_RB) && !(wdef >> (rb & 15u) & 1u)))
                 return fail("set %zu ins %u: W register read before write", s, i);
-            const bool bres = op >= PF_B_CONST && op <= PF_B_UMUL_NOOVF;
+            const bool bres = PF_OP_WRITES_B(op);
             const bool breads_ab = op >= PF_B_AND && op <= PF_B_XOR;
             if ((breads_ab && (!(bdef >> (ra & 31u) & 1u) || !(bdef >> (rb & 31u) & 1u))) ||
-                ((op == PF_B_NOT || op == PF_ASSERT) && !(bdef >> (ra & 31u) & 1u)) ||
+                ((op == PF_B_NOT || op == PF_ASSERT || op == PF_B_SPILL) && !(bdef >> (ra & 31u) & 1u)) ||
                 ((op == PF_W_ITE || op == PF_B_ITE) && !(bdef >> (rc & 31u) & 1u)) ||
                 (op == PF_B_ITE && (!(bdef >> (ra & 31u) & 1u) || !(bdef >> (rb & 31u) & 1u))))
                 return fail("set %zu ins %u: B register read before write", s, i);
+            if ((op == PF_W_SPILL || op == PF_W_FILL || op == PF_B_SPILL || op == PF_B_FILL) &&
+                I[2] >= PF_MAX_SPILL)
+                return fail("set %zu ins %u: spill slot %u >= %d", s, i, I[2], PF_MAX_SPILL);
+            if (op == PF_W_SPILL || op == PF_B_SPILL) sdef |= 1ull << I[2];
+            if ((op == PF_W_FILL || op == PF_B_FILL) && !(sdef >> I[2] & 1ull))
+                return fail("set %zu ins %u: spill slot %u filled before it was spilled", s, i, I[2]);
             if (tr & PF_TR_WW) wdef |= 1u << rd;
             if (bres) bdef |= 1u << (rd & 31u);
         }

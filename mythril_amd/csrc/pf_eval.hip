@@ -123,9 +123,17 @@ PF_INL u256 gen_var(const SetCtx& S, uint32_t v, uint32_t cand) {
         maskw(out, w);
         return out;
     }
+    uint4 m = philox(make_uint4(cand, v, 2u, 0u), S.k0, S.k1);
+    if (pslot != PF_NO_PARENT && (cand & 1u) && (m.w & ((4u << ((cand >> 1) & 3u)) - 1u)) != 0u) {
+        // neighbourhood candidate of the parent model: keep the parent value
+        const uint32_t* p = S.parents + (size_t)pslot * 8u;
+#pragma unroll
+        for (int i = 0; i < 8; i++) out.l[i] = p[i];
+        maskw(out, w);
+        return out;
+    }
     uint4 r0 = philox(make_uint4(cand, v, 0u, 0u), S.k0, S.k1);
     uint4 r1 = philox(make_uint4(cand, v, 1u, 0u), S.k0, S.k1);
-    uint4 m = philox(make_uint4(cand, v, 2u, 0u), S.k0, S.k1);
     u256 rv;
     rv.l[0] = r0.x; rv.l[1] = r0.y; rv.l[2] = r0.z; rv.l[3] = r0.w;
     rv.l[4] = r1.x; rv.l[5] = r1.y; rv.l[6] = r1.z; rv.l[7] = r1.w;
@@ -247,6 +255,9 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
     v16u W[8];
     // the 32 bool registers are the bits of one VGPR (bit r = B register r)
     uint32_t Bk = 0u;
+    // spill slots (lowering under register pressure): dynamically indexed, so the compiler
+    // keeps them in private scratch memory, never in the VGPR banks
+    uint32_t spill[PF_MAX_SPILL * 8];
 #define BGET(r) ((Bk >> ((r) & 31u)) & 1u)
     uint32_t root = 1u;
     uint64_t cost = 0;
@@ -382,6 +393,8 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
                     case PF_B_XOR: bres = BGET(a) ^ BGET(b); break;
                     case PF_B_NOT: bres = BGET(a) ^ 1u; break;
                     case PF_B_ITE: bres = BGET(c) ? BGET(a) : BGET(b); break;
+                    case PF_B_FILL: bres = spill[(aux & (PF_MAX_SPILL - 1u)) * 8u] & 1u; break;
+                    case PF_B_SPILL: spill[(aux & (PF_MAX_SPILL - 1u)) * 8u] = BGET(a); break;
                     default:  // PF_ASSERT
                         root &= BGET(a);
                         if ((flags & PF_FLAG_SHORTCIRCUIT) && __ballot(root && active) == 0ull)
@@ -412,6 +425,15 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
                         break;
                     }
                     case PF_W_MOV: z = x; break;
+                    case PF_W_SPILL:
+#pragma unroll
+                        for (int i = 0; i < 8; i++) spill[(aux & (PF_MAX_SPILL - 1u)) * 8u + i] = x.l[i];
+                        z = x;
+                        break;
+                    case PF_W_FILL:
+#pragma unroll
+                        for (int i = 0; i < 8; i++) z.l[i] = spill[(aux & (PF_MAX_SPILL - 1u)) * 8u + i];
+                        break;
                     case PF_W_NOT: z = pf::not256(x); break;
                     case PF_W_NEG: z = pf::neg256(x); break;
                     case PF_W_SEXT: z = sextw(x, aux); break;
@@ -436,7 +458,7 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
             const uint32_t dd = (tr & PF_TR_WW) ? (d & 15u) : (uint32_t)PF_W_SINK;
             WR_W(W, dd, z);
         }
-        if (op >= PF_B_CONST && op <= PF_B_UMUL_NOOVF) {
+        if (PF_OP_WRITES_B(op)) {
             const uint32_t bit = 1u << (d & 31u);
             Bk = (Bk & ~bit) | (bres ? bit : 0u);
         }

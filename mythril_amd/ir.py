@@ -20,6 +20,7 @@ NW = 15  # usable W registers; register 15 is the kernel's write sink
 NB = 32
 LIMBS = 8
 MAX_WIDTH = 256
+MAX_SPILL = 64   # spill slots per lane (PF_MAX_SPILL)
 NO_PARENT = 0xFFFFFFFF
 
 # ---- opcodes (pf_bytecode.h enum pf_opcode) ------------------------------------
@@ -49,6 +50,8 @@ W_CONCAT = 22
 W_SEXT = 23
 W_ITE = 24
 W_HASH = 25
+W_SPILL = 26
+W_FILL = 27
 B_CONST = 40
 B_VAR = 41
 B_EQ = 42
@@ -63,6 +66,8 @@ B_NOT = 50
 B_ITE = 51
 B_UADD_NOOVF = 52
 B_UMUL_NOOVF = 53
+B_FILL = 54
+B_SPILL = 55
 ASSERT = 60
 
 OPNAMES = {v: k for k, v in dict(globals()).items()
@@ -209,6 +214,7 @@ class Program:
 
     def validate(self) -> None:
         """Host-side shape check run before anything is launched (kernel assumes these)."""
+        spilled = set()
         for i, ins in enumerate(self.code):
             if ins.op not in OPNAMES:
                 raise ValueError(f"ins {i}: unknown opcode {ins.op}")
@@ -225,14 +231,27 @@ class Program:
                 raise ValueError(f"ins {i}: variable {ins.aux0} out of range")
             if ins.op == W_CONST and ins.aux0 >= len(self.consts):
                 raise ValueError(f"ins {i}: constant {ins.aux0} out of range")
+            if ins.op in (W_SPILL, W_FILL, B_SPILL, B_FILL):
+                if ins.aux0 >= MAX_SPILL:
+                    raise ValueError(f"ins {i}: spill slot {ins.aux0} >= {MAX_SPILL}")
+                if ins.op in (W_SPILL, B_SPILL):
+                    spilled.add(ins.aux0)
+                elif ins.aux0 not in spilled:
+                    raise ValueError(f"ins {i}: spill slot {ins.aux0} filled before it was spilled")
         if not self.code or self.code[-1].op != END:
             raise ValueError("program must end with END")
 
 
 def _reg_classes(op):
     """(W registers used, B registers used) of an instruction, as accessor functions."""
-    if op in (W_CONST, W_VAR):
+    if op in (W_CONST, W_VAR, W_FILL):
         return (lambda i: (i.dst,)), (lambda i: ())
+    if op == W_SPILL:
+        return (lambda i: (i.a,)), (lambda i: ())
+    if op == B_FILL:
+        return (lambda i: ()), (lambda i: (i.dst,))
+    if op == B_SPILL:
+        return (lambda i: ()), (lambda i: (i.a,))
     if op in W_UNARY or op in (W_EXTRACT, W_SEXT):
         return (lambda i: (i.dst, i.a)), (lambda i: ())
     if op in W_BINARY or op == W_CONCAT:

@@ -101,8 +101,23 @@ class Dag:
 _LEAF_KINDS = (K_VAR, K_CONST, K_BCONST, K_BVAR)
 
 
+def _subtree_sizes(dag: Dag) -> List[int]:
+    """Interior nodes below each node (shared subterms counted once per path, capped)."""
+    size = [0] * len(dag.nodes)
+    for i, n in enumerate(dag.nodes):   # topological: operands come first
+        if n.kind not in _LEAF_KINDS:
+            size[i] = min(1 + sum(size[a] for a in n.args), 1 << 20)
+    return size
+
+
 def _emission_order(dag: Dag) -> List[Tuple[str, int]]:
-    """Post-order per root (roots in order); ('node', i) and ('assert', i) events."""
+    """Post-order per root (roots in order); ('node', i) and ('assert', i) events.
+
+    Operands are visited largest subtree first (Sethi-Ullman): the small operand is then
+    computed right before its use instead of being held live across the big one.  That is
+    what keeps an ``ite`` chain (an array read checked against every earlier index,
+    mythril_amd/smt/to_dag.py) at two live values instead of one per link."""
+    size = _subtree_sizes(dag)
     seen = set()
     events: List[Tuple[str, int]] = []
     for r in dag.roots:
@@ -120,7 +135,8 @@ def _emission_order(dag: Dag) -> List[Tuple[str, int]]:
             if i in seen:
                 continue
             stack.append((i, True))
-            for a in reversed(n.args):
+            # the stack pops the last push first: push the smallest operand first
+            for a in sorted(n.args, key=lambda x: size[x]):
                 if dag.nodes[a].kind not in _LEAF_KINDS and a not in seen:
                     stack.append((a, False))
         events.append(("assert", r))
@@ -135,16 +151,21 @@ class _RegFile:
         self.holder: Dict[int, int] = {}   # reg -> node
         self.where: Dict[int, int] = {}    # node -> reg
 
-    def alloc(self, node: int, evict_rank, pinned) -> int:
-        """Take a free register, else evict the cheapest-to-restore value (evict_rank)."""
+    def alloc(self, node: int, evict_rank, pinned, spill=None, far=None) -> int:
+        """Take a free register, else evict the cheapest-to-restore value (evict_rank),
+        else spill the value used farthest in the future (spill(reg, node) emits it)."""
         if self.free:
             r = self.free.pop()
         else:
             cands = [(evict_rank(nd), rg) for rg, nd in self.holder.items() if rg not in pinned]
             cands = [c for c in cands if c[0] is not None]
-            if not cands:
-                raise LoweringError(f"more than {self.n} live {self.cls} values")
-            _, r = min(cands)
+            if cands:
+                _, r = min(cands)
+            else:
+                victims = [(far(nd), rg) for rg, nd in self.holder.items() if rg not in pinned]
+                if not victims or spill is None or not spill(max(victims)[1], self.holder[max(victims)[1]]):
+                    raise LoweringError(f"more than {self.n} live {self.cls} values")
+                r = max(victims)[1]
             old = self.holder.pop(r)
             del self.where[old]
         self.holder[r] = node
@@ -210,15 +231,41 @@ def lower(dag: Dag, seed: int = 0, name: str = "") -> Program:
 
     W = _RegFile(ir.NW, "W")
     B = _RegFile(ir.NB, "B")
+    # spill slots (PF_W_SPILL / PF_B_SPILL): values that can neither stay resident nor be
+    # recomputed cheaply; a spilled value keeps its slot until its last use, so evicting
+    # it again costs nothing and restoring it is one fill
+    slot_of: Dict[int, int] = {}
+    free_slots = list(range(ir.MAX_SPILL - 1, -1, -1))
 
     def rank(t):
         def f(nd):
-            sz = remat_size(nd)
+            sz = 1 if nd in slot_of else remat_size(nd)
             if sz is None:
                 return None
             # cheapest restore first, then farthest next use (Belady)
             return (sz, -next_use(nd, t))
         return f
+
+    def spill(rg: int, nd: int) -> bool:
+        if not free_slots:
+            return False
+        s = free_slots.pop()
+        n = dag.nodes[nd]
+        if n.is_bool:
+            prog.emit(ir.B_SPILL, 1, a=rg, aux0=s)
+        else:
+            prog.emit(ir.W_SPILL, n.width, a=rg, aux0=s)
+        slot_of[nd] = s
+        return True
+
+    def alloc(rf, nd, t, pinned):
+        return rf.alloc(nd, rank(t), pinned, spill, lambda x: next_use(x, t))
+
+    def done(nd):
+        regfile(nd).release(nd)
+        s = slot_of.pop(nd, None)
+        if s is not None:
+            free_slots.append(s)
 
     def regfile(nd):
         return B if dag.nodes[nd].is_bool else W
@@ -227,7 +274,7 @@ def lower(dag: Dag, seed: int = 0, name: str = "") -> Program:
         n = dag.nodes[i]
         rf = regfile(i)
         if n.kind in _LEAF_KINDS:
-            r = rf.alloc(i, rank(t), pinned_b if n.is_bool else pinned_w)
+            r = alloc(rf, i, t, pinned_b if n.is_bool else pinned_w)
             if n.kind == K_VAR:
                 prog.emit(ir.W_VAR, n.width, dst=r, aux0=n.aux)
             elif n.kind == K_CONST:
@@ -246,9 +293,9 @@ def lower(dag: Dag, seed: int = 0, name: str = "") -> Program:
         # operands whose last use is this node may be reused as destination
         for a in set(n.args):
             if next_use(a, t) >= (1 << 30):
-                regfile(a).release(a)
+                done(a)
                 (pb if dag.nodes[a].is_bool else pw).discard(regs[n.args.index(a)])
-        dst = rf.alloc(i, rank(t), pb if n.is_bool else pw)
+        dst = alloc(rf, i, t, pb if n.is_bool else pw)
         op = n.kind
         if op in (ir.W_ITE, ir.B_ITE):      # args: cond(B), then, else
             prog.emit(op, n.width if op == ir.W_ITE else 1, dst=dst, a=regs[1], b=regs[2], c=regs[0])
@@ -262,6 +309,14 @@ def lower(dag: Dag, seed: int = 0, name: str = "") -> Program:
         rf = regfile(nd)
         if nd in rf.where:
             return rf.where[nd]
+        if nd in slot_of:
+            n = dag.nodes[nd]
+            r = alloc(rf, nd, t, pinned_b if n.is_bool else pinned_w)
+            if n.is_bool:
+                prog.emit(ir.B_FILL, 1, dst=r, aux0=slot_of[nd])
+            else:
+                prog.emit(ir.W_FILL, n.width, dst=r, aux0=slot_of[nd])
+            return r
         if dag.nodes[nd].kind not in _LEAF_KINDS and remat_size(nd) is None:
             raise LoweringError("non-rematerialisable value was evicted")
         return emit_node(nd, t, pinned_w, pinned_b)
@@ -271,13 +326,13 @@ def lower(dag: Dag, seed: int = 0, name: str = "") -> Program:
             rb = materialize(i, t, set(), set())
             prog.emit(ir.ASSERT, 1, a=rb)
             if next_use(i, t) >= (1 << 30):
-                B.release(i)
+                done(i)
             continue
-        if i in regfile(i).where:
+        if i in regfile(i).where or i in slot_of:
             continue  # already (re)computed as an operand of an earlier node
         emit_node(i, t, set(), set())
         if next_use(i, t) >= (1 << 30):
-            regfile(i).release(i)
+            done(i)
     prog.finish()
     prog.validate()
     return prog

@@ -1,33 +1,48 @@
 """Batched GPU feasibility for constraint sets given as terms.
 
 ``check_sets`` is the batched form of the reference's objective-free query path: every set
-(one LASER state's ``Constraints.get_all_constraints()``) is lowered, all sets go to the GPU
-in one ``pf_check_batch`` launch, and each witness is materialised into a model whose
-``eval`` agrees bit for bit with the kernel.  Sets that cannot be lowered, or have no
-witness among the candidates, return ``None`` — the caller then asks z3, unchanged.
+(one LASER state's ``Constraints.get_all_constraints()``) is split into independence
+buckets (mythril/laser/smt/solver/independence_solver.py:38-83, here
+mythril_amd/smt/independence.py), every distinct bucket is lowered once, given a
+constraint-directed hint model (mythril_amd/seed.py) and searched in ONE ``pf_check_batch``
+launch; each witness is materialised into a model whose ``eval`` agrees bit for bit with
+the kernel.  A set is SAT when all its buckets are; sets that cannot be lowered, or have a
+bucket without a witness among the candidates, return ``None`` — the caller then asks z3,
+unchanged.
+
+Bucket witnesses are cached by bucket (terms are hash-consed, so a bucket is its tuple of
+constraint terms): LASER's sets grow by appending constraints, so the tx-boundary and fork
+queries of one analysis share most buckets — the GPU-resident counterpart of the
+reference's ``ModelCache`` (support/support_utils.py:57-71), keyed by structure instead of
+re-evaluating up to 100 models per query.
 """
 
 from __future__ import annotations
 
 import threading
+from collections import OrderedDict
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence, Tuple
 
-from .. import ir
+from .. import ir, seed
 from ..lower import LoweringError, lower
+from .independence import buckets
 from .interp import Witness
 from .model import WitnessModel
 from . import terms as T
-from .to_dag import DEFAULT_REGISTRY, TermLowering, UFRegistry
+from .to_dag import DEFAULT_REGISTRY, Lowered, TermLowering, UFRegistry
 
 
 @dataclass
 class GpuConfig:
-    budget: int = 65536          # candidates per set
+    budget: int = 65536          # candidates per bucket
     seed: int = 0x4D595448       # global candidate seed
     flags: int = ir.FLAG_EARLY_EXIT | ir.FLAG_SHORTCIRCUIT
     timeout_ms: int = 0
     enabled: bool = True
+    split: bool = True           # independence buckets
+    hints: bool = True           # constraint-directed parent (hint) models
+    cache_size: int = 1 << 16    # bucket witnesses kept
 
 
 CONFIG = GpuConfig()
@@ -36,69 +51,136 @@ CONFIG = GpuConfig()
 @dataclass
 class GpuStats:
     sets: int = 0            # sets offered to the GPU
-    lowered: int = 0         # sets that lowered to bytecode
+    lowered: int = 0         # sets whose every bucket lowered to bytecode
     sat: int = 0             # sets discharged with a GPU witness
+    buckets: int = 0         # distinct buckets searched on the GPU
+    bucket_hits: int = 0     # buckets answered from the witness cache
     lowering_failures: Dict[str, int] = field(default_factory=dict)
     kernel_ms: float = 0.0
     evals: int = 0
+    host_s: float = 0.0      # lowering + hints + witness re-checks
 
 
 STATS = GpuStats()
 _lock = threading.Lock()
+_CACHE: "OrderedDict[tuple, Tuple[Lowered, List[int]]]" = OrderedDict()
+
+
+def reset_cache() -> None:
+    with _lock:
+        _CACHE.clear()
 
 
 def _set_seed(constraints: Sequence[T.Term]) -> int:
     h = 0
     for c in constraints:
-        h = (h * 1000003) ^ (hash(T.to_sexpr(c)) & 0xFFFFFFFF)
+        h = (h * 1000003) ^ T.struct_hash(c)
     return h & 0xFFFFFFFF
+
+
+def _lower_bucket(bucket: List[T.Term], reg: UFRegistry, parent: Optional[dict], hints: bool):
+    tl = TermLowering(reg, parent)
+    lo = tl.lower(bucket)
+    if hints:
+        seed.apply_hints(lo.dag)
+    return lo, lower(lo.dag, seed=_set_seed(bucket))
 
 
 def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] = None,
                parents: Optional[Sequence[Optional[dict]]] = None,
                config: Optional[GpuConfig] = None) -> List[Optional[WitnessModel]]:
+    import time
+
     from ..engine import get_engine  # the GPU is required from here on: no host fallback
 
     cfg = config or CONFIG
     reg = registry or DEFAULT_REGISTRY
+    t0 = time.perf_counter()
     out: List[Optional[WitnessModel]] = [None] * len(sets)
-    progs, lows, idx = [], [], []
+    set_buckets: List[Optional[List[tuple]]] = []
+    found: Dict[tuple, Optional[Tuple[Lowered, List[int]]]] = {}   # bucket key -> witness
+    todo: Dict[tuple, int] = {}                                     # bucket key -> program idx
+    progs, lows, keys = [], [], []
+    n_lowered = hits = 0
+    # the keccak interpretation depends on the registry (intervals, concrete hashes): a
+    # cached witness is only valid for the registry state it was found under
+    reg_sig = tuple(sorted((n, s.lo, len(s.concrete)) for n, s in reg.keccak.items()))
     for i, cs in enumerate(sets):
-        cs = list(cs)
+        cs = [c for c in cs if c is not T.TRUE]
         if any(c is T.FALSE for c in cs):
+            set_buckets.append(None)
             continue
-        try:
-            tl = TermLowering(reg, parents[i] if parents else None)
-            lo = tl.lower(cs)
-            prog = lower(lo.dag, seed=_set_seed(cs))
-        except LoweringError as e:
-            key = str(e).split(":")[0][:60]
-            with _lock:
-                STATS.lowering_failures[key] = STATS.lowering_failures.get(key, 0) + 1
+        parent = parents[i] if parents else None
+        bks = buckets(cs) if cfg.split else [cs]
+        ks, ok = [], True
+        for b in bks:
+            key = (tuple(b), tuple(sorted(parent.items())) if parent else None, reg_sig)
+            ks.append(key)
+            if key in found or key in todo:
+                continue
+            cached = _CACHE.get(key)
+            if cached is not None:
+                found[key] = cached
+                hits += 1
+                continue
+            try:
+                lo, prog = _lower_bucket(b, reg, parent, cfg.hints)
+            except LoweringError as e:
+                err = str(e).split(":")[0][:60]
+                with _lock:
+                    STATS.lowering_failures[err] = STATS.lowering_failures.get(err, 0) + 1
+                found[key] = None
+                ok = False
+                continue
+            todo[key] = len(progs)
+            progs.append(prog)
+            lows.append(lo)
+            keys.append(key)
+        if ok and all(found.get(k, 0) is not None for k in ks):
+            n_lowered += 1
+        set_buckets.append(ks)
+
+    res = None
+    if progs:
+        eng = get_engine()
+        db = eng.upload(progs)
+        res = eng.check(db, budget=cfg.budget, seed=cfg.seed, flags=cfg.flags, timeout_ms=cfg.timeout_ms)
+        sat = [k for k in range(len(progs)) if res.found[k] != 0xFFFFFFFF]
+        vals = eng.materialize(db, sat, [int(res.found[k]) for k in sat], seed=cfg.seed) if sat else []
+        db.free()
+        for k in range(len(progs)):
+            found[keys[k]] = None
+        for k, v in zip(sat, vals):
+            key = keys[k]
+            w = Witness(lows[k], v, reg)
+            # re-check on the host under the same interpretation before trusting it
+            if all(w.ev(c) for c in key[0]):
+                found[key] = (lows[k], v)
+                with _lock:
+                    _CACHE[key] = (lows[k], v)
+                    while len(_CACHE) > cfg.cache_size:
+                        _CACHE.popitem(last=False)
+
+    n_sat = 0
+    for i, ks in enumerate(set_buckets):
+        if ks is None:
             continue
-        progs.append(prog)
-        lows.append(lo)
-        idx.append(i)
+        parts = [found.get(k) for k in ks]
+        if any(p is None for p in parts):
+            continue
+        w = Witness.union([Witness(lo, v, reg) for lo, v in parts], reg)
+        cs = [c for c in sets[i] if c is not T.TRUE]
+        if all(w.ev(c) for c in cs):
+            out[i] = WitnessModel(w, list(sets[i]))
+            n_sat += 1
     with _lock:
         STATS.sets += len(sets)
-        STATS.lowered += len(progs)
-    if not progs:
-        return out
-    eng = get_engine()
-    db = eng.upload(progs)
-    res = eng.check(db, budget=cfg.budget, seed=cfg.seed, flags=cfg.flags, timeout_ms=cfg.timeout_ms)
-    sat = [k for k in range(len(progs)) if res.found[k] != 0xFFFFFFFF]
-    if sat:
-        vals = eng.materialize(db, sat, [int(res.found[k]) for k in sat], seed=cfg.seed)
-        for k, v in zip(sat, vals):
-            i = idx[k]
-            w = Witness(lows[k], v, reg)
-            # re-check on the host under the same interpretation before handing it out
-            if all(w.ev(c) for c in sets[i]):
-                out[i] = WitnessModel(w, list(sets[i]))
-    db.free()
-    with _lock:
-        STATS.sat += sum(1 for m in out if m is not None)
-        STATS.kernel_ms += res.kernel_ms
-        STATS.evals += res.cands_decided
+        STATS.lowered += n_lowered
+        STATS.sat += n_sat
+        STATS.buckets += len(progs)
+        STATS.bucket_hits += hits
+        if res is not None:
+            STATS.kernel_ms += res.kernel_ms
+            STATS.evals += res.cands_decided
+        STATS.host_s += time.perf_counter() - t0 - (res.kernel_ms / 1e3 if res is not None else 0.0)
     return out

@@ -73,6 +73,25 @@ class Witness:
         self._tables: Optional[Dict[str, Dict[int, int]]] = None
         self._keccak_tables: Dict[int, List[Tuple[int, int]]] = {}
 
+    @classmethod
+    def union(cls, parts: List["Witness"], registry: Optional[UFRegistry] = None) -> "Witness":
+        """One witness from the witnesses of variable-disjoint buckets
+        (mythril_amd/smt/independence.py): symbols, arrays and keccak families never span
+        two buckets, so the interpretations merge without overlap."""
+        if len(parts) == 1:
+            return parts[0]
+        w = cls.__new__(cls)
+        w.reg = registry if registry is not None else (parts[0].reg if parts else None)
+        w.vars, w.bools, w.reads, w.array_reads, w.uf_apps = {}, {}, {}, {}, []
+        for p in parts:
+            w.vars.update(p.vars)
+            w.bools.update(p.bools)
+            w.reads.update(p.reads)
+            w.array_reads.update(p.array_reads)
+            w.uf_apps.extend(p.uf_apps)
+        w._memo, w._tables, w._keccak_tables = {}, None, {}
+        return w
+
     # ---- array interpretation: first earlier index with an equal value ------------------
     def tables(self) -> Dict[str, Dict[int, int]]:
         if self._tables is None:

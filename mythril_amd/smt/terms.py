@@ -298,6 +298,35 @@ def apply(fname: str, rng: int, *args: Term) -> Term:
     return Term("apply", bv_sort(rng), tuple(args), (fname, tuple(a.width for a in args)))
 
 
+# ---- structural hash (stable across processes, unlike Term.__hash__) --------------------
+_SHASH: Dict[Term, int] = {}
+
+
+def struct_hash(t: Term) -> int:
+    """32-bit hash of the term's structure (op, sort, value, operands), memoised."""
+    import zlib
+
+    r = _SHASH.get(t)
+    if r is not None:
+        return r
+    stack = [t]
+    while stack:
+        x = stack[-1]
+        if x in _SHASH:
+            stack.pop()
+            continue
+        pend = [a for a in x.args if a not in _SHASH]
+        if pend:
+            stack.extend(pend)
+            continue
+        stack.pop()
+        h = zlib.crc32(repr((x.op, x.sort, x.val)).encode())
+        for a in x.args:
+            h = zlib.crc32(_SHASH[a].to_bytes(4, "little"), h)
+        _SHASH[x] = h
+    return _SHASH[t]
+
+
 # ---- printing (SMT-LIB2-ish, for sexpr()/--solver-log style dumps) --------------------
 
 def to_sexpr(t: Term, _memo: Optional[dict] = None) -> str:

@@ -72,10 +72,11 @@ def get_model(constraints, minimize=(), maximize=(), solver_timeout=None):
     raise UnsatError
 
 
-def get_models(constraint_sets: Sequence, parents: Optional[Sequence[Optional[dict]]] = None
-               ) -> List[Optional[Model]]:
+def get_models(constraint_sets: Sequence, parents: Optional[Sequence[Optional[dict]]] = None,
+               registry=None) -> List[Optional[Model]]:
     """Objective-free feasibility of many sets in ONE GPU batch (tx-boundary pruning,
-    svm.py:279-283).  ``None`` = no GPU witness (ask z3 / treat as the reference would)."""
+    svm.py:279-283).  ``None`` = no GPU witness (ask z3 / treat as the reference would).
+    ``registry``: the keccak interpretation (defaults to the global keccak manager's)."""
     raws = []
     for cs in constraint_sets:
         try:
@@ -84,7 +85,7 @@ def get_models(constraint_sets: Sequence, parents: Optional[Sequence[Optional[di
             raws.append([T.FALSE])
     stats = SolverStatistics()
     stats.gpu_attempts += len(raws)
-    internals = check_sets(raws, parents=parents)
+    internals = check_sets(raws, registry=registry, parents=parents)
     out = []
     for m in internals:
         if m is None:

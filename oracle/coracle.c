@@ -157,6 +157,8 @@ static v256 gen(const SetV* S, uint32_t v, uint32_t cand, uint64_t gseed) {
     uint32_t c0[4] = {cand, v, 0, 0}, c1[4] = {cand, v, 1, 0}, c2[4] = {cand, v, 2, 0};
     philox(c0, k0, k1); philox(c1, k0, k1); philox(c2, k0, k1);
     memcpy(r, c0, 16); memcpy(r + 4, c1, 16); memcpy(m, c2, 16);
+    if (slot != 0xffffffffu && (cand & 1u) && (m[3] & ((4u << ((cand >> 1) & 3u)) - 1u)) != 0u)
+        return andv(from32(S->parents + 8 * (size_t)slot), M); /* neighbourhood candidate */
     v256 rv = from32(r), out;
     if (kind == 2) { /* keccak slot */
         v256 k = Z();
@@ -201,8 +203,9 @@ static v256 gen(const SetV* S, uint32_t v, uint32_t cand, uint64_t gseed) {
 
 /* values: optional explicit assignment [n_vars] (NULL = generate candidate cand) */
 static int eval_one(const SetV* S, const v256* values, uint32_t cand, uint64_t gseed) {
-    v256 W[16];
+    v256 W[16], SP[64]; /* SP: spill slots (PF_W_SPILL / PF_W_FILL / PF_B_SPILL / PF_B_FILL) */
     uint8_t B[32];
+    memset(SP, 0, sizeof SP);
     memset(W, 0, sizeof W);
     memset(B, 0, sizeof B);
     int root = 1;
@@ -254,6 +257,8 @@ static int eval_one(const SetV* S, const v256* values, uint32_t cand, uint64_t g
                 W[d] = andv(from32(o), M);
                 break;
             }
+            case 26: SP[I[2] & 63] = x; break;
+            case 27: W[d] = andv(SP[I[2] & 63], M); break;
             case 40: B[d] = I[2] & 1; break;
             case 41: B[d] = (uint8_t)((values ? values[I[2]] : gen(S, I[2], cand, gseed)).w[0] & 1); break;
             case 42: B[d] = eqv(x, y); break;
@@ -272,6 +277,8 @@ static int eval_one(const SetV* S, const v256* values, uint32_t cand, uint64_t g
             case 51: B[d] = B[c] ? B[a] : B[b]; break;
             case 52: { int cy; v256 s = addv(x, y, &cy); B[d] = !cy && eqv(andv(s, M), s); break; }
             case 53: { v256 p = mulv(x, y, &ov); B[d] = !ov && eqv(andv(p, M), p); break; }
+            case 54: B[d] = (uint8_t)(SP[I[2] & 63].w[0] & 1); break;
+            case 55: SP[I[2] & 63] = Z(); SP[I[2] & 63].w[0] = B[a]; break;
             case 60: root &= B[a]; break;
             default: return -1;
         }

@@ -287,6 +287,9 @@ def gen_values(cands: np.ndarray, var_index: int, schema: Sequence[int], consts:
         if c == 0 and parent is not None:
             out.append(parent & M(w))
             continue
+        if parent is not None and (c & 1) and (mi[3] & ((4 << ((c >> 1) & 3)) - 1)) != 0:
+            out.append(parent & M(w))  # neighbourhood candidate of the parent model
+            continue
         rv = sum(x << (32 * j) for j, x in enumerate(ri))
         if kind == VK_KECCAK:
             lo = consts[hint0]
@@ -331,9 +334,9 @@ def gen_values(cands: np.ndarray, var_index: int, schema: Sequence[int], consts:
 OP = dict(END=0, W_CONST=1, W_VAR=2, W_MOV=3, W_ADD=4, W_SUB=5, W_MUL=6, W_UDIV=7, W_UREM=8,
           W_SDIV=9, W_SREM=10, W_SMOD=11, W_AND=12, W_OR=13, W_XOR=14, W_NOT=15, W_NEG=16,
           W_SHL=17, W_LSHR=18, W_ASHR=19, W_EXP=20, W_EXTRACT=21, W_CONCAT=22, W_SEXT=23,
-          W_ITE=24, W_HASH=25, B_CONST=40, B_VAR=41, B_EQ=42, B_ULT=43, B_ULE=44, B_SLT=45, B_SLE=46,
+          W_ITE=24, W_HASH=25, W_SPILL=26, W_FILL=27, B_CONST=40, B_VAR=41, B_EQ=42, B_ULT=43, B_ULE=44, B_SLT=45, B_SLE=46,
           B_AND=47, B_OR=48, B_XOR=49, B_NOT=50, B_ITE=51, B_UADD_NOOVF=52, B_UMUL_NOOVF=53,
-          ASSERT=60)
+          B_FILL=54, B_SPILL=55, ASSERT=60)
 
 _WBIN = {
     OP["W_ADD"]: bvadd, OP["W_SUB"]: bvsub, OP["W_MUL"]: bvmul, OP["W_UDIV"]: bvudiv,
@@ -386,6 +389,7 @@ class SetView:
         """Evaluate the conjunction under one assignment (values indexed by variable)."""
         W: Dict[int, int] = {}
         B: Dict[int, bool] = {}
+        S: Dict[int, int] = {}   # spill slots
         root = True
         for (w0, w1, aux0, aux1) in self.code:
             op, w = w0 & 0xFF, (w0 >> 8) & 0x3FF
@@ -414,6 +418,14 @@ class SetView:
                 W[d] = W[a] if B[c] else W[b]
             elif op == OP["W_HASH"]:
                 W[d] = uf_hash(W[a], aux0) & M(w)
+            elif op == OP["W_SPILL"]:
+                S[aux0] = W[a]
+            elif op == OP["W_FILL"]:
+                W[d] = S[aux0] & M(w)
+            elif op == OP["B_SPILL"]:
+                S[aux0] = int(B[a])
+            elif op == OP["B_FILL"]:
+                B[d] = bool(S[aux0] & 1)
             elif op == OP["B_CONST"]:
                 B[d] = bool(aux0 & 1)
             elif op == OP["B_VAR"]:

@@ -1,5 +1,8 @@
 """CPU: lowering preserves the conjunction's value (term-level oracle == bytecode oracle)."""
 
+import random
+
+import coracle_py
 import numpy as np
 import pyoracle as O
 import pytest
@@ -53,6 +56,45 @@ def test_remat_under_pressure():
     _programs_agree(dag, prog, n=8)
 
 
+def _pressure_dag(n):
+    """n products, each used twice far apart: more than 15 live W values at once."""
+    dag = Dag()
+    ys = [dag.var(f"y{i}", 256) for i in range(n)]
+    ps = [dag.op(ir.W_MUL, 256, ys[i], ys[i]) for i in range(n)]
+    a1 = ps[0]
+    for p in ps[1:]:
+        a1 = dag.op(ir.W_ADD, 256, a1, p)
+    a2 = ps[-1]
+    for p in reversed(ps[:-1]):
+        a2 = dag.op(ir.W_XOR, 256, a2, p)
+    dag.assert_(dag.op(ir.B_EQ, 256, a1, a2))
+    return dag
+
+
+def test_register_pressure_spills_and_evaluates():
+    """More live values than registers: the lowering spills (PF_W_SPILL / PF_W_FILL) and
+    the bytecode still computes the DAG's value (oracle evaluation of the program)."""
+    dag = _pressure_dag(20)
+    prog = lower(dag)
+    ops = [i.op for i in prog.code]
+    assert ir.W_SPILL in ops and ir.W_FILL in ops
+    b = ir.Batch([prog])
+    sv = O.SetView.from_batch(b, 0)
+    rng = random.Random(5)
+    for _ in range(20):
+        vals = [rng.getrandbits(256) for _ in dag.vars]
+        assert sv.evaluate(vals) == bool(eval_dag(dag, vals))
+    P = coracle_py.Packed(b)
+    cands = sv.gen_assignments(np.arange(64, dtype=np.uint64), 3)
+    want = np.array([sv.evaluate(a) for a in cands])
+    assert (P.eval_generated(0, 3, 0, 64) == want).all()
+
+
+def test_beyond_spill_capacity_rejected():
+    with pytest.raises(LoweringError):
+        lower(_pressure_dag(ir.NW + ir.MAX_SPILL + 4))
+
+
 def test_too_many_live_values_rejected():
     dag = Dag()
     xs = [dag.var(f"x{i}", 256) for i in range(20)]
@@ -63,19 +105,8 @@ def test_too_many_live_values_rejected():
     # all products computed first would need 20 live registers; post-order avoids that
     dag.assert_(dag.op(ir.B_EQ, 256, acc, dag.const(0, 256)))
     lower(dag)  # fine in post-order
-    # a DAG whose products are each used twice, far apart, cannot stay within 15 registers
-    dag2 = Dag()
-    ys = [dag2.var(f"y{i}", 256) for i in range(20)]
-    ps = [dag2.op(ir.W_MUL, 256, ys[i], ys[i]) for i in range(20)]
-    a1 = ps[0]
-    for p in ps[1:]:
-        a1 = dag2.op(ir.W_ADD, 256, a1, p)
-    a2 = ps[-1]
-    for p in reversed(ps[:-1]):
-        a2 = dag2.op(ir.W_XOR, 256, a2, p)
-    dag2.assert_(dag2.op(ir.B_EQ, 256, a1, a2))
-    with pytest.raises(LoweringError):
-        lower(dag2)
+    # a DAG whose products are each used twice, far apart, cannot stay within 15 registers:
+    # it spills (test_register_pressure_spills_and_evaluates)
 
 
 def test_mythril_like_lowers():
