@@ -17,7 +17,7 @@ and is left to z3 (the engine never guesses).
 from __future__ import annotations
 
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple  # noqa: F401
 
 from . import ir
 from .ir import Ins, Program, Var
@@ -86,8 +86,88 @@ class Dag:
 
     # ---- interior ------------------------------------------------------------------
     def op(self, opcode: int, width: int, *args: int, aux: int = 0) -> int:
+        r = self._simplify(opcode, width, args, aux)
+        if r is not None:
+            return r
         is_bool = opcode >= ir.B_CONST
         return self.add(opcode, width, args, aux, is_bool)
+
+    def _cval(self, i: int) -> Optional[int]:
+        n = self.nodes[i]
+        return n.aux if n.kind == K_CONST else None
+
+    def _simplify(self, op: int, w: int, args, aux) -> Optional[int]:
+        """Word-slicing rewrites z3.simplify applies to every stored constraint
+        (constraints.py:60-70): selector and address extraction from a CALLDATALOAD word
+        (a 32-byte concat, calldata.py:233-246) keep only the bytes they read, so the
+        program and the hint derivation see 4 / 20 byte variables instead of 32."""
+        nodes = self.nodes
+        if op == ir.W_UDIV:                       # x / 2^k -> x >> k
+            c = self._cval(args[1])
+            if c is not None and c and c & (c - 1) == 0:
+                k = c.bit_length() - 1
+                return args[0] if k == 0 else self.op(ir.W_LSHR, w, args[0], self.const(k, w))
+        elif op == ir.W_LSHR:
+            k = self._cval(args[1])
+            x = nodes[args[0]]
+            if k is not None and k < w:
+                if k == 0:
+                    return args[0]
+                if x.kind == ir.W_MOV:                # zero-extended: shift the inner value
+                    inner = x.args[0]
+                    wi = nodes[inner].width
+                    if k >= wi:
+                        return self.const(0, w)
+                    return self.op(ir.W_MOV, w, self.op(ir.W_EXTRACT, wi - k, inner, aux=k))
+                if x.kind == ir.W_CONCAT:
+                    return self.op(ir.W_MOV, w, self.op(ir.W_EXTRACT, w - k, args[0], aux=k))
+        elif op == ir.W_AND:
+            for xi, ci in ((0, 1), (1, 0)):
+                c = self._cval(args[ci])
+                if c is not None and c and (c + 1) & c == 0 and c.bit_length() < w:
+                    k = c.bit_length()                # x & (2^k - 1) -> zext(x[k-1:0])
+                    return self.op(ir.W_MOV, w, self.op(ir.W_EXTRACT, k, args[xi], aux=0))
+        elif op == ir.W_EXTRACT:
+            x = nodes[args[0]]
+            if aux == 0 and w == x.width:
+                return args[0]
+            if x.kind == ir.W_CONCAT:
+                hi, lo = x.args
+                wl = x.aux
+                if aux >= wl:
+                    return self.op(ir.W_EXTRACT, w, hi, aux=aux - wl)
+                if aux + w <= wl:
+                    return self.op(ir.W_EXTRACT, w, lo, aux=aux)
+                top = self.op(ir.W_EXTRACT, aux + w - wl, hi, aux=0)
+                bot = self.op(ir.W_EXTRACT, wl - aux, lo, aux=aux)
+                return self.op(ir.W_CONCAT, w, top, bot, aux=wl - aux)
+            if x.kind == ir.W_MOV:
+                inner = x.args[0]
+                wi = nodes[inner].width
+                if aux + w <= wi:
+                    return self.op(ir.W_EXTRACT, w, inner, aux=aux)
+                if aux >= wi:
+                    return self.const(0, w)
+            if x.kind == K_CONST:
+                return self.const(x.aux >> aux, w)
+        elif op == ir.W_MOV:
+            x = nodes[args[0]]
+            if x.width == w:
+                return args[0]
+            if x.kind == ir.W_MOV:
+                return self.op(ir.W_MOV, w, x.args[0])
+            if x.kind == K_CONST:
+                return self.const(x.aux, w)
+        elif op == ir.B_EQ:
+            for xi, ci in ((0, 1), (1, 0)):
+                c = self._cval(args[ci])
+                x = nodes[args[xi]]
+                if c is not None and x.kind == ir.W_MOV:   # zext(y) == c  ->  y == c  (or false)
+                    wy = nodes[x.args[0]].width
+                    if c >> wy:
+                        return self.bconst(False)
+                    return self.op(ir.B_EQ, wy, x.args[0], self.const(c, wy))
+        return None
 
     def assert_(self, b: int) -> None:
         if not self.nodes[b].is_bool:

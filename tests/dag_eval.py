@@ -23,6 +23,12 @@ _B = {
 
 
 def eval_dag(dag, values):
+    val = eval_dag_values(dag, values)
+    return all(val[r] for r in dag.roots)
+
+
+def eval_dag_values(dag, values):
+    """Value of every node."""
     val = {}
     for i, n in enumerate(dag.nodes):
         k, w = n.kind, n.width
@@ -67,5 +73,5 @@ def eval_dag(dag, values):
         else:
             raise ValueError(k)
         val[i] = v
-    return all(val[r] for r in dag.roots)
+    return val
 

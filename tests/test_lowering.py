@@ -114,3 +114,59 @@ def test_mythril_like_lowers():
         p = synth.mythril_like_set(i)
         p.validate()
         assert p.code[-1].op == ir.END
+
+
+def _word_slicing_exprs(dag):
+    """Selector / address / low-mask / shift / division patterns over a calldata-like word
+    (32 bytes, each If(i <s size, b_i, 0), concatenated)."""
+    bs = [dag.var(f"b{i}", 8) for i in range(32)]
+    size = dag.var("size", 256)
+    parts = [dag.op(ir.W_ITE, 8, dag.op(ir.B_SLT, 256, dag.const(i, 256), size), b, dag.const(0, 8))
+             for i, b in enumerate(bs)]
+    word, wd = parts[0], 8
+    for p in parts[1:]:
+        wd += 8
+        word = dag.op(ir.W_CONCAT, wd, word, p, aux=8)
+    outs = [
+        dag.op(ir.W_LSHR, 256, word, dag.const(224, 256)),
+        dag.op(ir.W_AND, 256, dag.op(ir.W_UDIV, 256, word, dag.const(1 << 224, 256)), dag.const(0xFFFFFFFF, 256)),
+        dag.op(ir.W_AND, 256, word, dag.const((1 << 160) - 1, 256)),
+        dag.op(ir.W_AND, 256, dag.const((1 << 160) - 1, 256), word),
+        dag.op(ir.W_LSHR, 256, dag.op(ir.W_MOV, 256, dag.op(ir.W_EXTRACT, 100, word, aux=20)), dag.const(30, 256)),
+        dag.op(ir.W_EXTRACT, 40, word, aux=100),
+        dag.op(ir.W_EXTRACT, 16, dag.op(ir.W_MOV, 256, dag.op(ir.W_EXTRACT, 64, word, aux=8)), aux=60),
+        dag.op(ir.W_UDIV, 256, word, dag.const(1, 256)),
+        dag.op(ir.W_LSHR, 256, word, dag.const(0, 256)),
+        dag.op(ir.W_LSHR, 256, word, dag.const(300, 256)),
+    ]
+    bools = [dag.op(ir.B_EQ, 256, outs[0], dag.const(0xA9059CBB, 256)),
+             dag.op(ir.B_EQ, 256, dag.const(0x1FFFFFFFF, 256), outs[1]),
+             dag.op(ir.B_EQ, 256, outs[2], dag.const(7, 256))]
+    return outs + bools
+
+
+def test_word_slicing_rewrites_preserve_values(monkeypatch):
+    """Dag.op's z3.simplify-style rewrites (udiv by 2^k, shifts / masks / extracts of
+    concats) give the same value as the unrewritten DAG on every input."""
+    from dag_eval import eval_dag_values
+
+    monkeypatch.setattr(Dag, "_simplify", lambda self, *a: None)
+    plain = Dag()
+    e_plain = _word_slicing_exprs(plain)
+    monkeypatch.undo()
+    simp = Dag()
+    e_simp = _word_slicing_exprs(simp)
+    rng = random.Random(11)
+
+    def values(dag, raw):
+        return [raw[32] if v.name == "size" else raw[int(v.name[1:])] for v in dag.vars]
+
+    for trial in range(200):
+        raw = [rng.getrandbits(8) for _ in range(32)]
+        raw.append(rng.choice([0, 3, 4, 20, 36, 40, 1 << 255, rng.getrandbits(256)]))
+        if trial % 3 == 0:
+            raw[:4] = [0xA9, 0x05, 0x9C, 0xBB]
+        vp = eval_dag_values(plain, values(plain, raw))
+        vs = eval_dag_values(simp, values(simp, raw))
+        for a, b in zip(e_plain, e_simp):
+            assert vp[a] == vs[b], (trial, a, b)

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 TAG=${1:-r01}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-B="python bench.py --steps 2 --warmup 1 --no-cpu-baseline"
+B="python bench.py --steps 2 --warmup 1 --no-cpu-baseline --corpus-scenarios 0"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run -- $B > $OUT/trace.log 2>&1 || { echo "trace failed"; exit 1; }
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- $B > $OUT/fetch.log 2>&1 || { echo "fetch failed"; exit 1; }
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- $B > $OUT/write.log 2>&1 || { echo "write failed"; exit 1; }

@@ -11,5 +11,5 @@ timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smo
 tail -1 $O/smoke.log
 timeout -k 10 400 python -u bench.py ${BENCH_ARGS:-} > $O/bench.log 2>&1 || { echo "BENCH FAILED"; tail -20 $O/bench.log; exit 1; }
 tail -1 $O/bench.log
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace -o run -- python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > $O/trace.log 2>&1 || { echo "TRACE FAILED"; tail -20 $O/trace.log; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace -o run -- python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline --corpus-scenarios 0 ${BENCH_ARGS:-} > $O/trace.log 2>&1 || { echo "TRACE FAILED"; tail -20 $O/trace.log; exit 1; }
 echo ROUND-DONE
