@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--seed", type=int, default=0x5EED)
     ap.add_argument("--cpu-sample-s", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--keccak-log2", type=int, default=24,
+                    help="config 4: 2^k 64-byte key||slot messages per Keccak launch (0 = skip)")
     ap.add_argument("--corpus-scenarios", type=int, default=48,
                     help="LASER-shaped scenarios for the %% discharged half of the metric (0 = skip)")
     return ap.parse_args()
@@ -110,6 +112,52 @@ def discharge(args):
             "queries_per_s": n / max(t2 - t1, 1e-9),
             "corpus": f"mythril_amd/corpus.py, {args.corpus_scenarios} planted 2-tx scenarios "
                       f"(config-2 substitute: no z3/solc for --solver-log dumps)"}
+
+
+# Keccak-f[1600] = 6,500 int32 ops per permutation; a 64-byte key||slot
+# preimage is one permutation and moves 64 B in + 32 B out of HBM.
+KECCAK_OPS = 6500
+KECCAK_BYTES = 64 + 32
+
+
+def keccak_leg(args, torch, rank, world):
+    """Config 4 (BASELINE.json configs[3]): batched Keccak-256 over 2^k 64-byte mapping-slot
+    preimages resident in HBM (pf_keccak_fixed_kernel), HIP-event time of each launch on
+    the stream it runs on.  Weak scaling: every rank hashes its own 2^k messages."""
+    import ctypes
+
+    from mythril_amd import _lib
+
+    n = 1 << args.keccak_log2
+    g = torch.Generator(device="cuda").manual_seed(0x4B454343 + rank)
+    data = torch.randint(0, 256, (n * 64,), dtype=torch.uint8, device="cuda", generator=g)
+    out = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    L = _lib.lib()
+    ms = ctypes.c_float(0)
+    kms = []
+    for k in range(args.warmup + args.steps):
+        _lib.check(L.pf_keccak256_fixed_dev(data.data_ptr(), 64, n, out.data_ptr(),
+                                            ctypes.byref(ms), stream), "pf_keccak256_fixed_dev")
+        if k >= args.warmup:
+            kms.append(ms.value)
+    torch.cuda.synchronize()
+    t = float(np.mean(kms)) / 1e3
+    if world > 1:
+        import torch.distributed as dist
+
+        x = torch.tensor([t], dtype=torch.float64, device="cuda")
+        dist.all_reduce(x, op=dist.ReduceOp.MAX)
+        t = float(x.item())
+    ach = n * KECCAK_OPS / t
+    return {"workload": "config-4 Keccak-256 of 64-byte key||slot preimages (HBM-resident)",
+            "messages_per_launch_per_gpu": n, "value": world * n / t, "unit": "hashes/s",
+            "kernel": "pf_keccak_fixed_kernel", "kernel_ms_avg": 1e3 * t,
+            "roofline": {"bound": "valu", "achieved": ach / 1e12, "peak": INT32_PEAK_OPS / 1e12,
+                         "unit": "Tops/s (int32)", "frac": ach / INT32_PEAK_OPS,
+                         "hbm_GBps": n * KECCAK_BYTES / t / 1e9,
+                         "note": "6,500 int32 ops per Keccak-f[1600] (SURVEY §8(d)); the kernel "
+                                 "issues ~4,280 VALU instructions per permutation"}}
 
 
 def pmc_traffic(args):
@@ -192,6 +240,8 @@ def main():
         local = np.concatenate(founds)
         gather_found(local, rank * len(local), world * len(local))
 
+    kec = keccak_leg(args, torch, rank, world) if args.keccak_log2 > 0 else None
+
     if rank == 0:
         traffic, traffic_src = pmc_traffic(args)
         kernel_s = sum(kms) / 1e3
@@ -221,6 +271,13 @@ def main():
                                "at 512 products; the kernel's windowed EXP needs ~340, DESIGN.md §4)",
             "gen_upload_s": t_gen,
         }
+        if args.keccak_log2 > 0:
+            line["keccak"] = kec
+            if world == 1 and not args.no_cpu_baseline:
+                sys.path.insert(0, os.path.join(ROOT, "oracle"))
+                import coracle_py
+
+                line["keccak"]["cpu_baseline"] = coracle_py.keccak_baseline(64, 5.0)
         if args.corpus_scenarios > 0:
             line["discharge"] = discharge(args)
         if world == 1 and not args.no_cpu_baseline:

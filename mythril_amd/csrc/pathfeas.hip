@@ -444,8 +444,13 @@ int pf_keccak256_fixed_dev(const uint8_t* d_data, uint32_t len, size_t n, uint8_
     if (n == 0) return 0;
     hipStream_t st = pick_stream(stream);
     HIPCHK(hipEventRecord(g_ev0, st));
-    hipLaunchKernelGGL(pf_keccak_fixed_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st,
-                       d_data, len, (uint64_t)n, d_out32);
+    const bool fast = (len % 16u) == 0u && len < 136u && (((uintptr_t)d_data) & 15u) == 0u;
+    if (fast)
+        hipLaunchKernelGGL(pf_keccak_fixed_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0,
+                           st, d_data, len, (uint64_t)n, d_out32);
+    else
+        hipLaunchKernelGGL(pf_keccak_stride_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256),
+                           0, st, d_data, len, (uint64_t)n, d_out32);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(g_ev1, st));
     if (kernel_ms) {

@@ -1,137 +1,237 @@
 // pf_keccak.hip — batched Keccak-256 (original Keccak padding, as eth_hash / Mythril's
-// support_utils.sha3) for hash concretisation: one lane = one message, the 25-lane state
-// in 50 VGPRs, 24 rounds fully unrolled.  Messages are the 64-byte key||slot mapping
-// preimages in the common case (one Keccak-f[1600] block, rate 136 B).
+// support_utils.sha3) for hash concretisation: one lane = one message.
+//
+// gfx950 layout of the permutation: the 25 64-bit lanes live as 50 32-bit halves in VGPRs
+// (there is no 64-bit rotate or xor on the VALU, so working on halves costs nothing extra):
+//   * 64-bit rotates   = 2 x v_alignbit_b32 (a rotate by 32 is a rename);
+//   * theta            = column parities with 3-input xors (v_bitop3_b32, table 0x96), then
+//                        a[i] ^= C[x-1] ^ rot1(C[x+1]) as one 3-input xor per half;
+//   * rho + pi         = the in-place 24-cycle (one temp; after unrolling every move is a
+//                        register rename);
+//   * chi              = one v_bitop3_b32 per half: a ^ (~b & c) = truth table 0xD2 over
+//                        (a, b, c) — gfx950-only instruction;
+//   * iota             = two scalar-operand xors.
+// ≈ 178 VALU instructions per round, ≈ 4,280 per Keccak-f[1600] (unrolled form: 61 VGPRs,
+// no LDS, no scratch).
+// Messages are the 64-byte key||slot mapping preimages in the common case (one block,
+// rate 136 B); pf_keccak_fixed_kernel reads them as 16-byte vectors.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace {
 
-__constant__ uint64_t kRC[24] = {
-    0x0000000000000001ull, 0x0000000000008082ull, 0x800000000000808Aull, 0x8000000080008000ull,
-    0x000000000000808Bull, 0x0000000080000001ull, 0x8000000080008081ull, 0x8000000000008009ull,
-    0x000000000000008Aull, 0x0000000000000088ull, 0x0000000080008009ull, 0x000000008000000Aull,
-    0x000000008000808Bull, 0x800000000000008Bull, 0x8000000000008089ull, 0x8000000000008003ull,
-    0x8000000000008002ull, 0x8000000000000080ull, 0x000000000000800Aull, 0x800000008000000Aull,
-    0x8000000080008081ull, 0x8000000000008080ull, 0x0000000080000001ull, 0x8000000080008008ull};
+__constant__ uint32_t kRC[48] = {
+    0x00000001u, 0x00000000u, 0x00008082u, 0x00000000u, 0x0000808Au, 0x80000000u,
+    0x80008000u, 0x80000000u, 0x0000808Bu, 0x00000000u, 0x80000001u, 0x00000000u,
+    0x80008081u, 0x80000000u, 0x00008009u, 0x80000000u, 0x0000008Au, 0x00000000u,
+    0x00000088u, 0x00000000u, 0x80008009u, 0x00000000u, 0x8000000Au, 0x00000000u,
+    0x8000808Bu, 0x00000000u, 0x0000008Bu, 0x80000000u, 0x00008089u, 0x80000000u,
+    0x00008003u, 0x80000000u, 0x00008002u, 0x80000000u, 0x00000080u, 0x80000000u,
+    0x0000800Au, 0x00000000u, 0x8000000Au, 0x80000000u, 0x80008081u, 0x80000000u,
+    0x00008080u, 0x80000000u, 0x80000001u, 0x00000000u, 0x80008008u, 0x80000000u};
 
-__device__ __forceinline__ uint64_t rol64(uint64_t x, int n) {
-    return n == 0 ? x : ((x << n) | (x >> (64 - n)));
-}
+struct Lane {
+    uint32_t lo, hi;
+};
 
-// state index i = x + 5*y
-__device__ __forceinline__ void keccakf(uint64_t s[25]) {
-    // rho offsets r[x + 5y] and pi: B[y + 5*((2x+3y)%5)] = rol(A[x+5y], r)
-    constexpr int R[25] = {0, 1, 62, 28, 27, 36, 44, 6, 55, 20, 3, 10, 43,
-                           25, 39, 41, 45, 15, 21, 8, 18, 2, 61, 56, 14};
-#pragma unroll 1
-    for (int rnd = 0; rnd < 24; rnd++) {
-        uint64_t C[5], D[5], B[25];
-#pragma unroll
-        for (int x = 0; x < 5; x++) C[x] = s[x] ^ s[x + 5] ^ s[x + 10] ^ s[x + 15] ^ s[x + 20];
-#pragma unroll
-        for (int x = 0; x < 5; x++) D[x] = C[(x + 4) % 5] ^ rol64(C[(x + 1) % 5], 1);
-#pragma unroll
-        for (int x = 0; x < 5; x++)
-#pragma unroll
-            for (int y = 0; y < 5; y++) {
-                int i = x + 5 * y;
-                B[y + 5 * ((2 * x + 3 * y) % 5)] = rol64(s[i] ^ D[x], R[i]);
-            }
-#pragma unroll
-        for (int x = 0; x < 5; x++)
-#pragma unroll
-            for (int y = 0; y < 5; y++)
-                s[x + 5 * y] = B[x + 5 * y] ^ ((~B[(x + 1) % 5 + 5 * y]) & B[(x + 2) % 5 + 5 * y]);
-        s[0] ^= kRC[rnd];
+// rotate left by a compile-time amount
+template <int N>
+__device__ __forceinline__ Lane rotl(Lane v) {
+    static_assert(N >= 0 && N < 64, "rotation");
+    if constexpr (N == 0) {
+        return v;
+    } else if constexpr (N == 32) {
+        return Lane{v.hi, v.lo};
+    } else if constexpr (N < 32) {
+        return Lane{__builtin_amdgcn_alignbit(v.lo, v.hi, 32 - N),
+                    __builtin_amdgcn_alignbit(v.hi, v.lo, 32 - N)};
+    } else {
+        return Lane{__builtin_amdgcn_alignbit(v.hi, v.lo, 64 - N),
+                    __builtin_amdgcn_alignbit(v.lo, v.hi, 64 - N)};
     }
 }
 
-__device__ __forceinline__ void absorb_and_squeeze(const uint8_t* __restrict__ p, uint64_t len,
-                                                   uint8_t* __restrict__ out) {
-    uint64_t s[25];
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, (unsigned char)0x96);  // a ^ b ^ c
+}
+
+__device__ __forceinline__ uint32_t chi(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, (unsigned char)0xD2);  // a ^ (~b & c)
+}
+
+// the pi cycle (lane index order) and the rho offsets along it
+constexpr int kPi[24] = {10, 7, 11, 17, 18, 3, 5, 16, 8, 21, 24, 4,
+                         15, 23, 19, 13, 12, 2, 20, 14, 22, 9, 6, 1};
+constexpr int kRho[24] = {1, 3, 6, 10, 15, 21, 28, 36, 45, 55, 2, 14,
+                          27, 41, 56, 8, 25, 43, 62, 18, 39, 61, 20, 44};
+
+template <int I>
+__device__ __forceinline__ void rho_pi_step(Lane a[25], Lane& t) {
+    if constexpr (I < 24) {
+        const Lane next = a[kPi[I]];
+        a[kPi[I]] = rotl<kRho[I]>(t);
+        t = next;
+        rho_pi_step<I + 1>(a, t);
+    }
+}
+
+__device__ __forceinline__ void keccak_round(Lane a[25], uint32_t rc_lo, uint32_t rc_hi) {
+    // theta
+    Lane C[5], R[5];
 #pragma unroll
-    for (int i = 0; i < 25; i++) s[i] = 0;
-    const uint64_t rate = 136;
-    uint64_t off = 0;
-    const bool aligned8 = (((uintptr_t)p) & 7u) == 0;
-    // full blocks
-    while (len - off >= rate) {
+    for (int x = 0; x < 5; x++) {
+        C[x].lo = xor3(xor3(a[x].lo, a[x + 5].lo, a[x + 10].lo), a[x + 15].lo, a[x + 20].lo);
+        C[x].hi = xor3(xor3(a[x].hi, a[x + 5].hi, a[x + 10].hi), a[x + 15].hi, a[x + 20].hi);
+    }
 #pragma unroll
-        for (int i = 0; i < 17; i++) {
-            uint64_t lane;
-            if (aligned8) {
-                lane = *(const uint64_t*)(p + off + 8 * i);
-            } else {
-                lane = 0;
-                for (int b = 0; b < 8; b++) lane |= (uint64_t)p[off + 8 * i + b] << (8 * b);
-            }
-            s[i] ^= lane;
+    for (int x = 0; x < 5; x++) R[x] = rotl<1>(C[(x + 1) % 5]);
+#pragma unroll
+    for (int x = 0; x < 5; x++)
+#pragma unroll
+        for (int y = 0; y < 25; y += 5) {
+            a[x + y].lo = xor3(a[x + y].lo, C[(x + 4) % 5].lo, R[x].lo);
+            a[x + y].hi = xor3(a[x + y].hi, C[(x + 4) % 5].hi, R[x].hi);
         }
-        keccakf(s);
-        off += rate;
+    // rho + pi
+    Lane t = a[1];
+    rho_pi_step<0>(a, t);
+    // chi
+#pragma unroll
+    for (int y = 0; y < 25; y += 5) {
+        Lane b[5];
+#pragma unroll
+        for (int x = 0; x < 5; x++) b[x] = a[y + x];
+#pragma unroll
+        for (int x = 0; x < 5; x++) {
+            a[y + x].lo = chi(b[x].lo, b[(x + 1) % 5].lo, b[(x + 2) % 5].lo);
+            a[y + x].hi = chi(b[x].hi, b[(x + 1) % 5].hi, b[(x + 2) % 5].hi);
+        }
     }
-    // last (partial) block with pad10*1, domain byte 0x01
-    const uint64_t rem = len - off;
+    // iota
+    a[0].lo ^= rc_lo;
+    a[0].hi ^= rc_hi;
+}
+
+// kUnrolled: all 24 rounds unrolled (~4.3k instructions, 34 KB of code): the pi cycle has
+// order 24, so every lane move becomes a register rename — the rolled loop pays ~110 moves
+// per round at its back edge.  The rolled form serves the multi-block general path.
+template <bool kUnrolled>
+__device__ __forceinline__ void keccakf(Lane a[25]) {
+    if constexpr (kUnrolled) {
+#pragma unroll
+        for (int rnd = 0; rnd < 24; rnd++) keccak_round(a, kRC[2 * rnd], kRC[2 * rnd + 1]);
+    } else {
+#pragma unroll 1
+        for (int rnd = 0; rnd < 24; rnd++) keccak_round(a, kRC[2 * rnd], kRC[2 * rnd + 1]);
+    }
+}
+
+__device__ __forceinline__ void squeeze(const Lane a[25], uint8_t* __restrict__ out) {
+    if ((((uintptr_t)out) & 15u) == 0u) {
+        uint4* o = (uint4*)out;
+        o[0] = make_uint4(a[0].lo, a[0].hi, a[1].lo, a[1].hi);
+        o[1] = make_uint4(a[2].lo, a[2].hi, a[3].lo, a[3].hi);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                out[8 * i + b] = (uint8_t)(a[i].lo >> (8 * b));
+                out[8 * i + 4 + b] = (uint8_t)(a[i].hi >> (8 * b));
+            }
+    }
+}
+
+// General path: any length, any alignment (pad10*1 with domain byte 0x01).  Each block is
+// staged bytewise through the thread's own LDS column ([word][thread], no bank conflicts, no
+// barrier: a thread reads only what it wrote) so the state absorbs it with 34 static-offset
+// LDS reads — byte loads straight into the state would keep up to 136 of them in flight
+// (the compiler hoists them) and triple the kernel's VGPR budget.
+constexpr int kGenThreads = 256;
+
+__device__ __forceinline__ void absorb_staged(Lane a[25], uint32_t* __restrict__ col,
+                                              const uint8_t* __restrict__ p, uint32_t nbytes,
+                                              bool last) {
+#pragma unroll 1
+    for (int w = 0; w < 34; w++) col[w * kGenThreads] = 0u;
+#pragma unroll 1
+    for (uint32_t k = 0; k < nbytes; k++)
+        col[(k >> 2) * kGenThreads] |= (uint32_t)p[k] << (8 * (k & 3));
+    if (last) {
+        col[(nbytes >> 2) * kGenThreads] ^= 0x01u << (8 * (nbytes & 3));
+        col[33 * kGenThreads] ^= 0x80000000u;
+    }
 #pragma unroll
     for (int i = 0; i < 17; i++) {
-        uint64_t lane = 0;
-        for (int b = 0; b < 8; b++) {
-            uint64_t k = 8 * (uint64_t)i + b;
-            uint64_t byte = 0;
-            if (k < rem) byte = p[off + k];
-            else if (k == rem) byte = 0x01;
-            if (k == rate - 1) byte |= 0x80;
-            lane |= byte << (8 * b);
-        }
-        s[i] ^= lane;
+        a[i].lo ^= col[(2 * i) * kGenThreads];
+        a[i].hi ^= col[(2 * i + 1) * kGenThreads];
     }
-    keccakf(s);
+}
+
+__device__ __forceinline__ void absorb_and_squeeze(uint32_t* __restrict__ col,
+                                                   const uint8_t* __restrict__ p, uint64_t len,
+                                                   uint8_t* __restrict__ out) {
+    Lane a[25];
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-        uint64_t v = s[i];
-#pragma unroll
-        for (int b = 0; b < 8; b++) out[8 * i + b] = (uint8_t)(v >> (8 * b));
+    for (int i = 0; i < 25; i++) a[i] = Lane{0u, 0u};
+    const uint64_t rate = 136;
+    uint64_t off = 0;
+    while (len - off >= rate) {
+        absorb_staged(a, col, p + off, (uint32_t)rate, false);
+        keccakf<false>(a);
+        off += rate;
     }
+    absorb_staged(a, col, p + off, (uint32_t)(len - off), true);
+    keccakf<false>(a);
+    squeeze(a, out);
 }
 
 }  // namespace
 
-extern "C" __global__ void __launch_bounds__(256)
+extern "C" __global__ void __launch_bounds__(kGenThreads)
 pf_keccak_var_kernel(const uint8_t* __restrict__ data, const uint64_t* __restrict__ offsets,
                      uint64_t n, uint8_t* __restrict__ out32) {
+    __shared__ uint32_t stage[34 * kGenThreads];
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint64_t a = offsets[i], b = offsets[i + 1];
-    absorb_and_squeeze(data + a, b - a, out32 + 32 * i);
+    absorb_and_squeeze(stage + threadIdx.x, data + a, b - a, out32 + 32 * i);
 }
 
-// fixed-length messages; len % 8 == 0 and len < 136 is the single-block fast path
-// (loads 8 bytes per state lane, stores the digest as 4 x u64).
+// fixed-length messages, general case (any length / alignment)
+extern "C" __global__ void __launch_bounds__(kGenThreads)
+pf_keccak_stride_kernel(const uint8_t* __restrict__ data, uint32_t len, uint64_t n,
+                        uint8_t* __restrict__ out32) {
+    __shared__ uint32_t stage[34 * kGenThreads];
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    absorb_and_squeeze(stage + threadIdx.x, data + i * (uint64_t)len, len, out32 + 32 * i);
+}
+
+// fixed-length single-block fast path: the host launches it when len % 16 == 0,
+// len < 136 and the buffer is 16-byte aligned (16-byte vector loads, two 16-byte digest
+// stores, all 24 rounds unrolled).
 extern "C" __global__ void __launch_bounds__(256)
 pf_keccak_fixed_kernel(const uint8_t* __restrict__ data, uint32_t len, uint64_t n,
                        uint8_t* __restrict__ out32) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const uint8_t* p = data + i * (uint64_t)len;
-    if ((len & 7u) == 0u && len < 136u && ((((uintptr_t)data) & 7u) == 0u)) {
-        uint64_t s[25];
+    const uint4* q = (const uint4*)(data + i * (uint64_t)len);
+    Lane a[25];
+    const uint32_t nq = len >> 4;  // 16-byte chunks = state lane pairs
 #pragma unroll
-        for (int k = 0; k < 25; k++) s[k] = 0;
-        const uint64_t* q = (const uint64_t*)p;
-        const uint32_t nl = len >> 3;
-#pragma unroll
-        for (int k = 0; k < 17; k++) {
-            uint64_t v = ((uint32_t)k < nl) ? q[k] : 0ull;
-            if ((uint32_t)k == nl) v ^= 0x01ull;
-            if (k == 16) v ^= 0x8000000000000000ull;
-            s[k] ^= v;
-        }
-        keccakf(s);
-        uint64_t* o = (uint64_t*)(out32 + 32 * i);
-#pragma unroll
-        for (int k = 0; k < 4; k++) o[k] = s[k];
-    } else {
-        absorb_and_squeeze(p, len, out32 + 32 * i);
+    for (int k = 0; k < 8; k++) {
+        uint4 v = ((uint32_t)k < nq) ? q[k] : make_uint4(0u, 0u, 0u, 0u);
+        a[2 * k] = Lane{v.x, v.y};
+        a[2 * k + 1] = Lane{v.z, v.w};
     }
+    a[16] = Lane{0u, 0x80000000u};
+#pragma unroll
+    for (int k = 17; k < 25; k++) a[k] = Lane{0u, 0u};
+    // domain byte at offset len = low byte of state lane len/8
+#pragma unroll
+    for (int k = 0; k < 17; k++)
+        if ((uint32_t)k == (len >> 3)) a[k].lo ^= 0x01u;
+    keccakf<true>(a);
+    squeeze(a, out32 + 32 * i);
 }

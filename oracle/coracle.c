@@ -339,3 +339,65 @@ void co_gen_values(const uint32_t* code, const uint32_t* consts, const uint32_t*
         }
     }
 }
+
+/* ---- Keccak-256 (original Keccak padding 0x01..0x80, as eth_hash / support_utils.sha3,
+ * mythril/support/support_utils.py:93-101) — FIPS 202 Keccak-f[1600] restated with 64-bit
+ * lanes; the checker and CPU baseline for pf_keccak_*_kernel.  OpenMP over messages. */
+static const uint64_t KRC[24] = {
+    0x0000000000000001ull, 0x0000000000008082ull, 0x800000000000808Aull, 0x8000000080008000ull,
+    0x000000000000808Bull, 0x0000000080000001ull, 0x8000000080008081ull, 0x8000000000008009ull,
+    0x000000000000008Aull, 0x0000000000000088ull, 0x0000000080008009ull, 0x000000008000000Aull,
+    0x000000008000808Bull, 0x800000000000008Bull, 0x8000000000008089ull, 0x8000000000008003ull,
+    0x8000000000008002ull, 0x8000000000000080ull, 0x000000000000800Aull, 0x800000008000000Aull,
+    0x8000000080008081ull, 0x8000000000008080ull, 0x0000000080000001ull, 0x8000000080008008ull};
+static const int KROT[5][5] = {{0, 36, 3, 41, 18}, {1, 44, 10, 45, 2}, {62, 6, 43, 15, 61},
+                               {28, 55, 25, 21, 56}, {27, 20, 39, 8, 14}}; /* [x][y] */
+
+static uint64_t rol(uint64_t v, int n) { return n ? (v << n) | (v >> (64 - n)) : v; }
+
+static void keccak_f(uint64_t A[25]) { /* A[x + 5y] */
+    for (int r = 0; r < 24; r++) {
+        uint64_t C[5], B[25];
+        for (int x = 0; x < 5; x++) C[x] = A[x] ^ A[x + 5] ^ A[x + 10] ^ A[x + 15] ^ A[x + 20];
+        for (int x = 0; x < 5; x++) {
+            uint64_t D = C[(x + 4) % 5] ^ rol(C[(x + 1) % 5], 1);
+            for (int y = 0; y < 5; y++) A[x + 5 * y] ^= D;
+        }
+        for (int x = 0; x < 5; x++)
+            for (int y = 0; y < 5; y++) B[y + 5 * ((2 * x + 3 * y) % 5)] = rol(A[x + 5 * y], KROT[x][y]);
+        for (int x = 0; x < 5; x++)
+            for (int y = 0; y < 5; y++)
+                A[x + 5 * y] = B[x + 5 * y] ^ (~B[(x + 1) % 5 + 5 * y] & B[(x + 2) % 5 + 5 * y]);
+        A[0] ^= KRC[r];
+    }
+}
+
+static void keccak256_one(const uint8_t* p, uint64_t len, uint8_t* out) {
+    uint64_t A[25];
+    uint8_t blk[136];
+    memset(A, 0, sizeof A);
+    for (;;) {
+        uint64_t take = len < 136 ? len : 136;
+        memset(blk, 0, sizeof blk);
+        memcpy(blk, p, take);
+        int last = len < 136;
+        if (last) { blk[take] ^= 0x01; blk[135] ^= 0x80; }
+        for (int i = 0; i < 17; i++) {
+            uint64_t lane = 0;
+            for (int b = 0; b < 8; b++) lane |= (uint64_t)blk[8 * i + b] << (8 * b);
+            A[i] ^= lane;
+        }
+        keccak_f(A);
+        if (last) break;
+        p += 136;
+        len -= 136;
+    }
+    for (int i = 0; i < 4; i++)
+        for (int b = 0; b < 8; b++) out[8 * i + b] = (uint8_t)(A[i] >> (8 * b));
+}
+
+/* n fixed-length messages data[i*len .. (i+1)*len) -> out[32*i ..] */
+void co_keccak256_fixed(const uint8_t* data, uint64_t len, uint64_t n, uint8_t* out) {
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < (int64_t)n; i++) keccak256_one(data + (uint64_t)i * len, len, out + 32 * (uint64_t)i);
+}

@@ -31,6 +31,9 @@ def lib():
         L.co_gen_values.argtypes = [u32p] * 5 + [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64,
                                                  ctypes.c_uint32, ctypes.c_uint32, u32p]
         L.co_gen_values.restype = None
+        L.co_keccak256_fixed.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                         ctypes.c_void_p]
+        L.co_keccak256_fixed.restype = None
         _lib = L
     return _lib
 
@@ -87,3 +90,28 @@ def baseline(programs, budget, seed, target_s):
     return {"value": evals / dt, "unit": "evals/s", "cores": cores, "kind": "port",
             "sample": f"C restatement (oracle/coracle.c, OpenMP) over {s} sets x {chunk} "
                       f"candidates of the same workload, {dt:.1f} s"}
+
+
+def keccak256_fixed(data: np.ndarray, length: int, n: int) -> np.ndarray:
+    """Keccak-256 of n fixed-length messages (uint8 array, row-major) -> (n, 32) uint8."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    assert data.size >= length * n
+    out = np.zeros((n, 32), dtype=np.uint8)
+    lib().co_keccak256_fixed(data.ctypes.data, length, n, out.ctypes.data)
+    return out
+
+
+def keccak_baseline(length, target_s):
+    """CPU hashes/s of the C Keccak restatement on all host cores (bounded sample)."""
+    cores = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+    chunk = 1 << 16
+    data = np.random.default_rng(1).integers(0, 256, size=chunk * length, dtype=np.uint8)
+    t0 = time.perf_counter()
+    done = 0
+    while time.perf_counter() - t0 < target_s:
+        keccak256_fixed(data, length, chunk)
+        done += chunk
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "hashes/s", "cores": cores, "kind": "port",
+            "sample": f"C Keccak-256 restatement (oracle/coracle.c, OpenMP), {done} x {length}-byte "
+                      f"messages, {dt:.1f} s"}

@@ -167,22 +167,32 @@ def test_keccak_vmsha3_and_random(engine):
         assert g == O.keccak256(m)
 
 
-def test_keccak_fixed_dev_matches(engine):
+@pytest.mark.parametrize("ln,shift", [(64, 0), (32, 0), (128, 0), (16, 0), (0, 0),
+                                      (64, 8), (72, 0), (8, 0), (135, 0), (136, 0), (200, 0),
+                                      (1, 3)])
+def test_keccak_fixed_dev_matches(engine, ln, shift):
+    """pf_keccak256_fixed_dev: the unrolled single-block kernel (len % 16 == 0, < 136, 16-B
+    aligned) and the LDS-staged general kernel (any other length / alignment), every digest
+    against the C Keccak restatement."""
     torch = pytest.importorskip("torch")
-    from mythril_amd import _lib
     import ctypes
-    n, ln = 4096, 64
-    host = np.random.default_rng(5).integers(0, 256, size=n * ln, dtype=np.uint8)
-    d_in = torch.from_numpy(host).to("cuda")
+
+    import coracle_py
+    from mythril_amd import _lib
+    n = 5000
+    host = np.random.default_rng(5 + ln).integers(0, 256, size=n * ln + shift + 1, dtype=np.uint8)
+    d_buf = torch.from_numpy(host).to("cuda")
+    d_in = d_buf[shift:]
     d_out = torch.zeros(n * 32, dtype=torch.uint8, device="cuda")
     ms = ctypes.c_float(0)
     stream = torch.cuda.current_stream().cuda_stream  # same stream as the tensors' producers
     _lib.check(_lib.lib().pf_keccak256_fixed_dev(d_in.data_ptr(), ln, n, d_out.data_ptr(),
                                                  ctypes.byref(ms), stream), "keccak fixed")
     torch.cuda.synchronize()
-    out = d_out.cpu().numpy()
-    for i in range(0, n, 97):
-        assert out[32 * i:32 * i + 32].tobytes() == O.keccak256(host[ln * i:ln * i + ln].tobytes())
+    out = d_out.cpu().numpy().reshape(n, 32)
+    want = coracle_py.keccak256_fixed(host[shift:], ln, n)
+    assert np.array_equal(out, want)
+    assert out[0].tobytes() == O.keccak256(host[shift:shift + ln].tobytes())
 
 
 def _rand_operand(rng, w):

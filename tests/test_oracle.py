@@ -10,6 +10,8 @@
 
 import random
 
+import numpy as np
+
 import pyoracle as O
 import pytest
 from conftest import load_golden
@@ -110,3 +112,20 @@ def test_ops_golden_consistent():
         r = fns[v["op"]](int(v["a"], 16), int(v["b"], 16), v["w"])
         exp = v["r"] if isinstance(v["r"], int) else int(v["r"], 16)
         assert int(r) == exp
+
+
+def test_c_keccak_matches_python_and_vmsha3():
+    """oracle/coracle.c's Keccak-256 (the GPU keccak checker / CPU baseline) against the
+    spec restatement in pyoracle and the vmSha3Test digests."""
+    import coracle_py
+
+    for c in load_golden("vmsha3.json"):
+        m = np.zeros(c["size"], dtype=np.uint8)
+        got = coracle_py.keccak256_fixed(m, c["size"], 1)[0].tobytes()
+        assert "0x" + got.hex() == c["digest"].lower()
+    rng = np.random.default_rng(9)
+    for ln in [0, 1, 31, 64, 135, 136, 137, 271, 272, 500]:
+        d = rng.integers(0, 256, size=max(3 * ln, 1), dtype=np.uint8)
+        got = coracle_py.keccak256_fixed(d, ln, 3)
+        for i in range(3):
+            assert got[i].tobytes() == O.keccak256(d[ln * i:ln * i + ln].tobytes())
