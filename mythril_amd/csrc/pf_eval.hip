@@ -296,16 +296,13 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
         // instruction cache, since consecutive bytecode instructions jump between units.
         switch (unit) {
             case PF_U_MUL:
-                // ---- multiplier: MUL = one product; EXP = 2-bit-window square-and-multiply
-                // over the wave's largest exponent bit length (pf::exp256)
+                // ---- multiplier: MUL = one product; EXP = windowed square-and-multiply over
+                // the low 84 exponent bits + the 2-adic closed form for bits 84..253
+                // (pf::exp256_split)
                 if (op == PF_W_MUL) {
                     z = pf::mul256(x, y);
                 } else {
-                    uint32_t nb = 256u - pf::clz256(y);
-#pragma unroll
-                    for (int o = 32; o >= 1; o >>= 1) nb = max(nb, (uint32_t)__shfl_xor((int)nb, o));
-                    nb = min(__builtin_amdgcn_readfirstlane(nb), 256u);
-                    z = pf::exp256(x, y, nb, exp_tbl, 64u);
+                    z = pf::exp256_split(x, y, exp_tbl, 64u);
                 }
                 break;
             case PF_U_DIV: {

@@ -229,3 +229,40 @@ def test_random_arith_bulk(engine, name):
         want = np.array([i % 2 == 0 for i in range(len(cands))])
         bad = np.nonzero(got != want)[0]
         assert bad.size == 0, (name, w, [[hex(v) for v in cands[i]] for i in bad[:3]])
+
+
+def test_exp_split_edges(engine):
+    """pf::exp256_split (windowed low 84 bits + 2-adic closed form for bits 84..253) against
+    the oracle's pow(b, e, 2^w): exponents at the 84 / 254 / 256 boundaries, odd and even
+    bases, and whole waves (64 lanes) that are all-even / all-small-exponent so the
+    wave-uniform skips of the closed form are taken too."""
+    rng = np.random.default_rng(0xE4F)
+    M = (1 << 256) - 1
+    exps = [0, 1, 2, 255, 256, 257, (1 << 84) - 1, 1 << 84, (1 << 84) + 1, (1 << 85) + 3,
+            (1 << 126) + 5, (1 << 254) - 1, 1 << 254, (1 << 254) + 1, (1 << 255) + 7, M, M - 1]
+    bases = [0, 1, 2, 3, 5, 7, M, M - 1, 1 << 255, (1 << 255) + 1, 3 << 100, (1 << 84) + 1]
+    for w in (256, 200, 64):
+        Mw = ir.mask(w)
+        prog = _op_program("exp", w)
+        db = engine.upload([prog])
+        groups = []
+        for b in bases:
+            for e in exps:
+                groups.append((b, e))
+        for _ in range(640):
+            groups.append((int.from_bytes(rng.bytes(32), "little"), int.from_bytes(rng.bytes(32), "little")))
+        # uniform waves: all-even bases with big exponents, all-odd with small exponents
+        even_wave = [(int.from_bytes(rng.bytes(32), "little") & ~1, int.from_bytes(rng.bytes(32), "little"))
+                     for _ in range(64)]
+        small_wave = [(int.from_bytes(rng.bytes(32), "little") | 1, int(rng.integers(0, 1 << 62)))
+                      for _ in range(64)]
+        pairs = even_wave + small_wave + groups
+        cands = []
+        for b, e in pairs:
+            b, e = b & Mw, e & Mw
+            r = O.bvexp(b, e, w)
+            assert r == pow(b, e, 1 << w)
+            cands.append([b, e, r])
+        got = engine.eval_assignments(db, 0, ir.pack_assignments(prog, cands))
+        bad = np.nonzero(~got)[0]
+        assert bad.size == 0, (w, [[hex(v) for v in cands[i]] for i in bad[:3]])

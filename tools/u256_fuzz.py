@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Fuzz tools/u256_host_check.cpp (host build of csrc/u256.h) against Python big ints:
-udivrem256, mul256, sqr256, exp256.  Usage: python3 tools/u256_fuzz.py [n]"""
+udivrem256, mul256, sqr256, exp256, exp256_split.  Usage: python3 tools/u256_fuzz.py [n]"""
 import os
 import random
 import subprocess
@@ -14,7 +14,9 @@ CLANG = "/opt/rocm/llvm/bin/clang++"
 def vals(rng):
     k = rng.randrange(9)
     if k == 0:
-        return rng.choice([0, 1, 2, 3, M, M - 1, 1 << 255, (1 << 255) - 1, (1 << 128), (1 << 160) - 1])
+        return rng.choice([0, 1, 2, 3, 255, 256, 257, M, M - 1, 1 << 255, (1 << 255) - 1, (1 << 128),
+                           (1 << 160) - 1, (1 << 84) - 1, 1 << 84, (1 << 84) + 1, (1 << 254) - 1,
+                           1 << 254, (1 << 254) + 1])
     if k == 1:
         return rng.getrandbits(rng.randrange(1, 257))
     if k == 2:
@@ -32,11 +34,12 @@ def main():
     out = subprocess.run([exe], input=inp, capture_output=True, text=True, check=True).stdout.split("\n")
     bad = 0
     for (a, b), line in zip(cases, out):
-        q, r, m, sq, ex = (int(t, 16) for t in line.split())
+        q, r, m, sq, ex, ex2 = (int(t, 16) for t in line.split())
         wq = M if b == 0 else a // b
         wr = a if b == 0 else a % b
-        want = (wq, wr, (a * b) & M, (a * a) & M, pow(a, b, 1 << 256))
-        if (q, r, m, sq, ex) != want:
+        pw = pow(a, b, 1 << 256)
+        want = (wq, wr, (a * b) & M, (a * a) & M, pw, pw)
+        if (q, r, m, sq, ex, ex2) != want:
             bad += 1
             if bad < 5:
                 print("MISMATCH", hex(a), hex(b))

@@ -26,10 +26,12 @@ int main() {
         u256 sq = pf::sqr256(a);
         uint2 tbl[32];
         u256 ex = pf::exp256(a, b, (a.l[0] & 1u) ? 256u : 256u - pf::clz256(b), tbl, 1u);
+        u256 ex2 = pf::exp256_split(a, b, tbl, 1u);
         for (int i = 7; i >= 0; i--) printf("%08x", q.l[i]); printf(" ");
         for (int i = 7; i >= 0; i--) printf("%08x", r.l[i]); printf(" ");
         for (int i = 7; i >= 0; i--) printf("%08x", m.l[i]); printf(" ");
         for (int i = 7; i >= 0; i--) printf("%08x", sq.l[i]); printf(" ");
-        for (int i = 7; i >= 0; i--) printf("%08x", ex.l[i]); printf("\n");
+        for (int i = 7; i >= 0; i--) printf("%08x", ex.l[i]); printf(" ");
+        for (int i = 7; i >= 0; i--) printf("%08x", ex2.l[i]); printf("\n");
     }
 }
