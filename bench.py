@@ -46,6 +46,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--keccak-log2", type=int, default=24,
                     help="config 4: 2^k 64-byte key||slot messages per Keccak launch (0 = skip)")
+    ap.add_argument("--lib", default=None, help="alternative build of libpathfeas.so (experiments)")
     ap.add_argument("--corpus-scenarios", type=int, default=48,
                     help="LASER-shaped scenarios for the %% discharged half of the metric (0 = skip)")
     return ap.parse_args()
@@ -190,8 +191,11 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    from mythril_amd import ir, synth
+    from mythril_amd import _lib, ir, synth
     from mythril_amd.engine import Engine
+
+    if args.lib:
+        _lib.load_library(args.lib)
 
     eng = Engine(local)
     flags = ir.FLAG_COUNT_OPS | (ir.FLAG_EARLY_EXIT | ir.FLAG_SHORTCIRCUIT if args.mode == "early" else 0)

@@ -95,7 +95,11 @@ int check_launch(Batch* B, uint64_t gseed, uint32_t budget, uint32_t flags, uint
                  uint32_t* d_found, pf_stats* stats, hipStream_t st) {
     unsigned long long* d_counters = reinterpret_cast<unsigned long long*>(g_scratch_u32);
     uint64_t* d_t0 = reinterpret_cast<uint64_t*>(g_scratch_u32 + 8);
+#ifdef PF_PROFILE_UNITS
+    HIPCHK(hipMemsetAsync(g_scratch_u32, 0, 256, st));
+#else
     HIPCHK(hipMemsetAsync(g_scratch_u32, 0, 64, st));
+#endif
     HIPCHK(hipMemsetAsync(d_found, 0xff, B->n_sets * sizeof(uint32_t), st));
     if (B->n_sets == 0 || budget == 0) {
         if (stats) memset(stats, 0, sizeof(*stats));
@@ -133,6 +137,17 @@ int check_launch(Batch* B, uint64_t gseed, uint32_t budget, uint32_t flags, uint
 extern "C" {
 
 int pf_version(void) { return 1; }
+
+#ifdef PF_PROFILE_UNITS
+// profiling builds only (tools/unitprof.py): per-unit s_memtime cycles of the last launch
+int pf_prof_read(uint64_t* out) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (ensure_init_locked()) return -1;
+    HIPCHK(hipMemcpy(out, g_scratch_u32 + 2 * PF_PROF_SLOT, (PF_PROF_BUCKETS + 1) * 8,
+                     hipMemcpyDeviceToHost));
+    return 0;
+}
+#endif
 
 const char* pf_last_error(void) {
     std::lock_guard<std::mutex> lk(g_mu);

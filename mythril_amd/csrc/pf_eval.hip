@@ -19,6 +19,11 @@
 
 using pf::u256;
 
+// profiling buckets: the 8 datapath units, EXP (8), W_CONST (9); slot = u64 index in the
+// launch's counter scratch; bucket PF_PROF_BUCKETS = whole-wave time
+#define PF_PROF_BUCKETS 10
+#define PF_PROF_SLOT 16
+
 typedef uint32_t v16u __attribute__((ext_vector_type(16)));
 typedef uint32_t v32u __attribute__((ext_vector_type(32)));
 
@@ -236,6 +241,19 @@ PF_INL u256 gen_var(const SetCtx& S, uint32_t v, uint32_t cand) {
 
 enum Mode { MODE_GEN = 0, MODE_SOA = 1 };
 
+// Per-unit cycle accounting (profiling builds only, tools/unitprof.py): s_memtime deltas of
+// every bytecode instruction, bucketed by datapath unit (EXP separately), kept in SGPRs.
+struct UnitProf {
+    uint64_t c[PF_PROF_BUCKETS];
+};
+#ifdef PF_PROFILE_UNITS
+PF_INL void prof_add(UnitProf* P, uint32_t b, uint64_t dt) {
+#pragma unroll
+    for (int i = 0; i < PF_PROF_BUCKETS; i++)
+        if (b == (uint32_t)i) P->c[i] += dt;
+}
+#endif
+
 // LDS for EXP's window table (pf::exp256): 8 entries x 4 limb pairs per lane, 64 lanes,
 // 4 waves per 256-thread workgroup = 64 KiB; two workgroups per CU fit in 160 KiB.
 #define PF_EXP_LDS_U2 (4 * 8 * 4 * 64)
@@ -249,7 +267,7 @@ PF_INL uint2* exp_tbl_of(uint2* lds) {
 template <int MODE>
 PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_t flags,
                             const uint32_t* __restrict__ soa, uint32_t soa_n,
-                            uint2* exp_tbl, uint32_t* complete, uint64_t* ops) {
+                            uint2* exp_tbl, uint32_t* complete, uint64_t* ops, UnitProf* prof) {
     // No initialisation: pf_batch_create rejects programs that read a register before
     // writing it, so the banks never leak values between candidates.
     v16u W[8];
@@ -276,6 +294,9 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
                        c = (I.y >> 24) & 0xffu;
         const uint32_t aux = I.z;
         cost += I.w;
+#ifdef PF_PROFILE_UNITS
+        const uint64_t t_ins = __builtin_amdgcn_s_memtime();
+#endif
         // Issue the next fetch only after this instruction's words are decoded: scalar
         // loads return out of order, so a fetch issued before the decode would be waited
         // for together with the one being consumed (lgkmcnt(0)).
@@ -459,6 +480,12 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
             const uint32_t bit = 1u << (d & 31u);
             Bk = (Bk & ~bit) | (bres ? bit : 0u);
         }
+#ifdef PF_PROFILE_UNITS
+        prof_add(prof, op == PF_W_EXP ? 8u : (op == PF_W_CONST ? 9u : unit),
+                 __builtin_amdgcn_s_memtime() - t_ins);
+#else
+        (void)prof;
+#endif
     }
     *ops += cost;
     return root;
@@ -510,6 +537,12 @@ pf_check_kernel(const pf_set_desc* __restrict__ descs, uint32_t n_sets,
         unsigned long long prev = atomicCAS((unsigned long long*)t0_slot, 0ull, (unsigned long long)now);
         t0 = prev ? prev : now;
     }
+    UnitProf prof;
+#pragma unroll
+    for (int i = 0; i < PF_PROF_BUCKETS; i++) prof.c[i] = 0;
+#ifdef PF_PROFILE_UNITS
+    const uint64_t t_wave = __builtin_amdgcn_s_memtime();
+#endif
     const uint32_t begin = slice * per_wave;
     const uint32_t end = min(budget, begin + per_wave);
     uint64_t evals_full = 0, decided = 0, ops = 0;
@@ -526,7 +559,8 @@ pf_check_kernel(const pf_set_desc* __restrict__ descs, uint32_t n_sets,
         const bool active = cand < end;
         uint32_t complete = 0;
         uint64_t lane_ops = 0;
-        uint32_t sat = run_program<MODE_GEN>(S, cand, active, flags, nullptr, 0u, exp_tbl, &complete, &lane_ops);
+        uint32_t sat = run_program<MODE_GEN>(S, cand, active, flags, nullptr, 0u, exp_tbl, &complete,
+                                             &lane_ops, &prof);
         const uint64_t m_act = __ballot(active);
         const uint64_t m_sat = __ballot(active && sat);
         const uint64_t m_full = __ballot(active && complete);
@@ -543,6 +577,13 @@ pf_check_kernel(const pf_set_desc* __restrict__ descs, uint32_t n_sets,
         atomicAdd(counters + 0, (unsigned long long)evals_full);
         atomicAdd(counters + 1, (unsigned long long)decided);
         if (flags & PF_FLAG_COUNT_OPS) atomicAdd(counters + 2, (unsigned long long)ops);
+#ifdef PF_PROFILE_UNITS
+#pragma unroll
+        for (int i = 0; i < PF_PROF_BUCKETS; i++)
+            atomicAdd(counters + PF_PROF_SLOT + i, (unsigned long long)prof.c[i]);
+        atomicAdd(counters + PF_PROF_SLOT + PF_PROF_BUCKETS,
+                  (unsigned long long)(__builtin_amdgcn_s_memtime() - t_wave));
+#endif
     }
 }
 
@@ -558,8 +599,9 @@ pf_eval_soa_kernel(const pf_set_desc* __restrict__ descs, uint32_t set,
     __shared__ uint2 pf_exp_lds[PF_EXP_LDS_U2];
     uint32_t complete = 0;
     uint64_t ops = 0;
+    UnitProf prof;
     uint32_t sat = run_program<MODE_SOA>(S, active ? cand : 0u, active, 0u, soa, n_cand,
-                                         exp_tbl_of(pf_exp_lds), &complete, &ops);
+                                         exp_tbl_of(pf_exp_lds), &complete, &ops, &prof);
     if (active) out[cand] = (uint8_t)sat;
 }
 

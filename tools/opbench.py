@@ -55,7 +55,12 @@ def main():
     ap.add_argument("--budget", type=int, default=65536)
     ap.add_argument("--depth", type=int, default=32)
     ap.add_argument("--ops", default=",".join(OPS))
+    ap.add_argument("--lib", default=None, help="alternative build of libpathfeas.so (variants)")
     args = ap.parse_args()
+    if args.lib:
+        from mythril_amd import _lib
+
+        _lib.load_library(args.lib)
     eng = Engine(0)
     out = {}
     for name in args.ops.split(","):

@@ -27,7 +27,8 @@ def vals(rng):
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 20000
     exe = "/tmp/u256_host_check"
-    subprocess.check_call([CLANG, "-O2", "-std=c++17", "-o", exe, os.path.join(HERE, "u256_host_check.cpp")])
+    extra = os.environ.get("U256_FLAGS", "").split()
+    subprocess.check_call([CLANG, "-O2", "-std=c++17", *extra, "-o", exe, os.path.join(HERE, "u256_host_check.cpp")])
     rng = random.Random(1234)
     cases = [(vals(rng), vals(rng)) for _ in range(n)]
     inp = "".join(f"x {a:064x} {b:064x}\n" for a, b in cases)
