@@ -254,12 +254,16 @@ PF_INL void prof_add(UnitProf* P, uint32_t b, uint64_t dt) {
 }
 #endif
 
-// LDS for EXP's window table (pf::exp256): 8 entries x 4 limb pairs per lane, 64 lanes,
-// 4 waves per 256-thread workgroup = 64 KiB; two workgroups per CU fit in 160 KiB.
-#define PF_EXP_LDS_U2 (4 * 8 * 4 * 64)
+// LDS for EXP's window table (pf::exp256): 2^WB entries x 4 limb pairs per lane, 64 lanes,
+// 4 waves per 256-thread workgroup (2-bit window: 32 KiB, so PF_WG_PER_CU workgroups fit
+// in the CU's 160 KiB).
+#define PF_EXP_LDS_U2 (4 * PF_EXP_TBL_ENTRIES * 4 * 64)
 PF_INL uint2* exp_tbl_of(uint2* lds) {
-    return lds + (threadIdx.x >> 6) * (8 * 4 * 64) + (threadIdx.x & 63u);
+    return lds + (threadIdx.x >> 6) * (PF_EXP_TBL_ENTRIES * 4 * 64) + (threadIdx.x & 63u);
 }
+#ifndef PF_WG_PER_CU
+#define PF_WG_PER_CU 2
+#endif
 
 // Run one set's program for this lane's candidate.  Returns the lane's root (0/1);
 // *complete = 1 if the program ran to END (not short-circuited).  `ops` accumulates
@@ -515,7 +519,7 @@ PF_INL SetCtx make_ctx(const pf_set_desc* __restrict__ descs, uint32_t set,
 
 // ---- search kernel: generate + evaluate + ballot early exit ---------------------------
 // grid: one wave per (set, slice); a slice is `per_wave` consecutive candidates.
-extern "C" __global__ void __launch_bounds__(256, 2)
+extern "C" __global__ void __launch_bounds__(256, PF_WG_PER_CU)
 pf_check_kernel(const pf_set_desc* __restrict__ descs, uint32_t n_sets,
                 const uint4* __restrict__ code, const uint32_t* __restrict__ consts,
                 const uint4* __restrict__ schema, const uint32_t* __restrict__ parents,
@@ -588,7 +592,7 @@ pf_check_kernel(const pf_set_desc* __restrict__ descs, uint32_t n_sets,
 }
 
 // ---- explicit-assignment evaluation (SoA [var][limb][cand]) --------------------------
-extern "C" __global__ void __launch_bounds__(256, 2)
+extern "C" __global__ void __launch_bounds__(256, PF_WG_PER_CU)
 pf_eval_soa_kernel(const pf_set_desc* __restrict__ descs, uint32_t set,
                    const uint4* __restrict__ code, const uint32_t* __restrict__ consts,
                    const uint4* __restrict__ schema, const uint32_t* __restrict__ parents,

@@ -23,6 +23,7 @@ OPS = {
     "udiv": ir.W_UDIV, "urem": ir.W_UREM, "sdiv": ir.W_SDIV, "shl": ir.W_SHL,
     "lshr": ir.W_LSHR, "ashr": ir.W_ASHR, "exp": ir.W_EXP, "hash": ir.W_HASH,
     "ult_ite": "ult_ite", "var": "var", "concat8": "concat8",
+    "udiv_q1": "udiv_q1", "udiv_q8": "udiv_q8",
 }
 
 
@@ -39,6 +40,13 @@ def chain_program(kind, depth, seed):
         elif kind == "concat8":
             x = dag.op(ir.W_CONCAT, 256, dag.op(ir.W_EXTRACT, 248, x, aux=0),
                        dag.op(ir.W_EXTRACT, 8, y, aux=i % 32), aux=8)
+        elif kind in ("udiv_q1", "udiv_q8"):
+            # fresh 256-bit numerator each step; divisor y >> 8 (1 quotient digit) or
+            # y mod 2^32 (7-8 digits)
+            num = dag.op(ir.W_XOR, 256, x, y)
+            den = (dag.op(ir.W_LSHR, 256, y, dag.const(8, 256)) if kind == "udiv_q1" else
+                   dag.op(ir.W_AND, 256, y, dag.const(0xFFFFFFFF, 256)))
+            x = dag.op(ir.W_UDIV, 256, num, den)
         elif kind == ir.W_HASH:
             x = dag.op(ir.W_HASH, 256, x, aux=i)
         elif kind == ir.W_SHL or kind == ir.W_LSHR or kind == ir.W_ASHR:

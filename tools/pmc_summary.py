@@ -1,9 +1,13 @@
 #!/usr/bin/env python3
 """Summarise the PMC passes of tools/gpu_profile.sh into profiles/<tag>_pmc.{md,json}.
 
-HBM traffic per launch of pf_check_kernel: FETCH_SIZE (KiB, x2 — on gfx950 it reports half the
-bytes of wide coalesced reads, MI355X_MICROARCH.md §HBM) + WRITE_SIZE (KiB), each from its own
-pass, averaged over the bench's dispatches."""
+HBM traffic per launch: FETCH_SIZE (KiB, x2 — on gfx950 it reports half the bytes of wide
+coalesced reads, MI355X_MICROARCH.md §HBM) + WRITE_SIZE (KiB), each from its own pass,
+averaged over the bench's dispatches — for pf_check_kernel (config 3) and
+pf_keccak_fixed_kernel (config 4).  Hardware VALU view of pf_check_kernel: wave-level VALU
+instructions per launch (SQ_INSTS_VALU, int64 ones separately) and the effective clock
+(GRBM_GUI_ACTIVE / 8 XCDs / kernel time); bench.py turns them into the VALU issue-slot
+fraction with its live kernel time."""
 import csv
 import collections
 import json
@@ -11,12 +15,15 @@ import os
 import sys
 
 KERNEL = "pf_check_kernel"
+KECCAK = "pf_keccak_fixed_kernel"
 
 
-def per_dispatch(path):
+def per_dispatch(path, kernel=KERNEL):
     agg = collections.OrderedDict()
+    if not os.path.exists(path):
+        return []
     for r in csv.DictReader(open(path)):
-        if KERNEL not in r["Kernel_Name"]:
+        if kernel not in r["Kernel_Name"]:
             continue
         d = agg.setdefault(r["Dispatch_Id"], {})
         d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
@@ -30,9 +37,10 @@ def mean(rows, key):
 def main():
     src, tag = sys.argv[1], sys.argv[2]
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    fetch = per_dispatch(os.path.join(src, "fetch", "run_counter_collection.csv"))
-    write = per_dispatch(os.path.join(src, "write", "run_counter_collection.csv"))
-    sq = per_dispatch(os.path.join(src, "sq", "run_counter_collection.csv"))
+    csvp = lambda p: os.path.join(src, p, "run_counter_collection.csv")  # noqa: E731
+    fetch = per_dispatch(csvp("fetch"))
+    write = per_dispatch(csvp("write"))
+    sq = per_dispatch(csvp("sq"))
     fetch_b = 2 * mean(fetch, "FETCH_SIZE") * 1024
     write_b = mean(write, "WRITE_SIZE") * 1024
     keys = ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_VALU_INT32", "SQ_INSTS_VALU_INT64", "SQ_INSTS_SALU",
@@ -41,6 +49,16 @@ def main():
     out = {"kernel": KERNEL, "dispatches": len(fetch), "fetch_bytes": fetch_b, "write_bytes": write_b,
            "traffic_bytes": fetch_b + write_b, "sq": sqm,
            "workload": "bench.py default (1024 config-3 DAGs x 65536 candidates, full sweep)"}
+    clk = per_dispatch(csvp("clk"))
+    if clk:
+        out["clk"] = {k: mean(clk, k) for k in ("GRBM_GUI_ACTIVE", "SQ_BUSY_CYCLES",
+                                                 "SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU")}
+    kf, kw = per_dispatch(csvp("fetch"), KECCAK), per_dispatch(csvp("write"), KECCAK)
+    if kf and kw:
+        k = {"kernel": KECCAK, "fetch_bytes": 2 * mean(kf, "FETCH_SIZE") * 1024,
+             "write_bytes": mean(kw, "WRITE_SIZE") * 1024}
+        k["traffic_bytes"] = k["fetch_bytes"] + k["write_bytes"]
+        out["keccak"] = k
     with open(os.path.join(root, "profiles", f"{tag}_pmc.json"), "w") as f:
         json.dump(out, f, indent=1)
     lines = [f"# {tag} — PMC passes of `bench.py --steps 2 --warmup 1` ({KERNEL})", "",
@@ -48,12 +66,19 @@ def main():
              "| quantity | per launch |", "|---|---|",
              f"| FETCH_SIZE x2 (gfx950 half-count correction) | {fetch_b / 1e6:.2f} MB |",
              f"| WRITE_SIZE | {write_b / 1e6:.2f} MB |"]
-    for k in keys:
-        lines.append(f"| {k} | {sqm[k]:.4g} |")
+    for key in keys:
+        lines.append(f"| {key} | {sqm[key]:.4g} |")
+    if "clk" in out:
+        for key, v in out["clk"].items():
+            lines.append(f"| {key} (clock pass) | {v:.4g} |")
     w = sqm["SQ_WAVES"]
     lines += ["", f"per wave: {sqm['SQ_INSTS_VALU'] / w:.4g} VALU ({sqm['SQ_INSTS_VALU_INT64'] / w:.4g} int64), "
               f"{sqm['SQ_INSTS_SALU'] / w:.4g} SALU, {sqm['SQ_INSTS_BRANCH'] / w:.4g} branches, "
               f"{sqm['SQ_INSTS_SMEM'] / w:.4g} SMEM", ""]
+    if "keccak" in out:
+        k = out["keccak"]
+        lines += [f"{KECCAK} per launch: FETCH_SIZE x2 {k['fetch_bytes'] / 1e6:.1f} MB + WRITE_SIZE "
+                  f"{k['write_bytes'] / 1e6:.1f} MB (algorithmic: 96 B x 2^24 messages = 1610.6 MB)", ""]
     with open(os.path.join(root, "profiles", f"{tag}_pmc.md"), "w") as f:
         f.write("\n".join(lines) + "\n")
     print("\n".join(lines))
