@@ -94,11 +94,20 @@ PF_INL u256 pow2m1(uint32_t k) {  // 2^k - 1
 }
 
 // ---- Philox4x32-10 -------------------------------------------------------------------
+// 32 x 32 -> 64 product as ONE v_mad_u64_u32 (addend 0): the backend otherwise emits a
+// v_mul_lo_u32 + v_mul_hi_u32 pair, two quarter-rate instructions for the same product.
+PF_INL uint64_t mul_wide(uint32_t a, uint32_t m) {
+    uint64_t r, c;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(r), "=s"(c) : "v"(a), "s"(m));
+    return r;
+}
+
 PF_INL uint4 philox(uint4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
     for (int i = 0; i < 10; i++) {
-        uint32_t hi0 = __umulhi(PF_PHILOX_M0, c.x), lo0 = PF_PHILOX_M0 * c.x;
-        uint32_t hi1 = __umulhi(PF_PHILOX_M1, c.z), lo1 = PF_PHILOX_M1 * c.z;
+        const uint64_t p0 = mul_wide(c.x, PF_PHILOX_M0), p1 = mul_wide(c.z, PF_PHILOX_M1);
+        const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
         c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
         k0 += PF_PHILOX_W0;
         k1 += PF_PHILOX_W1;
