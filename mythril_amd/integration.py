@@ -139,24 +139,44 @@ def install() -> None:  # pragma: no cover - needs Mythril
     funnel.Optimize = gpu_optimize_class()
 
 
-def batch_open_states(open_states) -> int:  # pragma: no cover - needs Mythril + z3
-    """Tx-boundary batch: one GPU launch over all open states' constraint sets."""
-    from mythril.laser.ethereum.function_managers import keccak_function_manager
+def _z3_terms(raws):  # pragma: no cover - needs z3
+    """z3 ASTs -> (terms, cache key): through the assertions' SMT-LIB2 text (what
+    ``z3.Optimize.sexpr()`` prints, support/model.py:46-57) and mythril_amd.smtlib."""
+    import z3
 
+    s = z3.Optimize()
+    s.add(raws)
+    return read_query(s.sexpr()).assertions, tuple(sorted(r.get_id() for r in raws))
+
+
+def state_terms(state):
+    """One open state's query, as the funnel would pose it: ``get_all_constraints()``
+    (constraints.py:132-133 — path constraints + the keccak manager's conditions), python
+    bools dropped (support/model.py:87-93).  Constraints that already are mythril_amd.smt
+    terms (the drop-in facade) are used as they are; z3 ones go through SMT-LIB2."""
+    cs = [c for c in state.world_state.constraints.get_all_constraints() if not isinstance(c, bool)]
+    raws = [c.raw for c in cs]
+    if all(isinstance(r, T.Term) for r in raws):
+        return raws, tuple(id(r) for r in raws)
+    return _z3_terms(raws)
+
+
+def batch_open_states(open_states, kfm=None, registry: UFRegistry = DEFAULT_REGISTRY) -> int:
+    """Tx-boundary batch (svm.py:266-286): one GPU launch over every open state's
+    constraint set; each witness is parked in ``_BATCH_CACHE`` under the state's key so the
+    ``is_possible()`` pass that follows is answered without z3.  Returns the number of
+    states with a witness."""
     from .smt.gpu_check import check_sets
 
-    sync_keccak_registry(keccak_function_manager)
+    if kfm is None:  # pragma: no cover - needs Mythril
+        from mythril.laser.ethereum.function_managers import keccak_function_manager as kfm
+    sync_keccak_registry(kfm, registry)
     sets, keys = [], []
     for st in open_states:
-        cs = st.world_state.constraints.get_all_constraints()
-        raws = [c.raw for c in cs if not isinstance(c, bool)]
-        import z3
-
-        s = z3.Optimize()
-        s.add(raws)
-        sets.append(read_query(s.sexpr()).assertions)
-        keys.append(tuple(sorted(r.get_id() for r in raws)))
-    models = check_sets(sets)
+        terms, key = state_terms(st)
+        sets.append(terms)
+        keys.append(key)
+    models = check_sets(sets, registry=registry) if sets else []
     n = 0
     for k, m in zip(keys, models):
         if m is not None:
