@@ -187,33 +187,23 @@ PF_INL u256 gen_var(const SetCtx& S, uint32_t v, uint32_t cand) {
     if (sel <= 4u) {
         out = rv;
     } else if (sel <= 8u) {
-        uint32_t j = m.y % 12u, k = m.z % w;
-        if (j < 4u) {
-            out = pf::zero256();
-            out.l[0] = j;
-        } else if (j == 4u) {
-            out = pf::ones256();
-        } else if (j == 5u) {
-            out = pf::ones256();
-            out.l[0] = 0xfffffffeu;
-            // masked below: (2^w - 1) - 1 = 2^w - 2 for w > 1; w == 1 -> 0 (Python: (1-1)&1 = 0)
-            if (w < 32u) out.l[0] = ((w == 32u) ? 0xffffffffu : ((1u << w) - 1u)) - 1u;
-        } else if (j == 6u) {
-            out = pow2(w - 1u);
-        } else if (j == 7u) {
-            out = pow2m1(w - 1u);
-        } else if (j == 8u) {
-            out = pow2(k);
-        } else if (j == 9u) {
-            out = pow2m1(k);
-        } else if (j == 10u) {
-            out = pf::add256(pow2(k), pf::zero256());
-            u256 one = pf::zero256();
-            one.l[0] = 1u;
-            out = pf::add256(out, one);
-        } else {
-            out = pow2m1(160u);
-        }
+        // boundary table {0, 1, 2, 3, 2^w-1, 2^w-2, 2^(w-1), 2^(w-1)-1, 2^k, 2^k-1, 2^k+1,
+        // 2^160-1}[j] mod 2^w as ONE formula, (j >= 6 ? 2^p : 0) + delta — every entry is a
+        // power of two plus a small signed delta — instead of a 12-way branch chain the
+        // whole wave walked (lanes pick different j)
+        const uint32_t j = m.y % 12u, k = m.z % w;
+        const uint32_t p = j <= 7u ? w - 1u : (j <= 10u ? k : 160u);
+        const int32_t delta = j < 4u ? (int32_t)j
+                            : (j == 5u ? -2 : ((j == 6u || j == 8u) ? 0 : (j == 10u ? 1 : -1)));
+        u256 base = pow2(p);
+        const uint32_t usepow = j >= 6u ? 0xffffffffu : 0u;
+        u256 dl;
+        dl.l[0] = (uint32_t)delta;
+#pragma unroll
+        for (int i = 1; i < 8; i++) dl.l[i] = delta < 0 ? 0xffffffffu : 0u;
+#pragma unroll
+        for (int i = 0; i < 8; i++) base.l[i] &= usepow;
+        out = pf::add256(base, dl);
     } else if (sel <= 11u) {
         if (S.n_const > 0u) {
             const uint32_t* c = S.consts + (size_t)(m.y % S.n_const) * 8u;
