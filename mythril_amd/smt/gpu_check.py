@@ -64,11 +64,20 @@ class GpuStats:
 STATS = GpuStats()
 _lock = threading.Lock()
 _CACHE: "OrderedDict[tuple, Tuple[Lowered, List[int]]]" = OrderedDict()
+# buckets whose search found no witness, per search configuration: the search is a pure
+# function of (program, seed, budget, flags), so repeating it cannot change the answer —
+# LASER re-poses a parent's buckets at every fork below it (svm.py:351-358)
+_NEG: "OrderedDict[tuple, None]" = OrderedDict()
 
 
 def reset_cache() -> None:
     with _lock:
         _CACHE.clear()
+        _NEG.clear()
+
+
+def _neg_key(key: tuple, cfg: GpuConfig) -> tuple:
+    return (key, cfg.budget, cfg.seed, cfg.flags, cfg.hints)
 
 
 def _set_seed(constraints: Sequence[T.Term]) -> int:
@@ -123,6 +132,10 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
                 found[key] = cached
                 hits += 1
                 continue
+            if cfg.timeout_ms == 0 and _neg_key(key, cfg) in _NEG:
+                found[key] = None
+                hits += 1
+                continue
             try:
                 lo, prog = _lower_bucket(b, reg, parent, cfg.hints)
             except LoweringError as e:
@@ -150,6 +163,14 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
         db.free()
         for k in range(len(progs)):
             found[keys[k]] = None
+        if cfg.timeout_ms == 0:  # a deadline-cut search is not a complete answer
+            sat_set = set(sat)
+            with _lock:
+                for k in range(len(progs)):
+                    if k not in sat_set:
+                        _NEG[_neg_key(keys[k], cfg)] = None
+                while len(_NEG) > cfg.cache_size:
+                    _NEG.popitem(last=False)
         for k, v in zip(sat, vals):
             key = keys[k]
             w = Witness(lows[k], v, reg)

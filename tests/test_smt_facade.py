@@ -154,3 +154,47 @@ def test_keccak_interpretation_satisfies_conditions_by_construction():
     rng = np.random.default_rng(0)
     for _ in range(32):
         assert sv.evaluate([int.from_bytes(rng.bytes(32), "little")])
+
+
+def test_check_sets_caches_witnessless_buckets(monkeypatch):
+    """A bucket whose search found no witness is not lowered or searched again under the
+    same search configuration (the search is deterministic); a deadline-cut search is not
+    cached.  The engine is a stand-in that finds nothing (host logic only)."""
+    import mythril_amd.engine as E
+    from mythril_amd.smt import gpu_check
+
+    uploads = []
+
+    class _Res:
+        def __init__(self, n):
+            self.found = np.full(n, 0xFFFFFFFF, dtype=np.uint32)
+            self.kernel_ms, self.cands_decided = 0.0, 0
+
+    class _DB:
+        def __init__(self, n):
+            self.n = n
+
+        def free(self):
+            pass
+
+    class _Eng:
+        def upload(self, progs):
+            uploads.append(len(progs))
+            return _DB(len(progs))
+
+        def check(self, db, **kw):
+            return _Res(db.n)
+
+    monkeypatch.setattr(E, "get_engine", lambda *a, **k: _Eng())
+    gpu_check.reset_cache()
+    x, y = symbol_factory.BitVecSym("x", 256), symbol_factory.BitVecSym("y", 256)
+    sets = [[(x == symbol_factory.BitVecVal(5, 256)).raw, ULT(y, symbol_factory.BitVecVal(3, 256)).raw]]
+    assert gpu_check.check_sets(sets) == [None]
+    assert uploads == [2]                      # two independence buckets searched
+    assert gpu_check.check_sets(sets) == [None]
+    assert uploads == [2]                      # both answered from the negative cache
+    cfg = gpu_check.GpuConfig(timeout_ms=5)
+    gpu_check.check_sets(sets, config=cfg)
+    gpu_check.check_sets(sets, config=cfg)
+    assert uploads == [2, 2, 2]                # deadline searches are never cached
+    gpu_check.reset_cache()
