@@ -266,3 +266,27 @@ def test_exp_split_edges(engine):
         got = engine.eval_assignments(db, 0, ir.pack_assignments(prog, cands))
         bad = np.nonzero(~got)[0]
         assert bad.size == 0, (w, [[hex(v) for v in cands[i]] for i in bad[:3]])
+
+
+@pytest.mark.parametrize("name", ["udiv", "urem", "sdiv", "srem", "smod"])
+def test_division_one_limb_divisor_waves(engine, name):
+    """Whole waves whose divisors fit one 32-bit limb take the short-division path
+    (pf::udivrem256); zero divisors included (z3 conventions), signed forms through the
+    magnitudes (a negative 256-bit divisor is wide, so those lanes use positives)."""
+    fn = {"udiv": O.bvudiv, "urem": O.bvurem, "sdiv": O.bvsdiv, "srem": O.bvsrem,
+          "smod": O.bvsmod}[name]
+    rng = np.random.default_rng(0xD1 + len(name))
+    w = 256
+    prog = _op_program(name, w)
+    db = engine.upload([prog])
+    cands = []
+    for i in range(4096):
+        a = _rand_operand(rng, w)
+        b = [0, 1, 2, 3, 0xFFFFFFFF, 0x80000000, int(rng.integers(0, 1 << 32))][i % 7]
+        r = fn(a, b, w)
+        cands.append([a, b, r])
+        cands.append([a, b, r ^ (1 << int(rng.integers(0, w)))])
+    got = engine.eval_assignments(db, 0, ir.pack_assignments(prog, cands))
+    want = np.array([i % 2 == 0 for i in range(len(cands))])
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, (name, [[hex(v) for v in cands[i]] for i in bad[:3]])
