@@ -290,3 +290,29 @@ def test_division_one_limb_divisor_waves(engine, name):
     want = np.array([i % 2 == 0 for i in range(len(cands))])
     bad = np.nonzero(got != want)[0]
     assert bad.size == 0, (name, [[hex(v) for v in cands[i]] for i in bad[:3]])
+
+
+@pytest.mark.parametrize("name", ["udiv", "urem", "sdiv", "smod"])
+def test_division_one_digit_quotient_waves(engine, name):
+    """Whole waves whose quotients fit one 32-bit digit (bitlen(a) <= bitlen(b) + 31) take
+    the f64-estimate path of pf::udivrem256: exact multiples, multiples minus one and
+    random operands around the boundary."""
+    fn = {"udiv": O.bvudiv, "urem": O.bvurem, "sdiv": O.bvsdiv, "smod": O.bvsmod}[name]
+    rng = np.random.default_rng(0x0D16 + len(name))
+    w = 256
+    prog = _op_program(name, w)
+    db = engine.upload([prog])
+    cands = []
+    for i in range(4096):
+        lb = int(rng.integers(33, 255))
+        b = int.from_bytes(rng.bytes(32), "little") % (1 << lb) | (1 << (lb - 1))
+        k = int(rng.integers(0, 1 << 31))
+        a = [b * k, b * k + b - 1, b * k + 1,
+             int.from_bytes(rng.bytes(32), "little") % (1 << min(255, lb + 30))][i % 4] % (1 << 255)
+        r = fn(a, b, w)
+        cands.append([a, b, r])
+        cands.append([a, b, r ^ (1 << int(rng.integers(0, w)))])
+    got = engine.eval_assignments(db, 0, ir.pack_assignments(prog, cands))
+    want = np.array([i % 2 == 0 for i in range(len(cands))])
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, (name, [[hex(v) for v in cands[i]] for i in bad[:3]])
