@@ -124,33 +124,30 @@ struct SetCtx {
     uint32_t k0, k1;      // Philox key
 };
 
-// candidate value of variable v (include/pf_bytecode.h generator contract)
+// candidate value of variable v (include/pf_bytecode.h generator contract).
+// Laid out for latency, not branches: the three Philox blocks depend only on (cand, v, key)
+// and are formed before anything waits on the schema, parent or constant loads; the
+// strategy arms (random / boundary / constant +-1 / parent mutation / small) are each
+// computed for every lane and selected, so the wave runs one straight sequence instead of
+// walking a lane-divergent if-chain; the per-variable kind stays a (uniform) branch.
 PF_INL u256 gen_var(const SetCtx& S, uint32_t v, uint32_t cand) {
-    uint4 sc = S.schema[v];  // uniform -> scalar load
-    uint32_t kind = sc.x & 0xffu, w = (sc.x >> 8) & 0x3ffu;
-    uint32_t hint0 = sc.y, hint1 = sc.z, pslot = sc.w;
-    u256 out;
-    if (cand == 0u && pslot != PF_NO_PARENT) {
-        const uint32_t* p = S.parents + (size_t)pslot * 8u;
+    const uint4 m = philox(make_uint4(cand, v, 2u, 0u), S.k0, S.k1);
+    const uint4 r0 = philox(make_uint4(cand, v, 0u, 0u), S.k0, S.k1);
+    const uint4 r1 = philox(make_uint4(cand, v, 1u, 0u), S.k0, S.k1);
+    const uint4 sc = S.schema[v];  // uniform -> scalar load
+    const uint32_t kind = sc.x & 0xffu, w = (sc.x >> 8) & 0x3ffu;
+    const uint32_t hint0 = sc.y, hint1 = sc.z, pslot = sc.w;
+    const bool has_parent = pslot != PF_NO_PARENT;
+    u256 par = pf::zero256();
+    if (has_parent) {
+        const uint32_t* pp = S.parents + (size_t)pslot * 8u;
 #pragma unroll
-        for (int i = 0; i < 8; i++) out.l[i] = p[i];
-        maskw(out, w);
-        return out;
+        for (int i = 0; i < 8; i++) par.l[i] = pp[i];
     }
-    uint4 m = philox(make_uint4(cand, v, 2u, 0u), S.k0, S.k1);
-    if (pslot != PF_NO_PARENT && (cand & 1u) && (m.w & ((4u << ((cand >> 1) & 3u)) - 1u)) != 0u) {
-        // neighbourhood candidate of the parent model: keep the parent value
-        const uint32_t* p = S.parents + (size_t)pslot * 8u;
-#pragma unroll
-        for (int i = 0; i < 8; i++) out.l[i] = p[i];
-        maskw(out, w);
-        return out;
-    }
-    uint4 r0 = philox(make_uint4(cand, v, 0u, 0u), S.k0, S.k1);
-    uint4 r1 = philox(make_uint4(cand, v, 1u, 0u), S.k0, S.k1);
     u256 rv;
     rv.l[0] = r0.x; rv.l[1] = r0.y; rv.l[2] = r0.z; rv.l[3] = r0.w;
     rv.l[4] = r1.x; rv.l[5] = r1.y; rv.l[6] = r1.z; rv.l[7] = r1.w;
+    u256 out = pf::zero256();
     if (kind == PF_VK_KECCAK) {
         const uint32_t* lo = S.consts + (size_t)hint0 * 8u;
         u256 k = pf::zero256();
@@ -162,77 +159,79 @@ PF_INL u256 gen_var(const SetCtx& S, uint32_t v, uint32_t cand) {
 #pragma unroll
         for (int i = 0; i < 8; i++) base.l[i] = lo[i];
         out = pf::add256(base, k);
-        maskw(out, w);
-        return out;
-    }
-    if (kind == PF_VK_SMALL) {
-        out = pf::zero256();
+    } else if (kind == PF_VK_SMALL) {
         out.l[0] = (hint0 == 0xffffffffu) ? r0.x : (r0.x % (hint0 + 1u));
-        maskw(out, w);
-        return out;
-    }
-    if (kind == PF_VK_BOOL) {
-        out = pf::zero256();
+    } else if (kind == PF_VK_BOOL) {
         out.l[0] = r0.x & 1u;
-        return out;
-    }
-    if (kind == PF_VK_ACTOR && (m.y & 3u) < hint1) {
-        const uint32_t* a = S.consts + (size_t)(hint0 + (m.y & 3u)) * 8u;
-#pragma unroll
-        for (int i = 0; i < 8; i++) out.l[i] = a[i];
-        maskw(out, w);
-        return out;
-    }
-    uint32_t sel = m.x & 15u;
-    if (sel <= 4u) {
-        out = rv;
-    } else if (sel <= 8u) {
-        // boundary table {0, 1, 2, 3, 2^w-1, 2^w-2, 2^(w-1), 2^(w-1)-1, 2^k, 2^k-1, 2^k+1,
-        // 2^160-1}[j] mod 2^w as ONE formula, (j >= 6 ? 2^p : 0) + delta — every entry is a
-        // power of two plus a small signed delta — instead of a 12-way branch chain the
-        // whole wave walked (lanes pick different j)
-        const uint32_t j = m.y % 12u, k = m.z % w;
-        const uint32_t p = j <= 7u ? w - 1u : (j <= 10u ? k : 160u);
-        const int32_t delta = j < 4u ? (int32_t)j
-                            : (j == 5u ? -2 : ((j == 6u || j == 8u) ? 0 : (j == 10u ? 1 : -1)));
-        u256 base = pow2(p);
-        const uint32_t usepow = j >= 6u ? 0xffffffffu : 0u;
-        u256 dl;
-        dl.l[0] = (uint32_t)delta;
-#pragma unroll
-        for (int i = 1; i < 8; i++) dl.l[i] = delta < 0 ? 0xffffffffu : 0u;
-#pragma unroll
-        for (int i = 0; i < 8; i++) base.l[i] &= usepow;
-        out = pf::add256(base, dl);
-    } else if (sel <= 11u) {
+    } else {
+        const uint32_t sel = m.x & 15u;
+        // constant +-1 arm (sel 9..11): per-lane gather, issued early
+        u256 cst = rv;
         if (S.n_const > 0u) {
             const uint32_t* c = S.consts + (size_t)(m.y % S.n_const) * 8u;
 #pragma unroll
-            for (int i = 0; i < 8; i++) out.l[i] = c[i];
-            uint32_t dsel = m.z % 3u;
-            u256 dlt = (dsel == 0u) ? pf::zero256() : ((dsel == 1u) ? pow2(0u) : pf::ones256());
-            out = pf::add256(out, dlt);
-        } else {
-            out = rv;
+            for (int i = 0; i < 8; i++) cst.l[i] = c[i];
+            const uint32_t dsel = m.z % 3u;  // +0, +1, -1
+            u256 dl;
+            dl.l[0] = dsel == 0u ? 0u : (dsel == 1u ? 1u : 0xffffffffu);
+#pragma unroll
+            for (int i = 1; i < 8; i++) dl.l[i] = dsel == 2u ? 0xffffffffu : 0u;
+            cst = pf::add256(cst, dl);
         }
-    } else if (sel <= 13u) {
-        if (pslot != PF_NO_PARENT) {
-            const uint32_t* p = S.parents + (size_t)pslot * 8u;
+        // boundary arm (sel 5..8): {0, 1, 2, 3, 2^w-1, 2^w-2, 2^(w-1), 2^(w-1)-1, 2^k, 2^k-1,
+        // 2^k+1, 2^160-1}[j] mod 2^w as one formula, (j >= 6 ? 2^p : 0) + delta
+        u256 bnd;
+        {
+            const uint32_t j = m.y % 12u, k = m.z % w;
+            const uint32_t p = j <= 7u ? w - 1u : (j <= 10u ? k : 160u);
+            const int32_t delta = j < 4u ? (int32_t)j
+                                : (j == 5u ? -2 : ((j == 6u || j == 8u) ? 0 : (j == 10u ? 1 : -1)));
+            u256 base = pow2(p);
+            const uint32_t usepow = j >= 6u ? 0xffffffffu : 0u;
+            u256 dl;
+            dl.l[0] = (uint32_t)delta;
 #pragma unroll
-            for (int i = 0; i < 8; i++) out.l[i] = p[i];
-            if ((m.y & 3u) == 0u) {
-                u256 f = pow2(m.z % w);
+            for (int i = 1; i < 8; i++) dl.l[i] = delta < 0 ? 0xffffffffu : 0u;
 #pragma unroll
-                for (int i = 0; i < 8; i++) out.l[i] ^= f.l[i];
+            for (int i = 0; i < 8; i++) base.l[i] &= usepow;
+            bnd = pf::add256(base, dl);
+        }
+        // parent-mutation arm (sel 12..13): one bit of the parent flipped in a quarter of
+        // the lanes; without a parent, a random byte
+        u256 mut = pf::zero256();
+        if (has_parent) {
+            const u256 f = pow2(m.z % w);
+            const uint32_t flip = (m.y & 3u) == 0u ? 0xffffffffu : 0u;
+#pragma unroll
+            for (int i = 0; i < 8; i++) mut.l[i] = par.l[i] ^ (f.l[i] & flip);
+        } else {
+            mut.l[0] = r0.x & 0xffu;
+        }
+        // small arm (sel 14..15): 1..16 random low bits
+        const uint32_t nb = 1u + (m.y & 15u);
+        const uint32_t small = r0.x & ((nb >= 32u) ? 0xffffffffu : ((1u << nb) - 1u));
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const uint32_t sm = i == 0 ? small : 0u;
+            out.l[i] = sel <= 4u ? rv.l[i]
+                     : (sel <= 8u ? bnd.l[i] : (sel <= 11u ? cst.l[i] : (sel <= 13u ? mut.l[i] : sm)));
+        }
+        if (kind == PF_VK_ACTOR) {
+            // the actor set (transaction/symbolic.py:215) in most lanes
+            const uint32_t ai = m.y & 3u;
+            if (ai < hint1) {
+                const uint32_t* ap = S.consts + (size_t)(hint0 + ai) * 8u;
+#pragma unroll
+                for (int i = 0; i < 8; i++) out.l[i] = ap[i];
             }
-        } else {
-            out = pf::zero256();
-            out.l[0] = r0.x & 0xffu;
         }
-    } else {
-        out = pf::zero256();
-        uint32_t nb = 1u + (m.y & 15u);
-        out.l[0] = r0.x & ((nb >= 32u) ? 0xffffffffu : ((1u << nb) - 1u));
+    }
+    // the parent model itself (candidate 0) and its neighbourhood (odd candidates keep the
+    // parent value of most variables)
+    if (has_parent) {
+        const bool keep = cand == 0u || ((cand & 1u) && (m.w & ((4u << ((cand >> 1) & 3u)) - 1u)) != 0u);
+#pragma unroll
+        for (int i = 0; i < 8; i++) out.l[i] = keep ? par.l[i] : out.l[i];
     }
     maskw(out, w);
     return out;
