@@ -189,8 +189,8 @@ def valu_view(pmc, kernel_s):
     clk = pmc.get("clk")
     if clk and clk.get("GRBM_GUI_ACTIVE"):
         cyc = clk["GRBM_GUI_ACTIVE"] / 8.0
+        # both counts from the same PMC run: independent of this run's kernel time
         out["issue_frac_eff_clock"] = 2.0 * clk["SQ_INSTS_VALU"] / (1024 * cyc)
-        out["eff_clock_MHz"] = cyc / kernel_s / 1e6
     return out
 
 
