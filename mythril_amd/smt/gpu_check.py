@@ -19,6 +19,7 @@ re-evaluating up to 100 models per query.
 
 from __future__ import annotations
 
+import os
 import threading
 from collections import OrderedDict
 from dataclasses import dataclass, field
@@ -43,6 +44,11 @@ class GpuConfig:
     split: bool = True           # independence buckets
     hints: bool = True           # constraint-directed parent (hint) models
     cache_size: int = 1 << 16    # bucket witnesses kept
+    # host lowering workers (spawned processes; terms re-intern on unpickling): used for a
+    # call with at least `parallel_min` new buckets — the lowering is pure Python and was
+    # 95 % of the corpus' wall time on one core
+    workers: int = int(os.environ.get("PF_LOWER_WORKERS", "0")) or min(16, os.cpu_count() or 1)
+    parallel_min: int = 48
 
 
 CONFIG = GpuConfig()
@@ -95,6 +101,61 @@ def _lower_bucket(bucket: List[T.Term], reg: UFRegistry, parent: Optional[dict],
     return lo, lower(lo.dag, seed=_set_seed(bucket))
 
 
+def _lower_chunk(job):
+    """Worker: lower a chunk of buckets; the DAG stays behind (witnesses need only the
+    variable / UF / array-read terms)."""
+    items, reg, hints = job
+    out = []
+    for bucket, parent in items:
+        try:
+            lo, prog = _lower_bucket(bucket, reg, parent, hints)
+            out.append((Lowered(None, lo.var_terms, lo.uf_apps, lo.array_reads), prog, None))
+        except LoweringError as e:
+            out.append((None, None, str(e)))
+    return out
+
+
+_POOL = None
+_POOL_N = 0
+
+
+def _pool(n: int):
+    global _POOL, _POOL_N
+    if _POOL is None or _POOL_N != n:
+        import multiprocessing as mp
+
+        if _POOL is not None:
+            _POOL.terminate()
+        # spawn, never fork: the parent may hold an initialised HIP runtime
+        _POOL = mp.get_context("spawn").Pool(n)
+        _POOL_N = n
+        import atexit
+
+        atexit.register(_shutdown_pool)
+    return _POOL
+
+
+def _shutdown_pool() -> None:
+    global _POOL
+    if _POOL is not None:
+        _POOL.terminate()
+        _POOL.join()
+        _POOL = None
+
+
+def _lower_all(jobs, reg: UFRegistry, cfg: GpuConfig):
+    """[(bucket, parent)] -> [(Lowered | None, Program | None, error | None)], in order."""
+    n = min(cfg.workers, len(jobs))
+    if n <= 1 or len(jobs) < cfg.parallel_min:
+        return _lower_chunk((jobs, reg, cfg.hints))
+    per = max(1, (len(jobs) + 4 * n - 1) // (4 * n))
+    chunks = [(jobs[i:i + per], reg, cfg.hints) for i in range(0, len(jobs), per)]
+    out = []
+    for part in _pool(n).map(_lower_chunk, chunks):
+        out.extend(part)
+    return out
+
+
 def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] = None,
                parents: Optional[Sequence[Optional[dict]]] = None,
                config: Optional[GpuConfig] = None) -> List[Optional[WitnessModel]]:
@@ -114,6 +175,7 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
     # the keccak interpretation depends on the registry (intervals, concrete hashes): a
     # cached witness is only valid for the registry state it was found under
     reg_sig = tuple(sorted((n, s.lo, len(s.concrete)) for n, s in reg.keccak.items()))
+    jobs, job_keys, pending = [], [], set()
     for i, cs in enumerate(sets):
         cs = [c for c in cs if c is not T.TRUE]
         if any(c is T.FALSE for c in cs):
@@ -121,11 +183,11 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
             continue
         parent = parents[i] if parents else None
         bks = buckets(cs) if cfg.split else [cs]
-        ks, ok = [], True
+        ks = []
         for b in bks:
             key = (tuple(b), tuple(sorted(parent.items())) if parent else None, reg_sig)
             ks.append(key)
-            if key in found or key in todo:
+            if key in found or key in pending:
                 continue
             cached = _CACHE.get(key)
             if cached is not None:
@@ -136,22 +198,26 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
                 found[key] = None
                 hits += 1
                 continue
-            try:
-                lo, prog = _lower_bucket(b, reg, parent, cfg.hints)
-            except LoweringError as e:
-                err = str(e).split(":")[0][:60]
-                with _lock:
-                    STATS.lowering_failures[err] = STATS.lowering_failures.get(err, 0) + 1
-                found[key] = None
-                ok = False
-                continue
-            todo[key] = len(progs)
-            progs.append(prog)
-            lows.append(lo)
-            keys.append(key)
-        if ok and all(found.get(k, 0) is not None for k in ks):
-            n_lowered += 1
+            pending.add(key)
+            jobs.append((b, parent))
+            job_keys.append(key)
         set_buckets.append(ks)
+    failed = set()
+    for key, (lo, prog, err) in zip(job_keys, _lower_all(jobs, reg, cfg)):
+        if err is not None:
+            err = err.split(":")[0][:60]
+            with _lock:
+                STATS.lowering_failures[err] = STATS.lowering_failures.get(err, 0) + 1
+            found[key] = None
+            failed.add(key)
+            continue
+        todo[key] = len(progs)
+        progs.append(prog)
+        lows.append(lo)
+        keys.append(key)
+    for ks in set_buckets:
+        if ks is not None and not any(k in failed or (k in found and found[k] is None) for k in ks):
+            n_lowered += 1
 
     res = None
     if progs:

@@ -43,6 +43,11 @@ class Term:
         cls._table[key] = t
         return t
 
+    # pickling re-interns: a term sent to a lowering worker (or back) is rebuilt through
+    # the constructor, so it is the receiving process's canonical node for that structure
+    def __reduce__(self):
+        return (Term, (self.op, self.sort, self.args, self.val))
+
     # identity semantics: hash-consing makes structural equality == object identity
     def __hash__(self):
         return self._h

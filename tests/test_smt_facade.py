@@ -198,3 +198,48 @@ def test_check_sets_caches_witnessless_buckets(monkeypatch):
     gpu_check.check_sets(sets, config=cfg)
     assert uploads == [2, 2, 2]                # deadline searches are never cached
     gpu_check.reset_cache()
+
+
+def test_parallel_lowering_matches_sequential(monkeypatch):
+    """Lowering in spawned worker processes (terms re-intern on unpickling) yields the same
+    programs, in the same order, as lowering in-process."""
+    import mythril_amd.engine as E
+    from mythril_amd import corpus
+    from mythril_amd.smt import gpu_check
+
+    uploaded = []
+
+    class _Res:
+        def __init__(self, n):
+            self.found = np.full(n, 0xFFFFFFFF, dtype=np.uint32)
+            self.kernel_ms, self.cands_decided = 0.0, 0
+
+    class _DB:
+        def __init__(self, n):
+            self.n = n
+
+        def free(self):
+            pass
+
+    class _Eng:
+        def upload(self, progs):
+            uploaded.append(ir.Batch(progs))
+            return _DB(len(progs))
+
+        def check(self, db, **kw):
+            return _Res(db.n)
+
+        def keccak256(self, msgs):
+            return [O.keccak256(m) for m in msgs]
+
+    monkeypatch.setattr(E, "get_engine", lambda *a, **k: _Eng())
+    c = corpus.build(4, 2, seed=7)
+    sets = [q.constraints for q in c.queries]
+    for workers in (1, 2):
+        gpu_check.reset_cache()
+        cfg = gpu_check.GpuConfig(workers=workers, parallel_min=1)
+        gpu_check.check_sets(sets, registry=c.kfm.registry, config=cfg)
+    seq, par = uploaded
+    assert np.array_equal(seq.code, par.code) and np.array_equal(seq.consts, par.consts)
+    assert np.array_equal(seq.schema, par.schema) and np.array_equal(seq.descs, par.descs)
+    gpu_check.reset_cache()
