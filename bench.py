@@ -315,6 +315,8 @@ def main():
                                                 args.cpu_sample_s)
         print(json.dumps(line), flush=True)
     if dist is not None:
+        # rank 0 spends a few seconds on the host-side legs above: leave together
+        dist.barrier()
         dist.destroy_process_group()
 
 
