@@ -161,6 +161,33 @@ def keccak_leg(args, torch, rank, world):
                                  "issues ~4,280 VALU instructions per permutation"}}
 
 
+def early_leg(args, eng, batch, torch, dist):
+    """SURVEY §8(d) config 3 asks for both sweeps: the same DAGs searched with ballot early
+    exit and per-assert short-circuit on (the engine's production flags).  Reported: the
+    candidates decided per second (a lane whose set is already false at an assert stops
+    there), sets with a witness, and the kernel time of one launch."""
+    from mythril_amd import ir
+
+    flags = ir.FLAG_EARLY_EXIT | ir.FLAG_SHORTCIRCUIT | ir.FLAG_COUNT_OPS
+    eng.check(batch, budget=args.budget, seed=args.seed, flags=flags)  # warm
+    r = eng.check(batch, budget=args.budget, seed=args.seed, flags=flags)
+    vals = [float(r.cands_decided), r.kernel_ms / 1e3, float(int(r.sat.sum()))]
+    if dist is not None:
+        t = torch.tensor(vals, dtype=torch.float64, device="cuda")
+        s_ = t[[0, 2]].clone()
+        dist.all_reduce(s_, op=dist.ReduceOp.SUM)
+        m_ = t[1:2].clone()
+        dist.all_reduce(m_, op=dist.ReduceOp.MAX)
+        vals = [float(s_[0]), float(m_[0]), float(s_[1])]
+    n_sets = args.sets * (dist.get_world_size() if dist is not None else 1)
+    return {"flags": "early_exit|shortcircuit", "cands_decided_per_s": vals[0] / vals[1],
+            "set_verdicts_per_s": n_sets / vals[1],
+            "sets_with_witness": int(vals[2]), "sets": n_sets, "kernel_ms": 1e3 * vals[1],
+            "note": "same unplanted config-3 DAGs as the timed sweep, one launch: a set stops at "
+                    "the wave that finds its first witness; witness-free sets sweep the whole "
+                    "budget, a lane stops at its first false assert"}
+
+
 def pmc_traffic(args):
     """HBM bytes per launch of pf_check_kernel from the newest committed PMC summary
     (profiles/*_pmc.json, written by tools/pmc_summary.py from separate rocprofv3 --pmc
@@ -262,6 +289,16 @@ def main():
         local = np.concatenate(founds)
         gather_found(local, rank * len(local), world * len(local))
 
+    # node evaluations of the timed steps: every instruction of every set runs for every
+    # candidate in the full sweep (also report node-evals/s)
+    nodes_per_step = [sum(len(p.code) for p in step_progs[k]) for k in range(args.warmup, n_steps)]
+    tot_nodes = float(sum(nodes_per_step) * args.budget)
+    if dist is not None:
+        x = torch.tensor([tot_nodes], dtype=torch.float64, device="cuda")
+        dist.all_reduce(x, op=dist.ReduceOp.SUM)
+        tot_nodes = float(x.item())
+
+    early = early_leg(args, eng, batches[args.warmup], torch, dist) if args.mode == "full" else None
     kec = keccak_leg(args, torch, rank, world) if args.keccak_log2 > 0 else None
 
     if rank == 0:
@@ -296,6 +333,8 @@ def main():
                                "2-adic EXP (DESIGN.md §3) needs ~35 product-equivalents, so frac "
                                "exceeds 1 on this EXP-heavy mix. roofline.hw is the hardware view: "
                                "PMC VALU instructions per launch over the SIMDs' issue slots",
+            "node_evals_per_s": tot_nodes / max_dt,
+            "early_exit": early,
             "gen_upload_s": t_gen,
         }
         if args.keccak_log2 > 0:
