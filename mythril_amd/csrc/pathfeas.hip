@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -28,6 +29,12 @@ hipStream_t g_stream = nullptr;
 hipEvent_t g_ev0 = nullptr, g_ev1 = nullptr;
 uint32_t* g_scratch_u32 = nullptr;  // small device scratch (counters, t0)
 int g_num_cus = 256;
+// search-kernel waves launched per CU (PF_WAVES_PER_CU overrides both).  Measured on config 3
+// (1024 sets x 65,536 candidates, profiles/r01_wavesweep.md): the full sweep gains 17 % from
+// 64 -> 1024 (finer slices even out the sets' unequal costs in the last round of waves);
+// with early exit, more concurrent slices of a set run past its first witness, so 256.
+uint32_t g_waves_per_cu_full = 1024;
+uint32_t g_waves_per_cu_early = 256;
 
 int fail(const char* fmt, ...) {
     char buf[512];
@@ -80,8 +87,10 @@ hipStream_t pick_stream(void* s) { return s ? reinterpret_cast<hipStream_t>(s) :
 
 // launch geometry for the search kernel: enough waves to fill 256 CUs several times over,
 // each wave walking >= 64 candidates of one set.
-void geometry(uint32_t n_sets, uint32_t budget, uint32_t* per_wave, uint32_t* slices) {
-    const uint64_t target_waves = (uint64_t)g_num_cus * 8u * 8u;
+void geometry(uint32_t n_sets, uint32_t budget, uint32_t flags, uint32_t* per_wave,
+              uint32_t* slices) {
+    const uint64_t target_waves =
+        (uint64_t)g_num_cus * ((flags & PF_FLAG_EARLY_EXIT) ? g_waves_per_cu_early : g_waves_per_cu_full);
     uint64_t groups = (budget + 63u) / 64u;  // 64-candidate groups per set
     uint64_t sl = (target_waves + n_sets - 1) / std::max<uint32_t>(n_sets, 1u);
     sl = std::max<uint64_t>(1, std::min<uint64_t>(sl, groups));
@@ -106,7 +115,7 @@ int check_launch(Batch* B, uint64_t gseed, uint32_t budget, uint32_t flags, uint
         return 0;
     }
     uint32_t per_wave, slices;
-    geometry((uint32_t)B->n_sets, budget, &per_wave, &slices);
+    geometry((uint32_t)B->n_sets, budget, flags, &per_wave, &slices);
     const uint64_t waves = (uint64_t)B->n_sets * slices;
     if (waves > 0xffffffffull) return fail("batch too large: %llu waves", (unsigned long long)waves);
     const uint32_t blocks = (uint32_t)((waves + 3) / 4);
@@ -174,6 +183,10 @@ int pf_init(int device) {
     if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
         return fail("pf_init: device %d is %s, this build targets gfx950", device, prop.gcnArchName);
     g_num_cus = prop.multiProcessorCount;
+    if (const char* e = getenv("PF_WAVES_PER_CU")) {
+        long v = strtol(e, nullptr, 10);
+        if (v >= 8 && v <= 4096) g_waves_per_cu_full = g_waves_per_cu_early = (uint32_t)v;
+    }
     HIPCHK(hipStreamCreateWithFlags(&g_stream, hipStreamNonBlocking));
     HIPCHK(hipEventCreate(&g_ev0));
     HIPCHK(hipEventCreate(&g_ev1));
