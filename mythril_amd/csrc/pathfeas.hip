@@ -30,11 +30,12 @@ hipEvent_t g_ev0 = nullptr, g_ev1 = nullptr;
 uint32_t* g_scratch_u32 = nullptr;  // small device scratch (counters, t0)
 int g_num_cus = 256;
 // search-kernel waves launched per CU (PF_WAVES_PER_CU overrides both).  Measured on config 3
-// (1024 sets x 65,536 candidates, profiles/r01_wavesweep.md): the full sweep gains 17 % from
-// 64 -> 1024 (finer slices even out the sets' unequal costs in the last round of waves);
-// with early exit, more concurrent slices of a set run past its first witness, so 256.
-uint32_t g_waves_per_cu_full = 1024;
-uint32_t g_waves_per_cu_early = 256;
+// (1024 sets x 65,536 candidates, profiles/r01_wavesweep.md): with the longest-first set order
+// the full sweep peaks at 512 (finer slices even out the sets' unequal costs in the last round
+// of waves; 64 was 17 % slower); with early exit every concurrently running slice of a set
+// evaluates past its first witness, so fewer slices: 128.
+uint32_t g_waves_per_cu_full = 512;
+uint32_t g_waves_per_cu_early = 128;
 
 int fail(const char* fmt, ...) {
     char buf[512];
@@ -64,6 +65,7 @@ struct Batch {
     uint4* d_schema = nullptr;
     uint32_t* d_parents = nullptr;
     uint32_t* d_found = nullptr;
+    uint32_t* d_order = nullptr;  // set ids, most expensive first (search-kernel wave order)
 };
 
 int ensure_init_locked() {
@@ -121,7 +123,7 @@ int check_launch(Batch* B, uint64_t gseed, uint32_t budget, uint32_t flags, uint
     const uint32_t blocks = (uint32_t)((waves + 3) / 4);
     const uint64_t deadline = timeout_ms ? (uint64_t)timeout_ms * 100000ull : 0ull;  // 100 MHz
     HIPCHK(hipEventRecord(g_ev0, st));
-    hipLaunchKernelGGL(pf_check_kernel, dim3(blocks), dim3(256), 0, st, B->d_descs,
+    hipLaunchKernelGGL(pf_check_kernel, dim3(blocks), dim3(256), 0, st, B->d_descs, B->d_order,
                        (uint32_t)B->n_sets, B->d_code, B->d_consts, B->d_schema, B->d_parents,
                        gseed, budget, per_wave, slices, flags, deadline, d_t0, d_found, d_counters);
     HIPCHK(hipGetLastError());
@@ -299,6 +301,28 @@ int pf_batch_create(const uint32_t* code, size_t n_ins, const uint32_t* consts, 
     rc |= upload(&B->d_parents, parents, n_parents * 32);
     rc |= upload(&B->d_descs, descs, n_sets * sizeof(pf_set_desc));
     rc |= upload(&B->d_found, nullptr, n_sets * 4);
+    // Longest-first wave order: waves are dispatched in index order, so mapping the first
+    // waves to the most expensive sets leaves the cheap ones for the last, partly filled
+    // round.  Weights are measured SIMD cycles per instruction relative to a cheap op
+    // (EXP ~7.1k, a division ~2.6k, MUL ~750, cheap ~650).
+    {
+        std::vector<uint64_t> cost(n_sets, 0);
+        for (size_t s = 0; s < n_sets; ++s) {
+            const uint4* I = reinterpret_cast<const uint4*>(code) + descs[s].code_off;
+            uint64_t c = 0;
+            for (uint32_t i = 0; i < descs[s].n_ins; ++i) {
+                const uint32_t op = I[i].x & 0xffu;
+                c += op == PF_W_EXP ? 110u : op == PF_W_MUL ? 12u
+                     : pf_op_unit(op) == PF_U_DIV ? 40u : 10u;
+            }
+            cost[s] = c;
+        }
+        std::vector<uint32_t> order(n_sets);
+        for (size_t s = 0; s < n_sets; ++s) order[s] = (uint32_t)s;
+        std::stable_sort(order.begin(), order.end(),
+                         [&](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
+        rc |= upload(&B->d_order, order.data(), n_sets * 4);
+    }
     if (rc) {
         delete B;
         return -1;
@@ -319,6 +343,7 @@ int pf_batch_free(uint64_t handle) {
     hipFree(B->d_parents);
     hipFree(B->d_descs);
     hipFree(B->d_found);
+    hipFree(B->d_order);
     delete B;
     return 0;
 }

@@ -518,7 +518,8 @@ PF_INL SetCtx make_ctx(const pf_set_desc* __restrict__ descs, uint32_t set,
 // ---- search kernel: generate + evaluate + ballot early exit ---------------------------
 // grid: one wave per (set, slice); a slice is `per_wave` consecutive candidates.
 extern "C" __global__ void __launch_bounds__(256, PF_WG_PER_CU)
-pf_check_kernel(const pf_set_desc* __restrict__ descs, uint32_t n_sets,
+pf_check_kernel(const pf_set_desc* __restrict__ descs, const uint32_t* __restrict__ order,
+                uint32_t n_sets,
                 const uint4* __restrict__ code, const uint32_t* __restrict__ consts,
                 const uint4* __restrict__ schema, const uint32_t* __restrict__ parents,
                 uint64_t gseed, uint32_t budget, uint32_t per_wave, uint32_t slices,
@@ -527,7 +528,7 @@ pf_check_kernel(const pf_set_desc* __restrict__ descs, uint32_t n_sets,
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
     if (wave >= n_sets * slices) return;
-    const uint32_t set = __builtin_amdgcn_readfirstlane(wave / slices);
+    const uint32_t set = __builtin_amdgcn_readfirstlane(order[wave / slices]);
     const uint32_t slice = __builtin_amdgcn_readfirstlane(wave % slices);
     const SetCtx S = make_ctx(descs, set, code, consts, schema, parents, gseed);
     __shared__ uint2 pf_exp_lds[PF_EXP_LDS_U2];
