@@ -33,9 +33,9 @@ int g_num_cus = 256;
 // (1024 sets x 65,536 candidates, profiles/r01_wavesweep.md): with the longest-first set order
 // the full sweep peaks at 512 (finer slices even out the sets' unequal costs in the last round
 // of waves; 64 was 17 % slower); with early exit every concurrently running slice of a set
-// evaluates past its first witness, so fewer slices: 128.
+// evaluates past its first witness, so fewer slices: 96.
 uint32_t g_waves_per_cu_full = 512;
-uint32_t g_waves_per_cu_early = 128;
+uint32_t g_waves_per_cu_early = 96;
 
 int fail(const char* fmt, ...) {
     char buf[512];
