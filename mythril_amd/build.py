@@ -9,7 +9,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libpathfeas.so")
-SOURCES = ["pathfeas.hip", "pf_eval.hip", "pf_keccak.hip", "u256.h",
+SOURCES = ["pathfeas.hip", "pf_eval.hip", "pf_keccak.hip", "u256.h", "u256_cols.h",
            os.path.join("..", "..", "include", "pathfeas.h"),
            os.path.join("..", "..", "include", "pf_bytecode.h")]
 

@@ -123,7 +123,8 @@ int check_launch(Batch* B, uint64_t gseed, uint32_t budget, uint32_t flags, uint
     const uint32_t blocks = (uint32_t)((waves + 3) / 4);
     const uint64_t deadline = timeout_ms ? (uint64_t)timeout_ms * 100000ull : 0ull;  // 100 MHz
     HIPCHK(hipEventRecord(g_ev0, st));
-    hipLaunchKernelGGL(pf_check_kernel, dim3(blocks), dim3(256), 0, st, B->d_descs, B->d_order,
+    hipLaunchKernelGGL((flags & PF_FLAG_EARLY_EXIT) ? pf_check_early_kernel : pf_check_kernel,
+                       dim3(blocks), dim3(256), 0, st, B->d_descs, B->d_order,
                        (uint32_t)B->n_sets, B->d_code, B->d_consts, B->d_schema, B->d_parents,
                        gseed, budget, per_wave, slices, flags, deadline, d_t0, d_found, d_counters);
     HIPCHK(hipGetLastError());

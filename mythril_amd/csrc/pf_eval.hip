@@ -517,14 +517,17 @@ PF_INL SetCtx make_ctx(const pf_set_desc* __restrict__ descs, uint32_t set,
 
 // ---- search kernel: generate + evaluate + ballot early exit ---------------------------
 // grid: one wave per (set, slice); a slice is `per_wave` consecutive candidates.
-extern "C" __global__ void __launch_bounds__(256, PF_WG_PER_CU)
-pf_check_kernel(const pf_set_desc* __restrict__ descs, const uint32_t* __restrict__ order,
-                uint32_t n_sets,
-                const uint4* __restrict__ code, const uint32_t* __restrict__ consts,
-                const uint4* __restrict__ schema, const uint32_t* __restrict__ parents,
-                uint64_t gseed, uint32_t budget, uint32_t per_wave, uint32_t slices,
-                uint32_t flags, uint64_t deadline_ticks, uint64_t* __restrict__ t0_slot,
-                uint32_t* __restrict__ found, unsigned long long* __restrict__ counters) {
+// Two entry points over one body: the full sweep (pf_check_kernel) and the production
+// early-exit search (pf_check_early_kernel).  EARLY is a template constant so the full sweep
+// carries no found[] polling, and the two launches are separate rows in a rocprof trace.
+template <bool EARLY>
+PF_INL void check_body(const pf_set_desc* __restrict__ descs, const uint32_t* __restrict__ order,
+                       uint32_t n_sets,
+                       const uint4* __restrict__ code, const uint32_t* __restrict__ consts,
+                       const uint4* __restrict__ schema, const uint32_t* __restrict__ parents,
+                       uint64_t gseed, uint32_t budget, uint32_t per_wave, uint32_t slices,
+                       uint32_t flags, uint64_t deadline_ticks, uint64_t* __restrict__ t0_slot,
+                       uint32_t* __restrict__ found, unsigned long long* __restrict__ counters) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
     if (wave >= n_sets * slices) return;
@@ -550,7 +553,7 @@ pf_check_kernel(const pf_set_desc* __restrict__ descs, const uint32_t* __restric
     const uint32_t end = min(budget, begin + per_wave);
     uint64_t evals_full = 0, decided = 0, ops = 0;
     for (uint32_t base = begin; base < end; base += 64u) {
-        if (flags & PF_FLAG_EARLY_EXIT) {
+        if (EARLY) {
             uint32_t f = __hip_atomic_load(found + set, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (__builtin_amdgcn_readfirstlane(f) <= base) break;
         }
@@ -573,7 +576,7 @@ pf_check_kernel(const pf_set_desc* __restrict__ descs, const uint32_t* __restric
         if (m_sat) {
             uint32_t first = base + (uint32_t)__builtin_ctzll(m_sat);
             if (lane == 0) atomicMin(found + set, first);
-            if (flags & PF_FLAG_EARLY_EXIT) break;
+            if (EARLY) break;
         }
     }
     if (lane == 0) {
@@ -588,6 +591,24 @@ pf_check_kernel(const pf_set_desc* __restrict__ descs, const uint32_t* __restric
                   (unsigned long long)(__builtin_amdgcn_s_memtime() - t_wave));
 #endif
     }
+}
+
+#define PF_CHECK_PARAMS                                                                      \
+    const pf_set_desc *__restrict__ descs, const uint32_t *__restrict__ order, uint32_t n_sets, \
+        const uint4 *__restrict__ code, const uint32_t *__restrict__ consts,                   \
+        const uint4 *__restrict__ schema, const uint32_t *__restrict__ parents, uint64_t gseed, \
+        uint32_t budget, uint32_t per_wave, uint32_t slices, uint32_t flags,                   \
+        uint64_t deadline_ticks, uint64_t *__restrict__ t0_slot, uint32_t *__restrict__ found, \
+        unsigned long long *__restrict__ counters
+#define PF_CHECK_ARGS                                                                         \
+    descs, order, n_sets, code, consts, schema, parents, gseed, budget, per_wave, slices, flags, \
+        deadline_ticks, t0_slot, found, counters
+
+extern "C" __global__ void __launch_bounds__(256, PF_WG_PER_CU) pf_check_kernel(PF_CHECK_PARAMS) {
+    check_body<false>(PF_CHECK_ARGS);
+}
+extern "C" __global__ void __launch_bounds__(256, PF_WG_PER_CU) pf_check_early_kernel(PF_CHECK_PARAMS) {
+    check_body<true>(PF_CHECK_ARGS);
 }
 
 // ---- explicit-assignment evaluation (SoA [var][limb][cand]) --------------------------

@@ -116,13 +116,40 @@ _COST256 = {
 }
 
 
-def op_cost(op: int, width: int) -> int:
-    """Algorithmic int32 ops of one node (SURVEY.md §8(d) table), scaled by width."""
-    c = _COST256.get(op)
+# ---- reachable int32-op cost table (the roofline's `achieved`) -----------------------
+# The §8(d) table prices EXP as square-and-always-multiply (512 products) and division as
+# an 8-digit schoolbook quotient; the kernel's algorithms need far less, so that table's
+# "achieved" can exceed the VALU peak.  This table prices each node at the work of the
+# algorithm the kernel actually runs, so achieved <= peak:
+#   EXP      2-adic split: ~35 256-bit product equivalents (2-bit window over 8 exponent
+#            bits, 7 truncated squarings, ~25-term truncated Horner chain) x 72 = 2,520
+#   UDIV/UREM  Knuth algorithm D on 8 x 32-bit digits, worst case over divisor length n:
+#            (9 - n) quotient digits x (n mads + n subtracts + 4 estimate ops) + 2 x 16
+#            normalisation shifts, max at n = 4 -> 92, rounded to 96
+#   SDIV/SREM/SMOD  + three 8-limb negations = 120;  UMUL_NOOVF is one division = 96
+#   HASH     two Philox4x32-10 blocks = 20 rounds x 6 ops = 120
+_COST256_REACH = dict(_COST256)
+_COST256_REACH.update({
+    W_EXP: 35 * 72, W_UDIV: 96, W_UREM: 96, W_SDIV: 120, W_SREM: 120, W_SMOD: 120,
+    B_UMUL_NOOVF: 96, W_HASH: 120,
+})
+
+
+def _scaled(c: Optional[int], width: int) -> int:
     if c is None:
         return 0
     nl = (max(1, width) + 31) // 32
     return (c * nl + 7) // 8
+
+
+def op_cost(op: int, width: int) -> int:
+    """Algorithmic int32 ops of one node (SURVEY.md §8(d) table), scaled by width."""
+    return _scaled(_COST256.get(op), width)
+
+
+def reach_cost(op: int, width: int) -> int:
+    """Int32 ops of one node at the kernel's own algorithms (``_COST256_REACH``)."""
+    return _scaled(_COST256_REACH.get(op), width)
 
 
 def mask(w: int) -> int:
@@ -212,6 +239,9 @@ class Program:
     def node_cost(self) -> int:
         return sum(op_cost(i.op, i.width) for i in self.code)
 
+    def reach_cost(self) -> int:
+        return sum(reach_cost(i.op, i.width) for i in self.code)
+
     def validate(self) -> None:
         """Host-side shape check run before anything is launched (kernel assumes these)."""
         spilled = set()
@@ -284,8 +314,9 @@ class Batch:
             d_code = len(code)
             for ins in p.code:
                 w0, w1, a0, _ = ins.words()
-                # aux1 carries the node's algorithmic int32-op cost (PF_FLAG_COUNT_OPS)
-                code.append((w0, w1, a0, op_cost(ins.op, ins.width) if ins.op != END else 0))
+                # aux1 carries the node's int32-op cost at the kernel's algorithms
+                # (PF_FLAG_COUNT_OPS; reach_cost, so the roofline's achieved <= peak)
+                code.append((w0, w1, a0, reach_cost(ins.op, ins.width) if ins.op != END else 0))
             d_const = len(consts)
             for c in p.consts:
                 consts.append(to_limbs(c))

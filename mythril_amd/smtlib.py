@@ -100,6 +100,11 @@ _CMPS = {
     "bvsle": ("bvsle", False), "bvugt": ("bvult", True), "bvuge": ("bvule", True),
     "bvsgt": ("bvslt", True), "bvsge": ("bvsle", True), "bvumul_noovfl": ("bvumul_noovfl", False),
 }
+# overflow predicates of SMT-LIB 2.7 (newer z3 prints them): name -> (no-overflow form, negate)
+_OVFL = {
+    "bvuaddo": ("bvuadd_noovfl", True), "bvumulo": ("bvumul_noovfl", True),
+    "bvusubo": ("bvult", False),
+}
 
 
 class Reader:
@@ -152,63 +157,12 @@ class Reader:
             return self._indexed(head, [self.term(a, env) for a in e[1:]])
         args = [self.term(a, env) for a in e[1:]]
         h = _sym(head)
-        if h in _NARY:
-            acc = args[0]
-            for a in args[1:]:
-                acc = T.binop(_NARY[h], acc, a)
-            return acc
-        if h in _BIN:
-            return T.binop(_BIN[h], args[0], args[1])
-        if h == "bvneg":
-            return T.bvneg(args[0])
-        if h == "bvnot":
-            return T.bvnot(args[0])
-        if h in _CMPS:
-            op, swap = _CMPS[h]
-            a, b = (args[1], args[0]) if swap else (args[0], args[1])
-            return T.cmp(op, a, b)
-        if h == "bvnand":
-            return T.bvnot(T.binop("bvand", args[0], args[1]))
-        if h == "bvnor":
-            return T.bvnot(T.binop("bvor", args[0], args[1]))
-        if h == "bvxnor":
-            return T.bvnot(T.binop("bvxor", args[0], args[1]))
-        if h == "bvcomp":
-            return T.ite(T.eq(args[0], args[1]), T.const(1, 1), T.const(0, 1))
-        if h == "concat":
-            return T.concat(*args)
-        if h == "=":
-            if len(args) == 2:
-                return T.eq(args[0], args[1])
-            return T.and_(*[T.eq(args[i], args[i + 1]) for i in range(len(args) - 1)])
-        if h == "distinct":
-            return T.and_(*[T.not_(T.eq(args[i], args[j]))
-                            for i in range(len(args)) for j in range(i + 1, len(args))])
-        if h == "ite":
-            return T.ite(args[0], args[1], args[2])
-        if h == "and":
-            return T.and_(*args)
-        if h == "or":
-            return T.or_(*args)
-        if h == "not":
-            return T.not_(args[0])
-        if h == "xor":
-            acc = args[0]
-            for a in args[1:]:
-                acc = T.xor(acc, a)
-            return acc
-        if h == "=>":
-            return T.or_(T.not_(args[0]), args[1])
-        if h == "select":
-            return T.select(args[0], args[1])
-        if h == "store":
-            return T.store(args[0], args[1], args[2])
         if h in self.funs:
             doms, rng = self.funs[h]
             if rng[0] != "bv":
                 raise LoweringError(f"smtlib: UF {h} with range {rng}")
             return T.apply(h, rng[1], *args)
-        raise LoweringError(f"smtlib: unsupported operator {h}")
+        return apply_named(h, args)
 
     def _atom(self, tok: str, env) -> T.Term:
         s = _sym(tok)
@@ -238,33 +192,100 @@ class Reader:
 
     def _indexed(self, head: list, args: List[T.Term]) -> T.Term:
         if head[0] == "_":
-            op = head[1]
-            if op == "extract":
-                return T.extract(int(head[2]), int(head[3]), args[0])
-            if op == "zero_extend":
-                return T.zero_extend(int(head[2]), args[0])
-            if op == "sign_extend":
-                n = int(head[2])
-                a = args[0]
-                if n == 0:
-                    return a
-                msb = T.extract(a.width - 1, a.width - 1, a)
-                fill = T.ite(T.eq(msb, T.const(1, 1)), T.const(-1, n), T.const(0, n))
-                return T.concat(fill, a)
-            if op == "repeat":
-                return T.concat(*([args[0]] * int(head[2])))
-            if op in ("rotate_left", "rotate_right"):
-                a, k = args[0], int(head[2]) % args[0].width
-                if k == 0:
-                    return a
-                w = a.width
-                if op == "rotate_right":
-                    k = w - k
-                return T.concat(T.extract(w - 1 - k, 0, a), T.extract(w - 1, w - k, a))
+            return apply_indexed(head[1], [int(p) for p in head[2:]], args)
         if head[0] == "as" and head[1] == "const":
             srt = _sort(head[2])
             return T.const_array(srt[1], args[0])
         raise LoweringError(f"smtlib: unsupported indexed operator {head}")
+
+
+def apply_named(h: str, args: List[T.Term]) -> T.Term:
+    """An interpreted SMT-LIB2 / z3 operator applied to terms (shared by the text reader and
+    the z3-AST walker, mythril_amd/z3_terms.py)."""
+    if h in _NARY:
+        acc = args[0]
+        for a in args[1:]:
+            acc = T.binop(_NARY[h], acc, a)
+        return acc
+    if h in _BIN:
+        return T.binop(_BIN[h], args[0], args[1])
+    if h == "bvneg":
+        return T.bvneg(args[0])
+    if h == "bvnot":
+        return T.bvnot(args[0])
+    if h in _CMPS:
+        op, swap = _CMPS[h]
+        a, b = (args[1], args[0]) if swap else (args[0], args[1])
+        return T.cmp(op, a, b)
+    if h in _OVFL:
+        # SMT-LIB 2.7 overflow predicates (true iff the operation overflows)
+        op, neg = _OVFL[h]
+        r = T.cmp(op, args[0], args[1])
+        return T.not_(r) if neg else r
+    if h == "bvnand":
+        return T.bvnot(T.binop("bvand", args[0], args[1]))
+    if h == "bvnor":
+        return T.bvnot(T.binop("bvor", args[0], args[1]))
+    if h == "bvxnor":
+        return T.bvnot(T.binop("bvxor", args[0], args[1]))
+    if h == "bvcomp":
+        return T.ite(T.eq(args[0], args[1]), T.const(1, 1), T.const(0, 1))
+    if h == "concat":
+        return T.concat(*args)
+    if h == "=":
+        if len(args) == 2:
+            return T.eq(args[0], args[1])
+        return T.and_(*[T.eq(args[i], args[i + 1]) for i in range(len(args) - 1)])
+    if h == "distinct":
+        return T.and_(*[T.not_(T.eq(args[i], args[j]))
+                        for i in range(len(args)) for j in range(i + 1, len(args))])
+    if h in ("ite", "if"):
+        return T.ite(args[0], args[1], args[2])
+    if h == "and":
+        return T.and_(*args)
+    if h == "or":
+        return T.or_(*args)
+    if h == "not":
+        return T.not_(args[0])
+    if h == "xor":
+        acc = args[0]
+        for a in args[1:]:
+            acc = T.xor(acc, a)
+        return acc
+    if h == "=>":
+        return T.or_(T.not_(args[0]), args[1])
+    if h == "select":
+        return T.select(args[0], args[1])
+    if h == "store":
+        return T.store(args[0], args[1], args[2])
+    raise LoweringError(f"smtlib: unsupported operator {h}")
+
+
+def apply_indexed(op: str, params: List[int], args: List[T.Term]) -> T.Term:
+    """``((_ op p...) args)`` — extract / zero_extend / sign_extend / repeat / rotations."""
+    if op == "extract":
+        return T.extract(params[0], params[1], args[0])
+    if op == "zero_extend":
+        return T.zero_extend(params[0], args[0])
+    if op == "sign_extend":
+        n = params[0]
+        a = args[0]
+        if n == 0:
+            return a
+        msb = T.extract(a.width - 1, a.width - 1, a)
+        fill = T.ite(T.eq(msb, T.const(1, 1)), T.const(-1, n), T.const(0, n))
+        return T.concat(fill, a)
+    if op == "repeat":
+        return T.concat(*([args[0]] * params[0]))
+    if op in ("rotate_left", "rotate_right"):
+        a, k = args[0], params[0] % args[0].width
+        if k == 0:
+            return a
+        w = a.width
+        if op == "rotate_right":
+            k = w - k
+        return T.concat(T.extract(w - 1 - k, 0, a), T.extract(w - 1, w - k, a))
+    raise LoweringError(f"smtlib: unsupported indexed operator {op}")
 
 
 def read_query(text: str) -> Query:
