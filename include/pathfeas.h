@@ -39,7 +39,8 @@ typedef struct pf_stats {
     uint64_t ops;            /* algorithmic int32 ops executed (PF_FLAG_COUNT_OPS only)      */
     uint64_t n_sat;          /* sets with a witness                                          */
     float kernel_ms;         /* device time of the check kernel (HIP events, its stream)     */
-    float pad_;
+    uint32_t timed_out;      /* 1 if the timeout_ms deadline cut any wave's search: the
+                                NOT_FOUND verdicts are then incomplete                      */
 } pf_stats;
 
 /* ---- lifetime ---------------------------------------------------------------------- */

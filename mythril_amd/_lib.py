@@ -30,7 +30,7 @@ class pf_stats(ctypes.Structure):
         ("ops", ctypes.c_uint64),
         ("n_sat", ctypes.c_uint64),
         ("kernel_ms", ctypes.c_float),
-        ("pad_", ctypes.c_float),
+        ("timed_out", ctypes.c_uint32),
     ]
 
 

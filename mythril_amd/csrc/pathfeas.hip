@@ -66,7 +66,34 @@ struct Batch {
     uint32_t* d_parents = nullptr;
     uint32_t* d_found = nullptr;
     uint32_t* d_order = nullptr;  // set ids, most expensive first (search-kernel wave order)
+    ~Batch() {  // also the error path of pf_batch_create: frees whatever was allocated
+        hipFree(d_code);
+        hipFree(d_consts);
+        hipFree(d_schema);
+        hipFree(d_parents);
+        hipFree(d_descs);
+        hipFree(d_found);
+        hipFree(d_order);
+    }
 };
+
+// Temporary device buffer freed on every return path (HIPCHK returns early).
+struct DevBuf {
+    void* p = nullptr;
+    ~DevBuf() { hipFree(p); }
+    template <typename T>
+    T* as() { return static_cast<T*>(p); }
+};
+
+// The library's scratch counters and events are shared by every launch.  A launch on a
+// caller's stream (the *_dev entry points) returns without waiting, so before the next
+// launch on a different stream reuses them, that stream is drained.
+hipStream_t g_last_stream = nullptr;
+int switch_stream(hipStream_t st) {
+    if (g_last_stream && g_last_stream != st) HIPCHK(hipStreamSynchronize(g_last_stream));
+    g_last_stream = st;
+    return 0;
+}
 
 int ensure_init_locked() {
     if (g_device < 0) return fail("pf_init() has not been called");
@@ -104,6 +131,7 @@ void geometry(uint32_t n_sets, uint32_t budget, uint32_t flags, uint32_t* per_wa
 
 int check_launch(Batch* B, uint64_t gseed, uint32_t budget, uint32_t flags, uint32_t timeout_ms,
                  uint32_t* d_found, pf_stats* stats, hipStream_t st) {
+    if (switch_stream(st)) return -1;
     unsigned long long* d_counters = reinterpret_cast<unsigned long long*>(g_scratch_u32);
     uint64_t* d_t0 = reinterpret_cast<uint64_t*>(g_scratch_u32 + 8);
 #ifdef PF_PROFILE_UNITS
@@ -130,7 +158,7 @@ int check_launch(Batch* B, uint64_t gseed, uint32_t budget, uint32_t flags, uint
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(g_ev1, st));
     if (stats) {
-        unsigned long long h[3];
+        unsigned long long h[4];
         HIPCHK(hipMemcpyAsync(h, d_counters, sizeof(h), hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         float ms = 0.f;
@@ -140,6 +168,7 @@ int check_launch(Batch* B, uint64_t gseed, uint32_t budget, uint32_t flags, uint
         stats->ops = h[2];
         stats->kernel_ms = ms;
         stats->n_sat = 0;
+        stats->timed_out = h[3] ? 1u : 0u;
     }
     return 0;
 }
@@ -209,6 +238,7 @@ int pf_shutdown(void) {
     hipStreamDestroy(g_stream);
     g_scratch_u32 = nullptr;
     g_stream = nullptr;
+    g_last_stream = nullptr;
     g_device = -1;
     return 0;
 }
@@ -337,14 +367,9 @@ int pf_batch_free(uint64_t handle) {
     Batch* B = as_batch(handle);
     if (!B) return 0;
     hipSetDevice(B->device);
-    hipStreamSynchronize(g_stream);
-    hipFree(B->d_code);
-    hipFree(B->d_consts);
-    hipFree(B->d_schema);
-    hipFree(B->d_parents);
-    hipFree(B->d_descs);
-    hipFree(B->d_found);
-    hipFree(B->d_order);
+    // a *_dev launch may still be reading the batch on a caller's stream: drain the device
+    hipDeviceSynchronize();
+    g_last_stream = nullptr;
     delete B;
     return 0;
 }
@@ -401,11 +426,14 @@ int pf_materialize(uint64_t handle, uint64_t global_seed, const uint32_t* set_id
         total += B->h_descs[set_ids[i]].n_vars;
     }
     if (total == 0) return 0;
-    uint32_t *d_sets, *d_cands, *d_off, *d_out;
-    HIPCHK(hipMalloc(&d_sets, n * 4));
-    HIPCHK(hipMalloc(&d_cands, n * 4));
-    HIPCHK(hipMalloc(&d_off, n * 4));
-    HIPCHK(hipMalloc(&d_out, total * 32));
+    if (switch_stream(g_stream)) return -1;
+    DevBuf b_sets, b_cands, b_off, b_out;
+    HIPCHK(hipMalloc(&b_sets.p, n * 4));
+    HIPCHK(hipMalloc(&b_cands.p, n * 4));
+    HIPCHK(hipMalloc(&b_off.p, n * 4));
+    HIPCHK(hipMalloc(&b_out.p, total * 32));
+    uint32_t *d_sets = b_sets.as<uint32_t>(), *d_cands = b_cands.as<uint32_t>(),
+             *d_off = b_off.as<uint32_t>(), *d_out = b_out.as<uint32_t>();
     HIPCHK(hipMemcpyAsync(d_sets, set_ids, n * 4, hipMemcpyHostToDevice, g_stream));
     HIPCHK(hipMemcpyAsync(d_cands, cand_ids, n * 4, hipMemcpyHostToDevice, g_stream));
     HIPCHK(hipMemcpyAsync(d_off, off.data(), n * 4, hipMemcpyHostToDevice, g_stream));
@@ -417,10 +445,6 @@ int pf_materialize(uint64_t handle, uint64_t global_seed, const uint32_t* set_id
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(values_out, d_out, total * 32, hipMemcpyDeviceToHost, g_stream));
     HIPCHK(hipStreamSynchronize(g_stream));
-    hipFree(d_sets);
-    hipFree(d_cands);
-    hipFree(d_off);
-    hipFree(d_out);
     return 0;
 }
 
@@ -444,16 +468,16 @@ int pf_eval_assignments(uint64_t handle, uint32_t set, const uint32_t* soa, uint
     if (n_cand == 0) return 0;
     const size_t nv = std::max<uint32_t>(B->h_descs[set].n_vars, 1u);
     const size_t bytes = nv * 8 * (size_t)n_cand * 4;
-    uint32_t* d_soa;
-    uint8_t* d_out;
-    HIPCHK(hipMalloc(&d_soa, bytes));
-    HIPCHK(hipMalloc(&d_out, n_cand));
+    if (switch_stream(g_stream)) return -1;
+    DevBuf b_soa, b_out;
+    HIPCHK(hipMalloc(&b_soa.p, bytes));
+    HIPCHK(hipMalloc(&b_out.p, n_cand));
+    uint32_t* d_soa = b_soa.as<uint32_t>();
+    uint8_t* d_out = b_out.as<uint8_t>();
     HIPCHK(hipMemcpyAsync(d_soa, soa, bytes, hipMemcpyHostToDevice, g_stream));
     if (eval_launch(B, set, d_soa, n_cand, d_out, g_stream)) return -1;
     HIPCHK(hipMemcpyAsync(sat_out, d_out, n_cand, hipMemcpyDeviceToHost, g_stream));
     HIPCHK(hipStreamSynchronize(g_stream));
-    hipFree(d_soa);
-    hipFree(d_out);
     return 0;
 }
 
@@ -463,6 +487,7 @@ int pf_eval_assignments_dev(uint64_t handle, uint32_t set, const uint32_t* d_soa
     if (ensure_init_locked()) return -1;
     Batch* B = as_batch(handle);
     if (!B) return fail("pf_eval_assignments_dev: null batch");
+    if (switch_stream(pick_stream(stream))) return -1;
     return eval_launch(B, set, d_soa, n_cand, d_sat_out, pick_stream(stream));
 }
 
@@ -473,11 +498,13 @@ int pf_keccak256_batch(const uint8_t* data, const uint64_t* offsets, size_t n, u
     for (size_t i = 0; i < n; i++)
         if (offsets[i + 1] < offsets[i]) return fail("keccak: offsets not monotone at %zu", i);
     const uint64_t total = offsets[n];
-    uint8_t *d_data, *d_out;
-    uint64_t* d_off;
-    HIPCHK(hipMalloc(&d_data, total ? total : 8));
-    HIPCHK(hipMalloc(&d_off, (n + 1) * 8));
-    HIPCHK(hipMalloc(&d_out, n * 32));
+    if (switch_stream(g_stream)) return -1;
+    DevBuf b_data, b_off, b_out;
+    HIPCHK(hipMalloc(&b_data.p, total ? total : 8));
+    HIPCHK(hipMalloc(&b_off.p, (n + 1) * 8));
+    HIPCHK(hipMalloc(&b_out.p, n * 32));
+    uint8_t *d_data = b_data.as<uint8_t>(), *d_out = b_out.as<uint8_t>();
+    uint64_t* d_off = b_off.as<uint64_t>();
     if (total) HIPCHK(hipMemcpyAsync(d_data, data, total, hipMemcpyHostToDevice, g_stream));
     HIPCHK(hipMemcpyAsync(d_off, offsets, (n + 1) * 8, hipMemcpyHostToDevice, g_stream));
     hipLaunchKernelGGL(pf_keccak_var_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, g_stream,
@@ -485,9 +512,6 @@ int pf_keccak256_batch(const uint8_t* data, const uint64_t* offsets, size_t n, u
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(out32, d_out, n * 32, hipMemcpyDeviceToHost, g_stream));
     HIPCHK(hipStreamSynchronize(g_stream));
-    hipFree(d_data);
-    hipFree(d_off);
-    hipFree(d_out);
     return 0;
 }
 
@@ -497,6 +521,7 @@ int pf_keccak256_fixed_dev(const uint8_t* d_data, uint32_t len, size_t n, uint8_
     if (ensure_init_locked()) return -1;
     if (n == 0) return 0;
     hipStream_t st = pick_stream(stream);
+    if (switch_stream(st)) return -1;
     HIPCHK(hipEventRecord(g_ev0, st));
     const bool fast = (len % 16u) == 0u && len < 136u && (((uintptr_t)d_data) & 15u) == 0u;
     if (fast)

@@ -552,6 +552,7 @@ PF_INL void check_body(const pf_set_desc* __restrict__ descs, const uint32_t* __
     const uint32_t begin = slice * per_wave;
     const uint32_t end = min(budget, begin + per_wave);
     uint64_t evals_full = 0, decided = 0, ops = 0;
+    uint32_t cut = 0u;
     for (uint32_t base = begin; base < end; base += 64u) {
         if (EARLY) {
             uint32_t f = __hip_atomic_load(found + set, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -559,7 +560,10 @@ PF_INL void check_body(const pf_set_desc* __restrict__ descs, const uint32_t* __
         }
         if (deadline_ticks) {
             uint64_t now = __builtin_amdgcn_s_memrealtime();
-            if (now - t0 > deadline_ticks) break;
+            if (now - t0 > deadline_ticks) {
+                cut = 1u;  // this wave's slice is not fully searched: no complete verdict
+                break;
+            }
         }
         const uint32_t cand = base + lane;
         const bool active = cand < end;
@@ -583,6 +587,7 @@ PF_INL void check_body(const pf_set_desc* __restrict__ descs, const uint32_t* __
         atomicAdd(counters + 0, (unsigned long long)evals_full);
         atomicAdd(counters + 1, (unsigned long long)decided);
         if (flags & PF_FLAG_COUNT_OPS) atomicAdd(counters + 2, (unsigned long long)ops);
+        if (cut) atomicAdd(counters + 3, 1ull);
 #ifdef PF_PROFILE_UNITS
 #pragma unroll
         for (int i = 0; i < PF_PROF_BUCKETS; i++)

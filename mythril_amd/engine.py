@@ -31,6 +31,7 @@ class CheckResult:
     cands_decided: int
     ops: int
     kernel_ms: float
+    timed_out: bool = False   # the device deadline cut the search: NOT_FOUND is incomplete
 
     @property
     def sat(self) -> np.ndarray:
@@ -93,7 +94,8 @@ class Engine:
         _lib.check(_lib.lib().pf_check_batch(db.handle, seed, budget, flags, timeout_ms,
                                             _lib.ptr_u32(found), None, ctypes.byref(st)),
                    "pf_check_batch")
-        return CheckResult(found[:n], st.evals_full, st.cands_decided, st.ops, st.kernel_ms)
+        return CheckResult(found[:n], st.evals_full, st.cands_decided, st.ops, st.kernel_ms,
+                           bool(st.timed_out))
 
     def materialize(self, db: DeviceBatch, set_ids: Sequence[int], cand_ids: Sequence[int],
                     seed: int = 0) -> List[List[int]]:

@@ -1,15 +1,20 @@
 """Wiring into a real Mythril (z3-bearing) process: the drop-in ``Optimize`` and the LASER plugin.
 
-Nothing here runs in this build container (Mythril's dependencies — z3, eth_abi, eth_hash —
-are not installed); it is the code path INTEGRATION.md describes, kept import-safe.
+Mythril's own dependencies (z3, eth_abi, eth_hash) are not installed in the build image, so
+the CPU tests drive this module against faithful stand-ins of z3 (tests/fake_z3.py) and of the
+Mythril interfaces it touches (tests/mythril_standin.py); the GPU tests run the same code
+against the real engine.
 
 Seams:
 * ``mythril.support.model.Optimize`` is the one name the query funnel resolves at call time
   (support/model.py:13, :37) — ``install()`` rebinds it to :func:`gpu_optimize_class`'s class.
-  Its ``check()`` sends objective-free queries to the GPU (z3 assertions are read through
-  ``z3.Optimize.sexpr()`` with :mod:`mythril_amd.smtlib`), returns ``z3.sat`` with a model
-  whose ``eval`` answers z3 expressions from the GPU witness, and otherwise delegates to the
-  original z3 ``check()`` unchanged (objectives, no witness, unsupported shapes).
+  Its ``check()`` sends objective-free queries to the GPU: the z3 assertions are converted by
+  the AST-id-cached walker (mythril_amd/z3_terms.py), the search runs under the solver's own
+  timeout as a device deadline (``set_timeout``, support/model.py:38), and a witness returns
+  ``z3.sat`` with a model whose ``eval`` answers any z3 expression (also ones over symbols
+  outside the query, completed as z3's ``model_completion`` would).  Everything else
+  (objectives, no witness, unsupported shapes, engine errors) goes to the original z3
+  ``check()`` unchanged.
 * ``MythrilAmdPluginBuilder`` — a ``MythrilLaserPlugin`` (mythril/plugin/interface.py:40-46,
   ``plugin_default_enabled = True`` read at discovery.py:71) whose LASER plugin batches every
   open state's constraints at ``stop_sym_trans`` (svm.py:307-308) — right before the
@@ -20,19 +25,23 @@ Seams:
 from __future__ import annotations
 
 import logging
-from typing import Dict, List, Optional
+import threading
+from dataclasses import replace
+from typing import Dict, List, Optional, Tuple
 
 from .smt import terms as T
 from .smt.to_dag import DEFAULT_REGISTRY, KeccakSpec, UFRegistry
-from .smtlib import Reader, read_query
 
 log = logging.getLogger(__name__)
 
 PART = (2 ** 256 - 1) // 10 ** 40
 
-# precomputed verdicts of the tx-boundary batch: key = tuple of z3 AST ids of a state's
-# constraints (+ keccak conditions) -> internal witness model
-_BATCH_CACHE: Dict[tuple, object] = {}
+# Witnesses of the latest tx-boundary batch: key = the state's query as a tuple of
+# hash-consed terms (structural: a key can only match the same constraints, whatever z3 does
+# with AST ids) -> WitnessModel.  Cleared at every batch; a hit is re-checked against the
+# query before it is returned.
+_BATCH_CACHE: Dict[Tuple[T.Term, ...], object] = {}
+_BATCH_LOCK = threading.Lock()
 
 
 def sync_keccak_registry(kfm, registry: UFRegistry = DEFAULT_REGISTRY) -> None:
@@ -46,55 +55,118 @@ def sync_keccak_registry(kfm, registry: UFRegistry = DEFAULT_REGISTRY) -> None:
         spec.concrete[data.value] = digest.value
 
 
-class _Z3View:
-    """Adapter: evaluates z3 expressions under a GPU witness (Model-compatible)."""
+def _z3_sort_decl(z3, d):
+    """A z3 FuncDeclRef for one of the witness's declarations (mythril_amd.smt.model.Decl)."""
+    name, sort = d.name(), d.sort
+    if sort == T.BOOL:
+        return z3.Bool(name).decl()
+    if sort[0] == "bv":
+        return z3.BitVec(name, sort[1]).decl()
+    if sort[0] == "array":
+        return z3.Array(name, z3.BitVecSort(sort[1]), z3.BitVecSort(sort[2])).decl()
+    # ("fn", dom..., rng)
+    doms, rng = sort[1:-1], sort[-1]
+    return z3.Function(name, *[z3.BitVecSort(w) for w in doms], z3.BitVecSort(rng))
 
-    def __init__(self, internal, reader: Reader, z3mod):
-        self.internal = internal
-        self.reader = reader
-        self.z3 = z3mod
+
+class Z3WitnessView:
+    """A GPU witness seen as one internal model of ``mythril.laser.smt.Model``
+    (mythril/laser/smt/model.py:6-59): ``decls()``, ``__getitem__`` and ``eval`` over z3
+    expressions.
+
+    Immutable by design: the funnel stores the model in ``ModelCache`` (support/model.py:120)
+    and every later quick-sat check deep-copies it (support_utils.py:62-68), so a copy is
+    the object itself.  No module or reader object is held (z3 is imported where needed).
+    ``eval`` converts the expression with the process-wide AST converter and evaluates it
+    under the witness; symbols the witness does not assign evaluate to z3's
+    ``model_completion`` defaults (0 / false / arrays 0 everywhere), and UF applications
+    outside the query take the engine's interpretation of that UF.  With
+    ``model_completion=False`` the completed value is returned as well (z3 would hand back
+    the symbol itself for an unassigned one).
+    """
+
+    def __init__(self, internal):
+        self.internal = internal   # mythril_amd.smt.model.WitnessModel
+        self._decls = None
+
+    def __deepcopy__(self, memo):
+        return self
+
+    def __copy__(self):
+        return self
+
+    def __reduce__(self):
+        return (Z3WitnessView, (self.internal,))
 
     def decls(self):
-        return []
+        if self._decls is None:
+            import z3
+
+            self._decls = [_z3_sort_decl(z3, d) for d in self.internal.decls()]
+        return self._decls
 
     def __getitem__(self, item):
+        import z3
+
+        if isinstance(item, int):
+            return self.decls()[item]
         name = item.name()
         w = self.internal.w
         if name in w.vars:
-            return self.z3.BitVecVal(w.vars[name], item.range().size())
+            return z3.BitVecVal(w.vars[name], item.range().size())
         if name in w.bools:
-            return self.z3.BoolVal(w.bools[name])
+            return z3.BoolVal(w.bools[name])
         return None
 
     def eval(self, expression, model_completion: bool = False):
-        term = self.reader.term(_parse_one(expression.sexpr()), {})
+        import z3
+
+        from .z3_terms import converter
+
+        term = converter(z3).term(expression)
         v = self.internal.w.ev(term)
         if term.is_bool:
-            return self.z3.BoolVal(bool(v))
-        return self.z3.BitVecVal(int(v), term.width)
+            return z3.BoolVal(bool(v))
+        return z3.BitVecVal(int(v), term.width)
 
 
-def _parse_one(text: str):
-    from .smtlib import parse_sexprs
-
-    return parse_sexprs(text)[0]
+def _query_key(terms: List[T.Term]) -> Tuple[T.Term, ...]:
+    return tuple(t for t in terms if t is not T.TRUE)
 
 
-def gpu_optimize_class():  # pragma: no cover - needs Mythril + z3
-    """Build the drop-in subclass of mythril.laser.smt.Optimize."""
+def _lookup_batch(terms: List[T.Term]):
+    """A parked tx-boundary witness for exactly this query, re-checked before use."""
+    key = _query_key(terms)
+    with _BATCH_LOCK:
+        m = _BATCH_CACHE.get(key)
+    if m is None:
+        return None
+    if all(m.w.ev(c) for c in key):
+        return m
+    return None
+
+
+def gpu_optimize_class():
+    """Build the drop-in subclass of ``mythril.laser.smt.Optimize`` (needs Mythril + z3)."""
     import z3
+    from mythril.laser.ethereum.function_managers import keccak_function_manager
     from mythril.laser.smt import Optimize as MythrilOptimize
     from mythril.laser.smt.model import Model
-    from mythril.laser.ethereum.function_managers import keccak_function_manager
 
-    from .smt.gpu_check import check_sets
+    from .smt import gpu_check
     from .smt.solver import SolverStatistics
+    from .z3_terms import converter
 
     class GpuOptimize(MythrilOptimize):
         def __init__(self):
             super().__init__()
             self._objectives = False
             self._gpu_model = None
+            self._timeout_ms: Optional[int] = None
+
+        def set_timeout(self, timeout: int) -> None:
+            self._timeout_ms = timeout
+            super().set_timeout(timeout)
 
         def minimize(self, element):
             self._objectives = True
@@ -105,22 +177,24 @@ def gpu_optimize_class():  # pragma: no cover - needs Mythril + z3
             super().maximize(element)
 
         def check(self, *args):
-            if not self._objectives and not args:
+            self._gpu_model = None
+            if not self._objectives and not args and gpu_check.CONFIG.enabled:
                 stats = SolverStatistics()
                 stats.gpu_attempts += 1
                 try:
-                    reader = Reader()
-                    q = reader.read(self.raw.sexpr())
-                    key = tuple(sorted(a.get_id() for a in self.raw.assertions()))
-                    internal = _BATCH_CACHE.pop(key, None)
+                    terms = converter(z3).terms(self.raw.assertions())
+                    internal = _lookup_batch(terms)
                     if internal is None:
                         sync_keccak_registry(keccak_function_manager)
-                        internal = check_sets([q.assertions])[0]
+                        cfg = gpu_check.CONFIG
+                        if self._timeout_ms:
+                            cfg = replace(cfg, timeout_ms=int(self._timeout_ms))
+                        internal = gpu_check.check_sets([terms], config=cfg)[0]
                     if internal is not None:
                         stats.gpu_sat += 1
-                        self._gpu_model = Model([_Z3View(internal, reader, z3)])
+                        self._gpu_model = Model([Z3WitnessView(internal)])
                         return z3.sat
-                except Exception as e:
+                except Exception as e:  # the GPU never decides a query it cannot answer
                     log.info("GPU path skipped: %s", e)
             return super().check(*args)
 
@@ -132,60 +206,54 @@ def gpu_optimize_class():  # pragma: no cover - needs Mythril + z3
     return GpuOptimize
 
 
-def install() -> None:  # pragma: no cover - needs Mythril
+def install() -> None:
     """Rebind the funnel's Optimize (support/model.py:13 binds it by value at import)."""
     import mythril.support.model as funnel
 
     funnel.Optimize = gpu_optimize_class()
 
 
-def _z3_terms(raws):  # pragma: no cover - needs z3
-    """z3 ASTs -> (terms, cache key): through the assertions' SMT-LIB2 text (what
-    ``z3.Optimize.sexpr()`` prints, support/model.py:46-57) and mythril_amd.smtlib."""
-    import z3
-
-    s = z3.Optimize()
-    s.add(raws)
-    return read_query(s.sexpr()).assertions, tuple(sorted(r.get_id() for r in raws))
-
-
-def state_terms(state):
-    """One open state's query, as the funnel would pose it: ``get_all_constraints()``
-    (constraints.py:132-133 — path constraints + the keccak manager's conditions), python
-    bools dropped (support/model.py:87-93).  Constraints that already are mythril_amd.smt
-    terms (the drop-in facade) are used as they are; z3 ones go through SMT-LIB2."""
-    cs = [c for c in state.world_state.constraints.get_all_constraints() if not isinstance(c, bool)]
+def state_terms(state) -> List[T.Term]:
+    """One open state's query, as the funnel would pose it: the ``WorldState``'s
+    ``constraints.get_all_constraints()`` (world_state.py:39; constraints.py:132-133 — path
+    constraints + the keccak manager's conditions), python bools dropped
+    (support/model.py:87-93).  Facade constraints (mythril_amd.smt terms) are used as they
+    are; z3 ones go through the AST converter."""
+    cs = [c for c in state.constraints.get_all_constraints() if not isinstance(c, bool)]
     raws = [c.raw for c in cs]
     if all(isinstance(r, T.Term) for r in raws):
-        return raws, tuple(id(r) for r in raws)
-    return _z3_terms(raws)
+        return raws
+    import z3
+
+    from .z3_terms import converter
+
+    return converter(z3).terms(raws)
 
 
 def batch_open_states(open_states, kfm=None, registry: UFRegistry = DEFAULT_REGISTRY) -> int:
-    """Tx-boundary batch (svm.py:266-286): one GPU launch over every open state's
-    constraint set; each witness is parked in ``_BATCH_CACHE`` under the state's key so the
-    ``is_possible()`` pass that follows is answered without z3.  Returns the number of
+    """Tx-boundary batch (svm.py:266-286): one GPU launch over every open ``WorldState``'s
+    constraint set (svm.py:85,380: ``open_states`` holds WorldStates); each witness is
+    parked under the state's query so the ``is_possible()`` pass that follows is answered
+    without z3.  The previous batch's witnesses are dropped first.  Returns the number of
     states with a witness."""
     from .smt.gpu_check import check_sets
 
     if kfm is None:  # pragma: no cover - needs Mythril
         from mythril.laser.ethereum.function_managers import keccak_function_manager as kfm
     sync_keccak_registry(kfm, registry)
-    sets, keys = [], []
-    for st in open_states:
-        terms, key = state_terms(st)
-        sets.append(terms)
-        keys.append(key)
+    sets = [state_terms(st) for st in open_states]
     models = check_sets(sets, registry=registry) if sets else []
     n = 0
-    for k, m in zip(keys, models):
-        if m is not None:
-            _BATCH_CACHE[k] = m
-            n += 1
+    with _BATCH_LOCK:
+        _BATCH_CACHE.clear()
+        for terms, m in zip(sets, models):
+            if m is not None:
+                _BATCH_CACHE[_query_key(terms)] = m
+                n += 1
     return n
 
 
-def _plugin_classes():  # pragma: no cover - needs Mythril
+def _plugin_classes():
     from mythril.laser.plugin.builder import PluginBuilder
     from mythril.laser.plugin.interface import LaserPlugin
     from mythril.plugin.interface import MythrilLaserPlugin

@@ -194,7 +194,7 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
                 found[key] = cached
                 hits += 1
                 continue
-            if cfg.timeout_ms == 0 and _neg_key(key, cfg) in _NEG:
+            if _neg_key(key, cfg) in _NEG:  # a complete search found nothing: same answer
                 found[key] = None
                 hits += 1
                 continue
@@ -229,7 +229,7 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
         db.free()
         for k in range(len(progs)):
             found[keys[k]] = None
-        if cfg.timeout_ms == 0:  # a deadline-cut search is not a complete answer
+        if not res.timed_out:  # a deadline-cut search is not a complete answer
             sat_set = set(sat)
             with _lock:
                 for k in range(len(progs)):

@@ -187,3 +187,27 @@ def test_optimize_with_objectives_is_not_discharged(engine):
     o.add(ULT(x, BVV(10, 256)))
     o.minimize(x)
     assert o.check() in (unknown, sat)  # objectives always go to z3 (absent here -> unknown)
+
+
+def test_device_deadline_cuts_a_long_search(engine):
+    """Solver timeout as a device deadline (SURVEY §8b threading: the engine bounds its own
+    runtime by the passed timeout): a long witness-free search with a 2 ms deadline returns
+    within a few ms and reports the cut, so its NOT_FOUND verdicts are not cached; the same
+    search without a deadline reports no cut.  Any witness a cut search did report is real."""
+    import numpy as np
+
+    import pyoracle as O
+    from mythril_amd import ir, synth
+
+    progs = [synth.random_dag_set(9000 + i, plant=False)[0] for i in range(256)]
+    db = engine.upload(progs)
+    r = engine.check(db, budget=1 << 22, seed=0, flags=ir.FLAG_SHORTCIRCUIT, timeout_ms=2)
+    assert r.timed_out
+    assert r.kernel_ms < 100.0, r.kernel_ms
+    b = ir.Batch(progs)
+    for s in np.nonzero(r.found != 0xFFFFFFFF)[0][:8]:
+        vals = O.SetView.from_batch(b, int(s)).gen_assignments(np.array([r.found[s]], dtype=np.uint64), 0)[0]
+        assert O.SetView.from_batch(b, int(s)).evaluate(vals)
+    r2 = engine.check(db, budget=4096, seed=0, flags=ir.FLAG_SHORTCIRCUIT, timeout_ms=60000)
+    assert not r2.timed_out
+    db.free()

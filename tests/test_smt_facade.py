@@ -166,9 +166,10 @@ def test_check_sets_caches_witnessless_buckets(monkeypatch):
     uploads = []
 
     class _Res:
-        def __init__(self, n):
+        def __init__(self, n, cut):
             self.found = np.full(n, 0xFFFFFFFF, dtype=np.uint32)
             self.kernel_ms, self.cands_decided = 0.0, 0
+            self.timed_out = cut
 
     class _DB:
         def __init__(self, n):
@@ -178,14 +179,17 @@ def test_check_sets_caches_witnessless_buckets(monkeypatch):
             pass
 
     class _Eng:
+        cut = False
+
         def upload(self, progs):
             uploads.append(len(progs))
             return _DB(len(progs))
 
-        def check(self, db, **kw):
-            return _Res(db.n)
+        def check(self, db, timeout_ms=0, **kw):
+            return _Res(db.n, bool(timeout_ms) and self.cut)
 
-    monkeypatch.setattr(E, "get_engine", lambda *a, **k: _Eng())
+    eng = _Eng()
+    monkeypatch.setattr(E, "get_engine", lambda *a, **k: eng)
     gpu_check.reset_cache()
     x, y = symbol_factory.BitVecSym("x", 256), symbol_factory.BitVecSym("y", 256)
     sets = [[(x == symbol_factory.BitVecVal(5, 256)).raw, ULT(y, symbol_factory.BitVecVal(3, 256)).raw]]
@@ -195,8 +199,16 @@ def test_check_sets_caches_witnessless_buckets(monkeypatch):
     assert uploads == [2]                      # both answered from the negative cache
     cfg = gpu_check.GpuConfig(timeout_ms=5)
     gpu_check.check_sets(sets, config=cfg)
+    assert uploads == [2]                      # a complete negative holds under a deadline too
+    gpu_check.reset_cache()
+    eng.cut = True                             # the device deadline cuts every search
     gpu_check.check_sets(sets, config=cfg)
-    assert uploads == [2, 2, 2]                # deadline searches are never cached
+    gpu_check.check_sets(sets, config=cfg)
+    assert uploads == [2, 2, 2]                # deadline-cut searches are never cached
+    eng.cut = False
+    gpu_check.check_sets(sets, config=cfg)
+    gpu_check.check_sets(sets, config=cfg)
+    assert uploads == [2, 2, 2, 2]             # a deadline search that completed is cached
     gpu_check.reset_cache()
 
 
@@ -213,6 +225,7 @@ def test_parallel_lowering_matches_sequential(monkeypatch):
         def __init__(self, n):
             self.found = np.full(n, 0xFFFFFFFF, dtype=np.uint32)
             self.kernel_ms, self.cands_decided = 0.0, 0
+            self.timed_out = False
 
     class _DB:
         def __init__(self, n):
