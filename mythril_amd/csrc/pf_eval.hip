@@ -539,8 +539,11 @@ PF_INL void check_body(const pf_set_desc* __restrict__ descs, const uint32_t* __
 
     uint64_t t0 = 0;
     if (deadline_ticks) {
+        // the first wave stamps the launch's start; later waves only read it (a CAS from
+        // every one of ~10^5 waves on one address serialises in L2: ~100 ms per launch)
         uint64_t now = __builtin_amdgcn_s_memrealtime();
-        unsigned long long prev = atomicCAS((unsigned long long*)t0_slot, 0ull, (unsigned long long)now);
+        uint64_t prev = __hip_atomic_load(t0_slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == 0) prev = atomicCAS((unsigned long long*)t0_slot, 0ull, (unsigned long long)now);
         t0 = prev ? prev : now;
     }
     UnitProf prof;

@@ -16,7 +16,8 @@ Dependence keys follow the GPU's interpretation of arrays and UFs
   arguments — except when the set also applies the inverse ``keccak256_<n>-1`` to a value
   that is not itself an application: that lookup ranges over every application of width
   n, so then all of them share one family key.
-Other UFs (keyed hashes of their arguments, ``Power`` = EXP) are functions by construction.
+Other UFs (keyed hashes of their arguments) are functions by construction; ``Power`` couples
+every constraint that applies it (its symbolic applications are shared candidate variables).
 Top-level conjunctions are split first (``Constraints.get_all_constraints`` appends the
 keccak manager's conditions as one big ``And``, constraints.py:132-133; its conjuncts
 belong to different buckets).
@@ -89,6 +90,11 @@ def dependence_keys(t: T.Term) -> FrozenSet[str]:
             m = _KECCAK_RE.match(x.val[0])
             if m:
                 own.add("k:" + m.group(1))
+            elif x.val[0] == "Power":
+                # Power's symbolic applications are candidate variables kept functional
+                # by argument value across the set (to_dag.TermLowering._power): every
+                # constraint applying it, concrete table entries included, shares a bucket
+                own.add("f:Power")
         for a in x.args:
             own |= _keys_memo[a]
         _keys_memo[x] = frozenset(own)

@@ -65,6 +65,10 @@ class Witness:
                 self.vars[term.val] = val
             elif term.op == "bvar":
                 self.bools[term.val] = bool(val & 1)
+            elif term.op == "extract" and term.args[0].op == "var":
+                # one 256-bit chunk of a wider free symbol (to_dag._lower_wide)
+                name, lo = term.args[0].val, term.val[1]
+                self.vars[name] = self.vars.get(name, 0) | (val << lo)
             else:
                 self.reads[term] = val
         self.array_reads = lowered.array_reads
@@ -158,13 +162,27 @@ class Witness:
                 return self.ev(a.args[0])  # inv(f(x)) = x, as substituted by the lowering
             x = self.ev(a)
             return self._keccak(n, x) if m.group(2) is None else self._keccak_inv(n, x, t)
-        if fname == "Power" and len(t.args) == 2:
-            return pow(self.ev(t.args[0]), self.ev(t.args[1]), 1 << 256)
+        if fname == "Power" and len(t.args) == 2 and t.width == 256:
+            return self._power(t)
         h = None
         for a in t.args:
             for c in _chunks(self.ev(a), a.width):
                 h = uf_hash(c if h is None else h ^ c, salt_of(fname))
         return h & T.M(t.width)
+
+    def _power(self, t: T.Term) -> int:
+        """The lowering's Power interpretation (to_dag.TermLowering._power), by value."""
+        b, e = self.ev(t.args[0]), self.ev(t.args[1])
+        apps = [(args, app) for (fname, args, app) in self.uf_apps if fname == "Power" and len(args) == 2]
+        for args, _ in apps:
+            if args[0].op == "bv" and args[1].op == "bv" and (args[0].val, args[1].val) == (b, e):
+                return pow(b, e, 1 << 256)
+        if b == 256:
+            return 1 << (8 * (e % 32))
+        for args, app in apps:
+            if app in self.reads and (self.ev(args[0]), self.ev(args[1])) == (b, e):
+                return self.reads[app]
+        return 1   # model completion outside the set's applications: a positive value
 
     # ---- evaluator ------------------------------------------------------------------------
     def ev(self, t: T.Term):

@@ -18,10 +18,17 @@ every GPU candidate *is* a complete model:
   construction; ``keccak256_<n>-1`` is substituted through ``inv(f(t)) = t`` and otherwise
   looked up among the set's f-applications, with the injectivity of f on the set added as
   side constraints (f(a) = f(b) -> a = b) so the interpretation stays a function;
-* ``Power`` (exponent_function_manager.py:29-68) is interpreted as real modular EXP;
-  any other UF as a keyed hash of its arguments.
-Values wider than 256 bits (keccak256_512 inputs, zero-padded ``==``, bitvec.py:16-22) are
-carried as 256-bit chunks.  Anything else raises LoweringError -> the query goes to z3.
+* ``Power`` (exponent_function_manager.py:29-68) is interpreted so that its conditions hold
+  by construction (``TermLowering._power``): concrete facts c1^c2, base 256 as
+  256^(e mod 32), other symbolic applications as candidate variables kept functional by
+  argument value; any other UF as a keyed hash of its arguments.
+Values wider than 256 bits are carried as 256-bit chunks: keccak256_512 inputs, zero-padded
+``==`` (bitvec.py:16-22), and z3's expansion of ``BVAddNoOverflow(a, b, False)`` —
+``((_ extract 256 256) (bvadd ((_ zero_extend 1) a) ((_ zero_extend 1) b)))``, the 257-bit
+sum's carry (bitvec_helper.py:199-213, used by every IntegerArithmetics query,
+integer.py:144-158).  Chunked ops: concat / zero_extend / extract (across chunks) / ite /
+add / sub (carry rippled as a B value) / neg / and / or / xor / not / shifts by a constant /
+= / unsigned and signed orderings.  Anything else raises LoweringError -> z3.
 """
 
 from __future__ import annotations
@@ -107,9 +114,11 @@ class TermLowering:
         self.uf_apps: List[Tuple[str, tuple, T.Term]] = []
         self.side: List[int] = []
         self._actor_consts: Optional[int] = None
+        self.power_apps: List[Tuple[T.Term, T.Term, int, bool]] = []  # (b, e, value node, symbolic)
+        self.power_facts: Dict[Tuple[int, int], int] = {}            # concrete (b, e) -> b^e
 
     # ---- leaves -----------------------------------------------------------------------
-    def _var(self, name: str, w: int, term: T.Term) -> int:
+    def _var(self, name: str, w: int, term: T.Term, parent: Optional[int] = None) -> int:
         kind = var_kind(name, w)
         hint0 = hint1 = 0
         if kind == ir.VK_ACTOR:
@@ -117,7 +126,8 @@ class TermLowering:
         elif kind == ir.VK_SMALL:
             hint0 = 4 + 32 * 8
         before = len(self.dag.vars)
-        node = self.dag.var(name, w, kind, hint0, hint1, self.parent.get(name))
+        node = self.dag.var(name, w, kind, hint0, hint1,
+                            parent if parent is not None else self.parent.get(name))
         if len(self.dag.vars) > before:
             self.var_terms.append(term)
         return node
@@ -151,7 +161,10 @@ class TermLowering:
 
     def chunks(self, t: T.Term) -> List[Tuple[int, int]]:
         """Little-endian 256-bit-aligned chunks (node, width) of a value of any width."""
-        pieces = self._pieces(t)
+        return self._rechunk(self._pieces(t))
+
+    def _rechunk(self, pieces: List[Tuple[int, int]]) -> List[Tuple[int, int]]:
+        """LSB-first pieces (node, width) -> 256-bit-aligned chunks."""
         out: List[Tuple[int, int]] = []
         cur: List[Tuple[int, int]] = []   # pieces of the current chunk (LSB first)
         fill = 0
@@ -213,15 +226,7 @@ class TermLowering:
     def _lower_bv(self, t: T.Term):
         op, wd = t.op, t.width
         if wd > 256:
-            if op in ("concat", "zero_extend", "bv"):
-                return self.chunks(t)
-            if op == "apply":
-                return self._apply(t)
-            if op == "ite":
-                c = self.b(t.args[0])
-                a, b = self.chunks(t.args[1]), self.chunks(t.args[2])
-                return [(self.dag.op(ir.W_ITE, x[1], c, x[0], y[0]), x[1]) for x, y in zip(a, b)]
-            raise LoweringError(f"{wd}-bit {op}")
+            return self._lower_wide(t)
         if op == "bv":
             return self.dag.const(t.val, wd)
         if op == "var":
@@ -237,10 +242,8 @@ class TermLowering:
             src = t.args[0]
             if src.width <= 256:
                 return self.dag.op(ir.W_EXTRACT, wd, self.node(src), aux=lo)
-            for (base, cwid), cnode in self._chunk_offsets(src):
-                if base <= lo and hi < base + cwid:
-                    return self.dag.op(ir.W_EXTRACT, wd, cnode, aux=lo - base)
-            raise LoweringError("extract across a 256-bit chunk boundary")
+            (node, _), = self._slice(self.chunks(src), lo, wd)
+            return node
         if op == "concat":
             parts = t.args
             node, acc = self.node(parts[0]), parts[0].width
@@ -258,11 +261,114 @@ class TermLowering:
             return self._apply(t)
         raise LoweringError(f"unsupported bit-vector op {op}")
 
-    def _chunk_offsets(self, t):
-        off = 0
-        for node, cw in self.chunks(t):
-            yield (off, cw), node
-            off += cw
+    # ---- values wider than 256 bits (z3's 257-bit no-overflow expansions, 512-bit keccak
+    # inputs, zero-padded comparisons: bitvec.py:16-22, bitvec_helper.py:199-245) ---------
+    def _slice(self, chunks: List[Tuple[int, int]], lo: int, width: int) -> List[Tuple[int, int]]:
+        """Bits [lo, lo + width) of a chunked value, as chunks."""
+        d = self.dag
+        pieces, base = [], 0
+        for node, cw in chunks:
+            a, b = max(lo, base), min(lo + width, base + cw)
+            if a < b:
+                if a == base and b == base + cw:
+                    pieces.append((node, cw))
+                else:
+                    pieces.append((d.op(ir.W_EXTRACT, b - a, node, aux=a - base), b - a))
+            base += cw
+        return self._rechunk(pieces)
+
+    def _bit_to_w(self, bnode: int, w: int) -> int:
+        d = self.dag
+        return d.op(ir.W_ITE, w, bnode, d.const(1, w), d.const(0, w))
+
+    def _wide_addsub(self, A, B, sub: bool):
+        """Chunked add / subtract with the carry (borrow) rippled as a B value."""
+        d = self.dag
+        opc = ir.W_SUB if sub else ir.W_ADD
+        out, carry = [], None
+        for i, ((x, wx), (y, _)) in enumerate(zip(A, B)):
+            t = d.op(opc, wx, x, y)
+            s_, cw = t, None
+            if carry is not None:
+                cw = self._bit_to_w(carry, wx)
+                s_ = d.op(opc, wx, t, cw)
+            if i + 1 < len(A):   # carry out of a full 256-bit chunk
+                c1 = d.op(ir.B_ULT, wx, x, y) if sub else d.op(ir.B_ULT, wx, t, x)
+                if carry is not None:
+                    c2 = d.op(ir.B_ULT, wx, t, cw) if sub else d.op(ir.B_ULT, wx, s_, t)
+                    c1 = d.op(ir.B_OR, 1, c1, c2)
+                carry = c1
+            out.append((s_, wx))
+        return out
+
+    def _wide_cmp(self, op: str, a: T.Term, b: T.Term) -> int:
+        """bvult / bvule / bvslt / bvsle over chunks: decided by the highest differing chunk
+        (the top chunk compared signed for the signed forms)."""
+        d = self.dag
+        A, B = self.chunks(a), self.chunks(b)
+        signed = op in ("bvslt", "bvsle")
+        strict = op in ("bvult", "bvslt")
+        # lt over chunks 0..i, built from the bottom: lt_i = lt(x_i, y_i) | (x_i == y_i & lt_{i-1})
+        lt = None
+        for i, ((x, wx), (y, _)) in enumerate(zip(A, B)):
+            top = i == len(A) - 1
+            cmp = ir.B_SLT if (signed and top) else ir.B_ULT
+            li = d.op(cmp, wx, x, y)
+            if lt is not None:
+                li = d.op(ir.B_OR, 1, li, d.op(ir.B_AND, 1, d.op(ir.B_EQ, wx, x, y), lt))
+            lt = li
+        if strict:
+            return lt
+        # a <= b  <=>  not (b < a)
+        return d.op(ir.B_NOT, 1, self._wide_cmp("bvslt" if signed else "bvult", b, a))
+
+    def _lower_wide(self, t: T.Term):
+        op, wd = t.op, t.width
+        d = self.dag
+        if op in ("concat", "zero_extend", "bv"):
+            return self.chunks(t)
+        if op == "var":
+            # a free symbol wider than 256 bits: one candidate variable per chunk, each
+            # recorded as its extract term (the witness reassembles the symbol's value)
+            out, lo, pv = [], 0, self.parent.get(t.val)
+            while lo < wd:
+                cw = min(256, wd - lo)
+                part = T.extract(lo + cw - 1, lo, t)
+                out.append((self._var(f"{t.val}#{lo // 256}", cw, part,
+                                      None if pv is None else (pv >> lo) & ir.mask(cw)), cw))
+                lo += cw
+            return out
+        if op == "apply":
+            return self._apply(t)
+        if op == "ite":
+            c = self.b(t.args[0])
+            a, b = self.chunks(t.args[1]), self.chunks(t.args[2])
+            return [(d.op(ir.W_ITE, x[1], c, x[0], y[0]), x[1]) for x, y in zip(a, b)]
+        if op == "extract":
+            hi, lo = t.val
+            return self._slice(self.chunks(t.args[0]), lo, wd)
+        if op in ("bvadd", "bvsub"):
+            return self._wide_addsub(self.chunks(t.args[0]), self.chunks(t.args[1]), op == "bvsub")
+        if op == "bvneg":
+            zero = [(d.const(0, w), w) for _, w in self.chunks(t.args[0])]
+            return self._wide_addsub(zero, self.chunks(t.args[0]), True)
+        if op in ("bvand", "bvor", "bvxor"):
+            opc = {"bvand": ir.W_AND, "bvor": ir.W_OR, "bvxor": ir.W_XOR}[op]
+            return [(d.op(opc, wx, x, y), wx)
+                    for (x, wx), (y, _) in zip(self.chunks(t.args[0]), self.chunks(t.args[1]))]
+        if op == "bvnot":
+            return [(d.op(ir.W_NOT, wx, x), wx) for x, wx in self.chunks(t.args[0])]
+        if op in ("bvshl", "bvlshr") and t.args[1].op == "bv":
+            # shift by a constant k: bits move between chunks, zeros fill in
+            k = t.args[1].val
+            if k >= wd:
+                return self.chunks(T.const(0, wd))
+            A = self.chunks(t.args[0])
+            zeros = self.chunks(T.const(0, k)) if k else []
+            if op == "bvshl":   # concat(a[wd-1-k : 0], 0_k)
+                return self._rechunk(zeros + self._slice(A, 0, wd - k))
+            return self._rechunk(self._slice(A, k, wd - k) + zeros)
+        raise LoweringError(f"{wd}-bit {op}")
 
     def _lower_bool(self, t: T.Term) -> int:
         op = t.op
@@ -299,6 +405,8 @@ class TermLowering:
             return d.op(ir.B_EQ, a.width, self.node(a), self.node(b))
         if op in _BCMP:
             a, b = t.args
+            if a.width > 256 and op in ("bvult", "bvule", "bvslt", "bvsle"):
+                return self._wide_cmp(op, a, b)
             return d.op(_BCMP[op], a.width, self.node(a), self.node(b))
         raise LoweringError(f"unsupported bool op {op}")
 
@@ -372,11 +480,65 @@ class TermLowering:
             if m.group(2) is None:
                 return self._keccak(n, args[0], t)
             return self._keccak_inv(n, args[0], t)
+        if fname == "Power" and len(args) == 2 and t.width == 256:
+            return self._power(t)
         self.uf_apps.append((fname, args, t))
-        if fname == "Power" and len(args) == 2:
-            return d.op(ir.W_EXP, 256, self.node(args[0]), self.node(args[1]))
         h = self._hash_args(args, salt_of(fname))
         return h if t.width == 256 else d.op(ir.W_EXTRACT, t.width, h, aux=0)
+
+    def _power(self, t: T.Term) -> int:
+        """``Power(b, e)``, the UF Mythril uses for symbolic EXP
+        (exponent_function_manager.py:40-68; instructions.py:625-639).  Its conditions are
+        ``Power(b, e) >s 0`` per symbolic EXP, the 32 table entries ``Power(256, i) = 256^i``,
+        ``Power(256, e %u 32) == Power(256, e)`` for base 256, and ``Power(c1, c2) =
+        c1^c2 mod 2^256`` for a concrete EXP.  Interpretation, by argument value:
+        1. (b, e) equal to a concrete application's arguments (c1, c2) in the set ->
+           c1^c2 mod 2^256 (functional consistency with the concrete facts);
+        2. b == 256 -> 256^(e mod 32) = 2^(8 (e mod 32)) — satisfies the table, the
+           ``e %u 32`` condition and ``>s 0`` (at most 2^248) for every e;
+        3. otherwise a free candidate variable per symbolic application, equal to the first
+           earlier application whose arguments evaluate equal (a function, like the array
+           reads); the set's own ``>s 0`` constraint then decides the candidate.
+        Real modular EXP is not a model: ``Power(256, e) = 256^e mod 2^256`` is 0 for every
+        e >= 32, which the conditions forbid."""
+        d = self.dag
+        b_t, e_t = t.args
+        for (bt, et, node, _) in self.power_apps:
+            if bt is b_t and et is e_t:
+                return node
+        if b_t.op == "bv" and e_t.op == "bv":
+            val = d.const(pow(b_t.val, e_t.val, 1 << 256), 256)
+        else:
+            bn, en = self.node(b_t), self.node(e_t)
+            val = self._var(f"Power@{sum(1 for a in self.power_apps if a[3])}", 256, t)
+            for (bt, et, node, sym) in reversed(self.power_apps):
+                if sym:
+                    same = d.op(ir.B_AND, 1, d.op(ir.B_EQ, 256, bn, self.node(bt)),
+                                d.op(ir.B_EQ, 256, en, self.node(et)))
+                    val = d.op(ir.W_ITE, 256, same, node, val)
+            rule = d.op(ir.W_SHL, 256, d.const(1, 256),
+                        d.op(ir.W_SHL, 256, d.op(ir.W_AND, 256, en, d.const(31, 256)), d.const(3, 256)))
+            val = d.op(ir.W_ITE, 256, d.op(ir.B_EQ, 256, bn, d.const(256, 256)), rule, val)
+            for (c1, c2), pv in self.power_facts.items():
+                same = d.op(ir.B_AND, 1, d.op(ir.B_EQ, 256, bn, d.const(c1, 256)),
+                            d.op(ir.B_EQ, 256, en, d.const(c2, 256)))
+                val = d.op(ir.W_ITE, 256, same, d.const(pv, 256), val)
+        self.power_apps.append((b_t, e_t, val, not (b_t.op == "bv" and e_t.op == "bv")))
+        self.uf_apps.append(("Power", (b_t, e_t), t))
+        return val
+
+    def _collect_power_facts(self, constraints: List[T.Term]) -> None:
+        seen, stack = set(), list(constraints)
+        while stack:
+            x = stack.pop()
+            if x in seen:
+                continue
+            seen.add(x)
+            if (x.op == "apply" and x.val[0] == "Power" and len(x.args) == 2
+                    and x.args[0].op == "bv" and x.args[1].op == "bv"):
+                c1, c2 = x.args[0].val, x.args[1].val
+                self.power_facts[(c1, c2)] = pow(c1, c2, 1 << 256)
+            stack.extend(x.args)
 
     def _keccak(self, n: int, arg: T.Term, t: T.Term) -> int:
         d = self.dag
@@ -443,6 +605,7 @@ class TermLowering:
 
     # ---- driver ---------------------------------------------------------------------------
     def lower(self, constraints: List[T.Term]) -> Lowered:
+        self._collect_power_facts(constraints)
         for c in constraints:
             if not c.is_bool:
                 raise LoweringError("constraint is not a Bool")

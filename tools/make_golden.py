@@ -130,10 +130,38 @@ def ops_vectors(seed=20260101):
     return out
 
 
+def wide_vectors(seed=20261016):
+    """Per-op vectors at widths > 256 (257: z3's no-overflow expansions; 512: keccak inputs
+    and zero-padded equalities), expected values from the oracle's width-generic functions."""
+    import pyoracle as O
+    rng = random.Random(seed)
+    names = {"bvadd": O.bvadd, "bvsub": O.bvsub, "bvand": lambda a, b, w: a & b,
+             "bvxor": lambda a, b, w: a ^ b, "bvneg": lambda a, b, w: O.bvneg(a, w),
+             "bvnot": lambda a, b, w: O.bvnot(a, w), "bvult": O.ult, "bvule": O.ule,
+             "bvslt": O.slt, "bvsle": O.sle}
+    out = []
+    for w in (257, 300, 512):
+        M = (1 << w) - 1
+        pool = sorted({p & M for p in [0, 1, 2, M, M - 1, 1 << (w - 1), (1 << (w - 1)) - 1,
+                                        (1 << 256) - 1, 1 << 256, (1 << 255) + 7]})
+        for name, fn in names.items():
+            pairs = [(a, b) for a in pool[::2] for b in pool[1::2]]
+            pairs += [(rng.getrandbits(w), rng.getrandbits(w)) for _ in range(6)]
+            for a, b in pairs:
+                r = fn(a, b, w)
+                out.append({"op": name, "w": w, "a": a, "b": b, "r": int(r)})
+    return {"source": "oracle/pyoracle.py width-generic ops (tools/make_golden.py wide_vectors)",
+            "vectors": out}
+
+
 def main():
     os.makedirs(GOLD, exist_ok=True)
+    if "--wide-only" in sys.argv:
+        with open(os.path.join(GOLD, "wide.json"), "w") as f:
+            json.dump(wide_vectors(), f, indent=0, sort_keys=True)
+        return
     sets = {"vmtests.json": vmtests(), "vmsha3.json": vmsha3(), "eip145.json": eip145(),
-            "ops.json": ops_vectors()}
+            "ops.json": ops_vectors(), "wide.json": wide_vectors()}
     for fn, data in sets.items():
         with open(os.path.join(GOLD, fn), "w") as f:
             json.dump(data, f, indent=0, sort_keys=True)
