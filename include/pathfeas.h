@@ -18,8 +18,10 @@
  *   pf_keccak256_batch    eth_hash keccak via support_utils.sha3 (support_utils.py:93-101) as
  *                         called by KeccakFunctionManager.find_concrete_keccak
  *                         (keccak_function_manager.py:57-69) and get_code_hash (:74-90)
+ *   pf_check_batches      the same over several devices of one process (one batch each):
+ *                         the tx-boundary batch of svm.py:266-286 split across a node
  * The *_dev variants take device pointers (HBM-resident inputs, e.g. torch tensors) and an
- * optional hipStream_t (NULL = the library's stream).
+ * optional hipStream_t (NULL = the library stream of the batch's device).
  */
 #ifndef PATHFEAS_H
 #define PATHFEAS_H
@@ -44,7 +46,11 @@ typedef struct pf_stats {
 } pf_stats;
 
 /* ---- lifetime ---------------------------------------------------------------------- */
-int pf_init(int device);            /* select the device, create the library stream      */
+/* Initialise the devices of device_mask (bit d = HIP device d; all must be gfx950): one
+ * library stream per device.  Callable again to add devices.  The lowest initialised device
+ * is the default one (pf_batch_create, Keccak).  One process can drive every GPU of a node
+ * this way (Mythril's analysis is one process); one process per GPU passes one bit.      */
+int pf_init(uint64_t device_mask);
 int pf_shutdown(void);
 const char* pf_last_error(void);
 int pf_version(void);               /* ABI version                                         */
@@ -58,6 +64,11 @@ int pf_batch_create(const uint32_t* code, size_t n_ins, const uint32_t* consts, 
                     const uint32_t* schema, size_t n_vars, const uint32_t* parents,
                     size_t n_parents, const pf_set_desc* descs, size_t n_sets,
                     uint64_t* handle_out);
+/* same, on a given initialised device (-1 = the default device)                            */
+int pf_batch_create_on(int device, const uint32_t* code, size_t n_ins, const uint32_t* consts,
+                       size_t n_const, const uint32_t* schema, size_t n_vars,
+                       const uint32_t* parents, size_t n_parents, const pf_set_desc* descs,
+                       size_t n_sets, uint64_t* handle_out);
 int pf_batch_free(uint64_t handle);
 
 /* Generate candidates [0, budget) on device for every set and search for a witness.
@@ -69,6 +80,11 @@ int pf_batch_free(uint64_t handle);
 int pf_check_batch(uint64_t handle, uint64_t global_seed, uint32_t budget, uint32_t flags,
                    uint32_t timeout_ms, uint32_t* found_out, uint8_t* sat_bitmap_out,
                    pf_stats* stats);
+/* Search n batches (typically one per device) at once: every launch is enqueued on its
+ * device's stream before any result is read, so the devices run concurrently; found_out
+ * receives the verdicts concatenated in handle order; stats (optional) has n entries.    */
+int pf_check_batches(const uint64_t* handles, size_t n, uint64_t global_seed, uint32_t budget,
+                     uint32_t flags, uint32_t timeout_ms, uint32_t* found_out, pf_stats* stats);
 /* same, result left in a device buffer of n_sets u32 (d_found), no host copy of results   */
 int pf_check_batch_dev(uint64_t handle, uint64_t global_seed, uint32_t budget, uint32_t flags,
                        uint32_t timeout_ms, uint32_t* d_found, pf_stats* stats, void* stream);

@@ -41,17 +41,22 @@ _sz = ctypes.c_size_t
 
 # name -> (restype, argtypes); kept in sync with include/pathfeas.h (tests/test_abi.py)
 SIGNATURES = {
-    "pf_init": (ctypes.c_int, [ctypes.c_int]),
+    "pf_init": (ctypes.c_int, [ctypes.c_uint64]),
     "pf_shutdown": (ctypes.c_int, []),
     "pf_last_error": (ctypes.c_char_p, []),
     "pf_version": (ctypes.c_int, []),
     "pf_device_count": (ctypes.c_int, []),
     "pf_batch_create": (ctypes.c_int, [_u32p, _sz, _u32p, _sz, _u32p, _sz, _u32p, _sz, _u32p,
                                        _sz, _u64p]),
+    "pf_batch_create_on": (ctypes.c_int, [ctypes.c_int, _u32p, _sz, _u32p, _sz, _u32p, _sz, _u32p,
+                                          _sz, _u32p, _sz, _u64p]),
     "pf_batch_free": (ctypes.c_int, [ctypes.c_uint64]),
     "pf_check_batch": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
                                       ctypes.c_uint32, ctypes.c_uint32, _u32p, _u8p,
                                       ctypes.POINTER(pf_stats)]),
+    "pf_check_batches": (ctypes.c_int, [_u64p, _sz, ctypes.c_uint64, ctypes.c_uint32,
+                                        ctypes.c_uint32, ctypes.c_uint32, _u32p,
+                                        ctypes.POINTER(pf_stats)]),
     "pf_check_batch_dev": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
                                           ctypes.POINTER(pf_stats), ctypes.c_void_p]),
@@ -69,7 +74,7 @@ SIGNATURES = {
 
 _lib = None
 _lib_lock = threading.Lock()
-_initialised_device: Optional[int] = None
+_initialised: set = set()
 
 
 def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
@@ -110,16 +115,23 @@ def check(rc: int, what: str) -> None:
         raise PathFeasError(f"{what} failed ({rc}): {msg}")
 
 
-def init(device: int = 0) -> None:
-    """Select the GPU for this process (one process per GPU)."""
-    global _initialised_device
+def init(devices=0) -> None:
+    """Initialise the engine's GPUs: one index (one process per GPU) or several (one process
+    driving a node: pf_init's device mask)."""
+    devs = [devices] if isinstance(devices, int) else list(devices)
     L = lib()
-    if _initialised_device == device:
+    if set(devs) <= _initialised:
         return
-    if L.pf_device_count() <= 0:
+    n = L.pf_device_count()
+    if n <= 0:
         raise PathFeasError("no HIP device visible: the MI355X path-feasibility engine has no CPU fallback")
-    check(L.pf_init(device), f"pf_init({device})")
-    _initialised_device = device
+    mask = 0
+    for d in devs:
+        if not 0 <= d < min(n, 64):
+            raise PathFeasError(f"device {d} out of range ({n} visible)")
+        mask |= 1 << d
+    check(L.pf_init(mask), f"pf_init({devs})")
+    _initialised.update(devs)
 
 
 def ptr_u32(a: np.ndarray):

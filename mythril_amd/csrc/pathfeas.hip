@@ -24,11 +24,19 @@ namespace {
 std::mutex g_mu;
 thread_local std::string g_err_tls;
 std::string g_err;
-int g_device = -1;
-hipStream_t g_stream = nullptr;
-hipEvent_t g_ev0 = nullptr, g_ev1 = nullptr;
-uint32_t* g_scratch_u32 = nullptr;  // small device scratch (counters, t0)
-int g_num_cus = 256;
+
+// One entry per initialised device (pf_init's mask): its library stream, timing events for
+// the Keccak launches and the launch geometry inputs.  Batches live on one device each and
+// carry their own counters and events, so launches of different batches never share scratch.
+struct Dev {
+    int id = -1;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    int num_cus = 256;
+    hipStream_t last_stream = nullptr;  // see switch_stream
+};
+std::vector<Dev> g_devs;  // ascending device ids
+int g_default = -1;       // index in g_devs of the default device (lowest id)
 // search-kernel waves launched per CU (PF_WAVES_PER_CU overrides both).  Measured on config 3
 // (1024 sets x 65,536 candidates, profiles/r01_wavesweep.md): with the longest-first set order
 // the full sweep peaks at 512 (finer slices even out the sets' unequal costs in the last round
@@ -65,7 +73,9 @@ struct Batch {
     uint4* d_schema = nullptr;
     uint32_t* d_parents = nullptr;
     uint32_t* d_found = nullptr;
-    uint32_t* d_order = nullptr;  // set ids, most expensive first (search-kernel wave order)
+    uint32_t* d_order = nullptr;    // set ids, most expensive first (search-kernel wave order)
+    uint32_t* d_scratch = nullptr;  // this batch's launch counters (u64 [0..3]) and t0 (u64 [4])
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
     ~Batch() {  // also the error path of pf_batch_create: frees whatever was allocated
         hipFree(d_code);
         hipFree(d_consts);
@@ -74,6 +84,9 @@ struct Batch {
         hipFree(d_descs);
         hipFree(d_found);
         hipFree(d_order);
+        hipFree(d_scratch);
+        if (ev0) hipEventDestroy(ev0);
+        if (ev1) hipEventDestroy(ev1);
     }
 };
 
@@ -85,20 +98,38 @@ struct DevBuf {
     T* as() { return static_cast<T*>(p); }
 };
 
-// The library's scratch counters and events are shared by every launch.  A launch on a
-// caller's stream (the *_dev entry points) returns without waiting, so before the next
-// launch on a different stream reuses them, that stream is drained.
-hipStream_t g_last_stream = nullptr;
-int switch_stream(hipStream_t st) {
-    if (g_last_stream && g_last_stream != st) HIPCHK(hipStreamSynchronize(g_last_stream));
-    g_last_stream = st;
+Dev* find_dev(int id) {
+    for (auto& d : g_devs)
+        if (d.id == id) return &d;
+    return nullptr;
+}
+
+// A launch on a caller's stream (the *_dev entry points) returns without waiting; before the
+// device's next launch on a different stream reuses the Keccak events or a batch it reads,
+// that stream is drained.
+int switch_stream(Dev* D, hipStream_t st) {
+    if (D->last_stream && D->last_stream != st) HIPCHK(hipStreamSynchronize(D->last_stream));
+    D->last_stream = st;
     return 0;
 }
 
-int ensure_init_locked() {
-    if (g_device < 0) return fail("pf_init() has not been called");
-    HIPCHK(hipSetDevice(g_device));
-    return 0;
+// select (and make current) a device: the default one for device < 0
+Dev* use_dev(int device) {
+    if (g_devs.empty()) {
+        fail("pf_init() has not been called");
+        return nullptr;
+    }
+    Dev* D = device < 0 ? &g_devs[g_default] : find_dev(device);
+    if (!D) {
+        fail("device %d was not initialised by pf_init", device);
+        return nullptr;
+    }
+    hipError_t e = hipSetDevice(D->id);
+    if (e != hipSuccess) {
+        fail("hipSetDevice(%d): %s", D->id, hipGetErrorString(e));
+        return nullptr;
+    }
+    return D;
 }
 
 template <typename T>
@@ -112,14 +143,14 @@ int upload(T** dst, const void* src, size_t bytes) {
 
 Batch* as_batch(uint64_t h) { return reinterpret_cast<Batch*>(static_cast<uintptr_t>(h)); }
 
-hipStream_t pick_stream(void* s) { return s ? reinterpret_cast<hipStream_t>(s) : g_stream; }
+hipStream_t pick_stream(Dev* D, void* s) { return s ? reinterpret_cast<hipStream_t>(s) : D->stream; }
 
-// launch geometry for the search kernel: enough waves to fill 256 CUs several times over,
+// launch geometry for the search kernel: enough waves to fill the CUs several times over,
 // each wave walking >= 64 candidates of one set.
-void geometry(uint32_t n_sets, uint32_t budget, uint32_t flags, uint32_t* per_wave,
+void geometry(int num_cus, uint32_t n_sets, uint32_t budget, uint32_t flags, uint32_t* per_wave,
               uint32_t* slices) {
     const uint64_t target_waves =
-        (uint64_t)g_num_cus * ((flags & PF_FLAG_EARLY_EXIT) ? g_waves_per_cu_early : g_waves_per_cu_full);
+        (uint64_t)num_cus * ((flags & PF_FLAG_EARLY_EXIT) ? g_waves_per_cu_early : g_waves_per_cu_full);
     uint64_t groups = (budget + 63u) / 64u;  // 64-candidate groups per set
     uint64_t sl = (target_waves + n_sets - 1) / std::max<uint32_t>(n_sets, 1u);
     sl = std::max<uint64_t>(1, std::min<uint64_t>(sl, groups));
@@ -129,40 +160,44 @@ void geometry(uint32_t n_sets, uint32_t budget, uint32_t flags, uint32_t* per_wa
     if (*slices == 0) *slices = 1;
 }
 
-int check_launch(Batch* B, uint64_t gseed, uint32_t budget, uint32_t flags, uint32_t timeout_ms,
-                 uint32_t* d_found, pf_stats* stats, hipStream_t st) {
-    if (switch_stream(st)) return -1;
-    unsigned long long* d_counters = reinterpret_cast<unsigned long long*>(g_scratch_u32);
-    uint64_t* d_t0 = reinterpret_cast<uint64_t*>(g_scratch_u32 + 8);
+// Enqueue one search over batch B on stream st (B's device must be current).
+int check_enqueue(Batch* B, uint64_t gseed, uint32_t budget, uint32_t flags, uint32_t timeout_ms,
+                  uint32_t* d_found, hipStream_t st) {
+    Dev* D = find_dev(B->device);
+    unsigned long long* d_counters = reinterpret_cast<unsigned long long*>(B->d_scratch);
+    uint64_t* d_t0 = reinterpret_cast<uint64_t*>(B->d_scratch + 8);
 #ifdef PF_PROFILE_UNITS
-    HIPCHK(hipMemsetAsync(g_scratch_u32, 0, 256, st));
+    HIPCHK(hipMemsetAsync(B->d_scratch, 0, 256, st));
 #else
-    HIPCHK(hipMemsetAsync(g_scratch_u32, 0, 64, st));
+    HIPCHK(hipMemsetAsync(B->d_scratch, 0, 64, st));
 #endif
-    HIPCHK(hipMemsetAsync(d_found, 0xff, B->n_sets * sizeof(uint32_t), st));
-    if (B->n_sets == 0 || budget == 0) {
-        if (stats) memset(stats, 0, sizeof(*stats));
-        return 0;
+    HIPCHK(hipMemsetAsync(d_found, 0xff, std::max<size_t>(B->n_sets, 1) * sizeof(uint32_t), st));
+    HIPCHK(hipEventRecord(B->ev0, st));
+    if (B->n_sets > 0 && budget > 0) {
+        uint32_t per_wave, slices;
+        geometry(D->num_cus, (uint32_t)B->n_sets, budget, flags, &per_wave, &slices);
+        const uint64_t waves = (uint64_t)B->n_sets * slices;
+        if (waves > 0xffffffffull) return fail("batch too large: %llu waves", (unsigned long long)waves);
+        const uint32_t blocks = (uint32_t)((waves + 3) / 4);
+        const uint64_t deadline = timeout_ms ? (uint64_t)timeout_ms * 100000ull : 0ull;  // 100 MHz
+        hipLaunchKernelGGL((flags & PF_FLAG_EARLY_EXIT) ? pf_check_early_kernel : pf_check_kernel,
+                           dim3(blocks), dim3(256), 0, st, B->d_descs, B->d_order,
+                           (uint32_t)B->n_sets, B->d_code, B->d_consts, B->d_schema, B->d_parents,
+                           gseed, budget, per_wave, slices, flags, deadline, d_t0, d_found, d_counters);
+        HIPCHK(hipGetLastError());
     }
-    uint32_t per_wave, slices;
-    geometry((uint32_t)B->n_sets, budget, flags, &per_wave, &slices);
-    const uint64_t waves = (uint64_t)B->n_sets * slices;
-    if (waves > 0xffffffffull) return fail("batch too large: %llu waves", (unsigned long long)waves);
-    const uint32_t blocks = (uint32_t)((waves + 3) / 4);
-    const uint64_t deadline = timeout_ms ? (uint64_t)timeout_ms * 100000ull : 0ull;  // 100 MHz
-    HIPCHK(hipEventRecord(g_ev0, st));
-    hipLaunchKernelGGL((flags & PF_FLAG_EARLY_EXIT) ? pf_check_early_kernel : pf_check_kernel,
-                       dim3(blocks), dim3(256), 0, st, B->d_descs, B->d_order,
-                       (uint32_t)B->n_sets, B->d_code, B->d_consts, B->d_schema, B->d_parents,
-                       gseed, budget, per_wave, slices, flags, deadline, d_t0, d_found, d_counters);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(g_ev1, st));
+    HIPCHK(hipEventRecord(B->ev1, st));
+    return 0;
+}
+
+// Wait for B's last search on stream st and read its counters.
+int check_collect(Batch* B, hipStream_t st, pf_stats* stats) {
+    unsigned long long h[4];
+    HIPCHK(hipMemcpyAsync(h, B->d_scratch, sizeof(h), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, B->ev0, B->ev1));
     if (stats) {
-        unsigned long long h[4];
-        HIPCHK(hipMemcpyAsync(h, d_counters, sizeof(h), hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
-        float ms = 0.f;
-        HIPCHK(hipEventElapsedTime(&ms, g_ev0, g_ev1));
         stats->evals_full = h[0];
         stats->cands_decided = h[1];
         stats->ops = h[2];
@@ -177,14 +212,16 @@ int check_launch(Batch* B, uint64_t gseed, uint32_t budget, uint32_t flags, uint
 
 extern "C" {
 
-int pf_version(void) { return 1; }
+int pf_version(void) { return 2; }
 
 #ifdef PF_PROFILE_UNITS
-// profiling builds only (tools/unitprof.py): per-unit s_memtime cycles of the last launch
-int pf_prof_read(uint64_t* out) {
+// profiling builds only (tools/unitprof.py): per-unit s_memtime cycles of a batch's last launch
+int pf_prof_read(uint64_t handle, uint64_t* out) {
     std::lock_guard<std::mutex> lk(g_mu);
-    if (ensure_init_locked()) return -1;
-    HIPCHK(hipMemcpy(out, g_scratch_u32 + 2 * PF_PROF_SLOT, (PF_PROF_BUCKETS + 1) * 8,
+    Batch* B = as_batch(handle);
+    if (!B || !use_dev(B->device)) return -1;
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(out, B->d_scratch + 2 * PF_PROF_SLOT, (PF_PROF_BUCKETS + 1) * 8,
                      hipMemcpyDeviceToHost));
     return 0;
 }
@@ -202,53 +239,58 @@ int pf_device_count(void) {
     return n;
 }
 
-int pf_init(int device) {
+int pf_init(uint64_t device_mask) {
     std::lock_guard<std::mutex> lk(g_mu);
     int n = 0;
     HIPCHK(hipGetDeviceCount(&n));
-    if (device < 0 || device >= n) return fail("pf_init: device %d out of range (%d devices)", device, n);
-    if (g_device == device) return 0;
-    if (g_device >= 0) return fail("pf_init: already initialised on device %d", g_device);
-    HIPCHK(hipSetDevice(device));
-    hipDeviceProp_t prop;
-    HIPCHK(hipGetDeviceProperties(&prop, device));
-    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
-        return fail("pf_init: device %d is %s, this build targets gfx950", device, prop.gcnArchName);
-    g_num_cus = prop.multiProcessorCount;
+    if (device_mask == 0) return fail("pf_init: empty device mask");
+    if (n < 64 && (device_mask >> n)) return fail("pf_init: mask %llx names devices beyond the %d visible",
+                                                  (unsigned long long)device_mask, n);
     if (const char* e = getenv("PF_WAVES_PER_CU")) {
         long v = strtol(e, nullptr, 10);
         if (v >= 8 && v <= 4096) g_waves_per_cu_full = g_waves_per_cu_early = (uint32_t)v;
     }
-    HIPCHK(hipStreamCreateWithFlags(&g_stream, hipStreamNonBlocking));
-    HIPCHK(hipEventCreate(&g_ev0));
-    HIPCHK(hipEventCreate(&g_ev1));
-    HIPCHK(hipMalloc((void**)&g_scratch_u32, 256));
-    g_device = device;
+    for (int id = 0; id < n && id < 64; ++id) {
+        if (!((device_mask >> id) & 1ull) || find_dev(id)) continue;
+        HIPCHK(hipSetDevice(id));
+        hipDeviceProp_t prop;
+        HIPCHK(hipGetDeviceProperties(&prop, id));
+        if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+            return fail("pf_init: device %d is %s, this build targets gfx950", id, prop.gcnArchName);
+        Dev D;
+        D.id = id;
+        D.num_cus = prop.multiProcessorCount;
+        HIPCHK(hipStreamCreateWithFlags(&D.stream, hipStreamNonBlocking));
+        HIPCHK(hipEventCreate(&D.ev0));
+        HIPCHK(hipEventCreate(&D.ev1));
+        g_devs.push_back(D);
+    }
+    std::sort(g_devs.begin(), g_devs.end(), [](const Dev& a, const Dev& b) { return a.id < b.id; });
+    g_default = 0;
     return 0;
 }
 
 int pf_shutdown(void) {
     std::lock_guard<std::mutex> lk(g_mu);
-    if (g_device < 0) return 0;
-    hipSetDevice(g_device);
-    hipStreamSynchronize(g_stream);
-    hipFree(g_scratch_u32);
-    hipEventDestroy(g_ev0);
-    hipEventDestroy(g_ev1);
-    hipStreamDestroy(g_stream);
-    g_scratch_u32 = nullptr;
-    g_stream = nullptr;
-    g_last_stream = nullptr;
-    g_device = -1;
+    for (auto& D : g_devs) {
+        hipSetDevice(D.id);
+        hipDeviceSynchronize();
+        hipEventDestroy(D.ev0);
+        hipEventDestroy(D.ev1);
+        hipStreamDestroy(D.stream);
+    }
+    g_devs.clear();
+    g_default = -1;
     return 0;
 }
 
-int pf_batch_create(const uint32_t* code, size_t n_ins, const uint32_t* consts, size_t n_const,
-                    const uint32_t* schema, size_t n_vars, const uint32_t* parents,
-                    size_t n_parents, const pf_set_desc* descs, size_t n_sets,
-                    uint64_t* handle_out) {
+int pf_batch_create_on(int device, const uint32_t* code, size_t n_ins, const uint32_t* consts,
+                       size_t n_const, const uint32_t* schema, size_t n_vars,
+                       const uint32_t* parents, size_t n_parents, const pf_set_desc* descs,
+                       size_t n_sets, uint64_t* handle_out) {
     std::lock_guard<std::mutex> lk(g_mu);
-    if (ensure_init_locked()) return -1;
+    Dev* Dv = use_dev(device);
+    if (!Dv) return -1;
     if (!handle_out) return fail("pf_batch_create: null handle_out");
     // host-side shape checks: every kernel index is derived from these
     uint32_t max_vars = 0;
@@ -317,7 +359,7 @@ int pf_batch_create(const uint32_t* code, size_t n_ins, const uint32_t* consts, 
     }
     code = code_fixed.data();
     Batch* B = new Batch();
-    B->device = g_device;
+    B->device = Dv->id;
     B->n_ins = n_ins;
     B->n_const = n_const;
     B->n_vars = n_vars;
@@ -332,6 +374,9 @@ int pf_batch_create(const uint32_t* code, size_t n_ins, const uint32_t* consts, 
     rc |= upload(&B->d_parents, parents, n_parents * 32);
     rc |= upload(&B->d_descs, descs, n_sets * sizeof(pf_set_desc));
     rc |= upload(&B->d_found, nullptr, n_sets * 4);
+    rc |= upload(&B->d_scratch, nullptr, 256);
+    if (!rc && (hipEventCreate(&B->ev0) != hipSuccess || hipEventCreate(&B->ev1) != hipSuccess))
+        rc = fail("pf_batch_create: hipEventCreate failed");
     // Longest-first wave order: waves are dispatched in index order, so mapping the first
     // waves to the most expensive sets leaves the cheap ones for the last, partly filled
     // round.  Weights are measured SIMD cycles per instruction relative to a cheap op
@@ -362,32 +407,31 @@ int pf_batch_create(const uint32_t* code, size_t n_ins, const uint32_t* consts, 
     return 0;
 }
 
+int pf_batch_create(const uint32_t* code, size_t n_ins, const uint32_t* consts, size_t n_const,
+                    const uint32_t* schema, size_t n_vars, const uint32_t* parents,
+                    size_t n_parents, const pf_set_desc* descs, size_t n_sets,
+                    uint64_t* handle_out) {
+    return pf_batch_create_on(-1, code, n_ins, consts, n_const, schema, n_vars, parents, n_parents,
+                              descs, n_sets, handle_out);
+}
+
 int pf_batch_free(uint64_t handle) {
     std::lock_guard<std::mutex> lk(g_mu);
     Batch* B = as_batch(handle);
     if (!B) return 0;
-    hipSetDevice(B->device);
+    Dev* D = use_dev(B->device);
     // a *_dev launch may still be reading the batch on a caller's stream: drain the device
     hipDeviceSynchronize();
-    g_last_stream = nullptr;
+    if (D) D->last_stream = nullptr;
     delete B;
     return 0;
 }
 
-int pf_check_batch(uint64_t handle, uint64_t global_seed, uint32_t budget, uint32_t flags,
-                   uint32_t timeout_ms, uint32_t* found_out, uint8_t* sat_bitmap_out,
-                   pf_stats* stats) {
-    std::lock_guard<std::mutex> lk(g_mu);
-    if (ensure_init_locked()) return -1;
-    Batch* B = as_batch(handle);
-    if (!B) return fail("pf_check_batch: null batch");
-    pf_stats local;
-    pf_stats* st = stats ? stats : &local;
-    if (check_launch(B, global_seed, budget, flags, timeout_ms, B->d_found, st, g_stream)) return -1;
-    std::vector<uint32_t> found(B->n_sets);
-    if (B->n_sets)
-        HIPCHK(hipMemcpyAsync(found.data(), B->d_found, B->n_sets * 4, hipMemcpyDeviceToHost, g_stream));
-    HIPCHK(hipStreamSynchronize(g_stream));
+static int found_to_host(Batch* B, hipStream_t st, uint32_t* found_out, uint8_t* sat_bitmap_out,
+                         pf_stats* stats) {
+    std::vector<uint32_t> found(std::max<size_t>(B->n_sets, 1));
+    HIPCHK(hipMemcpyAsync(found.data(), B->d_found, found.size() * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
     uint64_t nsat = 0;
     if (sat_bitmap_out) memset(sat_bitmap_out, 0, (B->n_sets + 7) / 8);
     for (size_t s = 0; s < B->n_sets; s++) {
@@ -397,26 +441,70 @@ int pf_check_batch(uint64_t handle, uint64_t global_seed, uint32_t budget, uint3
             if (sat_bitmap_out) sat_bitmap_out[s / 8] |= (uint8_t)(1u << (s % 8));
         }
     }
-    st->n_sat = nsat;
+    if (stats) stats->n_sat = nsat;
+    return 0;
+}
+
+int pf_check_batch(uint64_t handle, uint64_t global_seed, uint32_t budget, uint32_t flags,
+                   uint32_t timeout_ms, uint32_t* found_out, uint8_t* sat_bitmap_out,
+                   pf_stats* stats) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    Batch* B = as_batch(handle);
+    if (!B) return fail("pf_check_batch: null batch");
+    Dev* D = use_dev(B->device);
+    if (!D || switch_stream(D, D->stream)) return -1;
+    if (check_enqueue(B, global_seed, budget, flags, timeout_ms, B->d_found, D->stream)) return -1;
+    if (check_collect(B, D->stream, stats)) return -1;
+    return found_to_host(B, D->stream, found_out, sat_bitmap_out, stats);
+}
+
+int pf_check_batches(const uint64_t* handles, size_t n, uint64_t global_seed, uint32_t budget,
+                     uint32_t flags, uint32_t timeout_ms, uint32_t* found_out, pf_stats* stats) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    // 1. enqueue every batch's search on its device's stream: devices run concurrently
+    for (size_t i = 0; i < n; ++i) {
+        Batch* B = as_batch(handles[i]);
+        if (!B) return fail("pf_check_batches: null batch %zu", i);
+        Dev* D = use_dev(B->device);
+        if (!D || switch_stream(D, D->stream)) return -1;
+        if (check_enqueue(B, global_seed, budget, flags, timeout_ms, B->d_found, D->stream)) return -1;
+    }
+    // 2. gather: verdicts concatenated in handle order
+    size_t off = 0;
+    for (size_t i = 0; i < n; ++i) {
+        Batch* B = as_batch(handles[i]);
+        Dev* D = use_dev(B->device);
+        if (!D) return -1;
+        pf_stats* st = stats ? stats + i : nullptr;
+        if (check_collect(B, D->stream, st)) return -1;
+        if (found_to_host(B, D->stream, found_out ? found_out + off : nullptr, nullptr, st)) return -1;
+        off += B->n_sets;
+    }
     return 0;
 }
 
 int pf_check_batch_dev(uint64_t handle, uint64_t global_seed, uint32_t budget, uint32_t flags,
                        uint32_t timeout_ms, uint32_t* d_found, pf_stats* stats, void* stream) {
     std::lock_guard<std::mutex> lk(g_mu);
-    if (ensure_init_locked()) return -1;
     Batch* B = as_batch(handle);
     if (!B) return fail("pf_check_batch_dev: null batch");
     if (!d_found) return fail("pf_check_batch_dev: null d_found");
-    return check_launch(B, global_seed, budget, flags, timeout_ms, d_found, stats, pick_stream(stream));
+    Dev* D = use_dev(B->device);
+    if (!D) return -1;
+    hipStream_t st = pick_stream(D, stream);
+    if (switch_stream(D, st)) return -1;
+    if (check_enqueue(B, global_seed, budget, flags, timeout_ms, d_found, st)) return -1;
+    return stats ? check_collect(B, st, stats) : 0;
 }
 
 int pf_materialize(uint64_t handle, uint64_t global_seed, const uint32_t* set_ids,
                    const uint32_t* cand_ids, size_t n, uint32_t* values_out) {
     std::lock_guard<std::mutex> lk(g_mu);
-    if (ensure_init_locked()) return -1;
     Batch* B = as_batch(handle);
     if (!B) return fail("pf_materialize: null batch");
+    Dev* D = use_dev(B->device);
+    if (!D) return -1;
+    hipStream_t st = D->stream;
     if (n == 0) return 0;
     std::vector<uint32_t> off(n);
     uint64_t total = 0;
@@ -426,7 +514,7 @@ int pf_materialize(uint64_t handle, uint64_t global_seed, const uint32_t* set_id
         total += B->h_descs[set_ids[i]].n_vars;
     }
     if (total == 0) return 0;
-    if (switch_stream(g_stream)) return -1;
+    if (switch_stream(D, st)) return -1;
     DevBuf b_sets, b_cands, b_off, b_out;
     HIPCHK(hipMalloc(&b_sets.p, n * 4));
     HIPCHK(hipMalloc(&b_cands.p, n * 4));
@@ -434,17 +522,17 @@ int pf_materialize(uint64_t handle, uint64_t global_seed, const uint32_t* set_id
     HIPCHK(hipMalloc(&b_out.p, total * 32));
     uint32_t *d_sets = b_sets.as<uint32_t>(), *d_cands = b_cands.as<uint32_t>(),
              *d_off = b_off.as<uint32_t>(), *d_out = b_out.as<uint32_t>();
-    HIPCHK(hipMemcpyAsync(d_sets, set_ids, n * 4, hipMemcpyHostToDevice, g_stream));
-    HIPCHK(hipMemcpyAsync(d_cands, cand_ids, n * 4, hipMemcpyHostToDevice, g_stream));
-    HIPCHK(hipMemcpyAsync(d_off, off.data(), n * 4, hipMemcpyHostToDevice, g_stream));
+    HIPCHK(hipMemcpyAsync(d_sets, set_ids, n * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_cands, cand_ids, n * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_off, off.data(), n * 4, hipMemcpyHostToDevice, st));
     const uint32_t mv = std::max<uint32_t>(B->max_vars, 1u);
     const uint64_t threads = (uint64_t)n * mv;
     hipLaunchKernelGGL(pf_materialize_kernel, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0,
-                       g_stream, B->d_descs, B->d_code, B->d_consts, B->d_schema, B->d_parents,
+                       st, B->d_descs, B->d_code, B->d_consts, B->d_schema, B->d_parents,
                        global_seed, d_sets, d_cands, d_off, (uint32_t)n, mv, d_out);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(values_out, d_out, total * 32, hipMemcpyDeviceToHost, g_stream));
-    HIPCHK(hipStreamSynchronize(g_stream));
+    HIPCHK(hipMemcpyAsync(values_out, d_out, total * 32, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
     return 0;
 }
 
@@ -461,68 +549,74 @@ static int eval_launch(Batch* B, uint32_t set, const uint32_t* d_soa, uint32_t n
 int pf_eval_assignments(uint64_t handle, uint32_t set, const uint32_t* soa, uint32_t n_cand,
                         uint8_t* sat_out) {
     std::lock_guard<std::mutex> lk(g_mu);
-    if (ensure_init_locked()) return -1;
     Batch* B = as_batch(handle);
     if (!B) return fail("pf_eval_assignments: null batch");
+    Dev* D = use_dev(B->device);
+    if (!D) return -1;
+    hipStream_t st = D->stream;
     if (set >= B->n_sets) return fail("eval: set %u out of range", set);
     if (n_cand == 0) return 0;
     const size_t nv = std::max<uint32_t>(B->h_descs[set].n_vars, 1u);
     const size_t bytes = nv * 8 * (size_t)n_cand * 4;
-    if (switch_stream(g_stream)) return -1;
+    if (switch_stream(D, st)) return -1;
     DevBuf b_soa, b_out;
     HIPCHK(hipMalloc(&b_soa.p, bytes));
     HIPCHK(hipMalloc(&b_out.p, n_cand));
     uint32_t* d_soa = b_soa.as<uint32_t>();
     uint8_t* d_out = b_out.as<uint8_t>();
-    HIPCHK(hipMemcpyAsync(d_soa, soa, bytes, hipMemcpyHostToDevice, g_stream));
-    if (eval_launch(B, set, d_soa, n_cand, d_out, g_stream)) return -1;
-    HIPCHK(hipMemcpyAsync(sat_out, d_out, n_cand, hipMemcpyDeviceToHost, g_stream));
-    HIPCHK(hipStreamSynchronize(g_stream));
+    HIPCHK(hipMemcpyAsync(d_soa, soa, bytes, hipMemcpyHostToDevice, st));
+    if (eval_launch(B, set, d_soa, n_cand, d_out, st)) return -1;
+    HIPCHK(hipMemcpyAsync(sat_out, d_out, n_cand, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
     return 0;
 }
 
 int pf_eval_assignments_dev(uint64_t handle, uint32_t set, const uint32_t* d_soa,
                             uint32_t n_cand, uint8_t* d_sat_out, void* stream) {
     std::lock_guard<std::mutex> lk(g_mu);
-    if (ensure_init_locked()) return -1;
     Batch* B = as_batch(handle);
     if (!B) return fail("pf_eval_assignments_dev: null batch");
-    if (switch_stream(pick_stream(stream))) return -1;
-    return eval_launch(B, set, d_soa, n_cand, d_sat_out, pick_stream(stream));
+    Dev* D = use_dev(B->device);
+    if (!D) return -1;
+    if (switch_stream(D, pick_stream(D, stream))) return -1;
+    return eval_launch(B, set, d_soa, n_cand, d_sat_out, pick_stream(D, stream));
 }
 
 int pf_keccak256_batch(const uint8_t* data, const uint64_t* offsets, size_t n, uint8_t* out32) {
     std::lock_guard<std::mutex> lk(g_mu);
-    if (ensure_init_locked()) return -1;
+    Dev* D = use_dev(-1);
+    if (!D) return -1;
+    hipStream_t st = D->stream;
     if (n == 0) return 0;
     for (size_t i = 0; i < n; i++)
         if (offsets[i + 1] < offsets[i]) return fail("keccak: offsets not monotone at %zu", i);
     const uint64_t total = offsets[n];
-    if (switch_stream(g_stream)) return -1;
+    if (switch_stream(D, st)) return -1;
     DevBuf b_data, b_off, b_out;
     HIPCHK(hipMalloc(&b_data.p, total ? total : 8));
     HIPCHK(hipMalloc(&b_off.p, (n + 1) * 8));
     HIPCHK(hipMalloc(&b_out.p, n * 32));
     uint8_t *d_data = b_data.as<uint8_t>(), *d_out = b_out.as<uint8_t>();
     uint64_t* d_off = b_off.as<uint64_t>();
-    if (total) HIPCHK(hipMemcpyAsync(d_data, data, total, hipMemcpyHostToDevice, g_stream));
-    HIPCHK(hipMemcpyAsync(d_off, offsets, (n + 1) * 8, hipMemcpyHostToDevice, g_stream));
-    hipLaunchKernelGGL(pf_keccak_var_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, g_stream,
+    if (total) HIPCHK(hipMemcpyAsync(d_data, data, total, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_off, offsets, (n + 1) * 8, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(pf_keccak_var_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st,
                        d_data, d_off, (uint64_t)n, d_out);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(out32, d_out, n * 32, hipMemcpyDeviceToHost, g_stream));
-    HIPCHK(hipStreamSynchronize(g_stream));
+    HIPCHK(hipMemcpyAsync(out32, d_out, n * 32, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
     return 0;
 }
 
 int pf_keccak256_fixed_dev(const uint8_t* d_data, uint32_t len, size_t n, uint8_t* d_out32,
                            float* kernel_ms, void* stream) {
     std::lock_guard<std::mutex> lk(g_mu);
-    if (ensure_init_locked()) return -1;
+    Dev* D = use_dev(-1);
+    if (!D) return -1;
     if (n == 0) return 0;
-    hipStream_t st = pick_stream(stream);
-    if (switch_stream(st)) return -1;
-    HIPCHK(hipEventRecord(g_ev0, st));
+    hipStream_t st = pick_stream(D, stream);
+    if (switch_stream(D, st)) return -1;
+    HIPCHK(hipEventRecord(D->ev0, st));
     const bool fast = (len % 16u) == 0u && len < 136u && (((uintptr_t)d_data) & 15u) == 0u;
     if (fast)
         hipLaunchKernelGGL(pf_keccak_fixed_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0,
@@ -531,10 +625,10 @@ int pf_keccak256_fixed_dev(const uint8_t* d_data, uint32_t len, size_t n, uint8_
         hipLaunchKernelGGL(pf_keccak_stride_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256),
                            0, st, d_data, len, (uint64_t)n, d_out32);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(g_ev1, st));
+    HIPCHK(hipEventRecord(D->ev1, st));
     if (kernel_ms) {
-        HIPCHK(hipEventSynchronize(g_ev1));
-        HIPCHK(hipEventElapsedTime(kernel_ms, g_ev0, g_ev1));
+        HIPCHK(hipEventSynchronize(D->ev1));
+        HIPCHK(hipEventElapsedTime(kernel_ms, D->ev0, D->ev1));
     }
     return 0;
 }

@@ -69,7 +69,7 @@ def sharded_check(programs, search_fn: Optional[Callable] = None, budget: int = 
     import torch.distributed as dist
 
     rank, world = dist.get_rank(group), dist.get_world_size(group)
-    costs = [len(p.code) for p in programs]
+    costs = [p.sched_cost() for p in programs]
     lo, hi = shard_bounds(costs, world)[rank]
     if search_fn is None:
         from .engine import get_engine

@@ -39,24 +39,26 @@ class CheckResult:
 
 
 class DeviceBatch:
-    """A :class:`~mythril_amd.ir.Batch` resident in HBM (pf_batch_create)."""
+    """A :class:`~mythril_amd.ir.Batch` resident in one device's HBM (pf_batch_create_on)."""
 
-    def __init__(self, batch: Batch):
+    def __init__(self, batch: Batch, device: int = -1):
         L = _lib.lib()
         self.batch = batch
+        self.device = device
         h = ctypes.c_uint64(0)
         descs = np.ascontiguousarray(batch.descs, dtype=np.uint32)
         code = np.ascontiguousarray(batch.code, dtype=np.uint32)
         consts = np.ascontiguousarray(batch.consts, dtype=np.uint32)
         schema = np.ascontiguousarray(batch.schema, dtype=np.uint32)
         parents = np.ascontiguousarray(batch.parents, dtype=np.uint32)
-        _lib.check(L.pf_batch_create(
+        _lib.check(L.pf_batch_create_on(
+            device,
             _lib.ptr_u32(code.reshape(-1)) if code.size else None, code.shape[0],
             _lib.ptr_u32(consts.reshape(-1)) if consts.size else None, consts.shape[0],
             _lib.ptr_u32(schema.reshape(-1)) if schema.size else None, schema.shape[0],
             _lib.ptr_u32(parents.reshape(-1)) if parents.size else None, parents.shape[0],
             _lib.ptr_u32(descs.reshape(-1)) if descs.size else None, descs.shape[0],
-            ctypes.byref(h)), "pf_batch_create")
+            ctypes.byref(h)), "pf_batch_create_on")
         self.handle = h.value
 
     def __len__(self):
@@ -75,16 +77,18 @@ class DeviceBatch:
 
 
 class Engine:
-    """The per-process engine: one GPU, one library stream."""
+    """The per-process engine: one GPU (one process per GPU) or several GPUs driven by one
+    process (``devices``), one library stream per device."""
 
-    def __init__(self, device: int = 0):
-        _lib.init(device)
-        self.device = device
+    def __init__(self, device: int = 0, devices: Optional[Sequence[int]] = None):
+        self.devices = list(devices) if devices is not None else [device]
+        _lib.init(self.devices)
+        self.device = self.devices[0]
 
     # ---- search -------------------------------------------------------------------
-    def upload(self, programs: Sequence[Program] | Batch) -> DeviceBatch:
+    def upload(self, programs: Sequence[Program] | Batch, device: Optional[int] = None) -> DeviceBatch:
         batch = programs if isinstance(programs, Batch) else Batch(programs)
-        return DeviceBatch(batch)
+        return DeviceBatch(batch, self.device if device is None else device)
 
     def check(self, db: DeviceBatch, budget: int = 65536, seed: int = 0, flags: int = 2,
               timeout_ms: int = 0) -> CheckResult:
@@ -96,6 +100,39 @@ class Engine:
                    "pf_check_batch")
         return CheckResult(found[:n], st.evals_full, st.cands_decided, st.ops, st.kernel_ms,
                            bool(st.timed_out))
+
+    def upload_sharded(self, programs: Sequence[Program]) -> List[DeviceBatch]:
+        """Size-balanced contiguous shards, one per device (mythril_amd.dist.shard_bounds
+        over the bytecode cost model), each uploaded to its device."""
+        from .dist import shard_bounds
+
+        progs = list(programs)
+        nd = len(self.devices)
+        if nd == 1 or len(progs) < 2:
+            return [self.upload(progs)]
+        out = []
+        for (lo, hi), d in zip(shard_bounds([p.sched_cost() for p in progs], nd), self.devices):
+            if hi > lo:
+                out.append(self.upload(progs[lo:hi], device=d))
+        return out
+
+    def check_many(self, dbs: Sequence[DeviceBatch], budget: int = 65536, seed: int = 0,
+                   flags: int = 2, timeout_ms: int = 0) -> CheckResult:
+        """One search over several device batches at once (pf_check_batches: every device
+        launches before any result is read); verdicts concatenated in batch order, the
+        kernel time is the slowest device's."""
+        if len(dbs) == 1:
+            return self.check(dbs[0], budget, seed, flags, timeout_ms)
+        n = sum(len(db) for db in dbs)
+        found = np.full(max(n, 1), NOT_FOUND, dtype=np.uint32)
+        stats = (_lib.pf_stats * len(dbs))()
+        handles = np.array([db.handle for db in dbs], dtype=np.uint64)
+        _lib.check(_lib.lib().pf_check_batches(_lib.ptr_u64(handles), len(dbs), seed, budget, flags,
+                                              timeout_ms, _lib.ptr_u32(found), stats),
+                   "pf_check_batches")
+        return CheckResult(found[:n], sum(s.evals_full for s in stats),
+                           sum(s.cands_decided for s in stats), sum(s.ops for s in stats),
+                           max(s.kernel_ms for s in stats), any(s.timed_out for s in stats))
 
     def materialize(self, db: DeviceBatch, set_ids: Sequence[int], cand_ids: Sequence[int],
                     seed: int = 0) -> List[List[int]]:
@@ -143,9 +180,20 @@ _engine: Optional[Engine] = None
 
 
 def get_engine(device: Optional[int] = None) -> Engine:
+    """The process's engine.  Device selection: an explicit ``device``; else ``PF_DEVICES``
+    (comma-separated indices, or ``all``: one process driving every visible GPU — the live
+    analysis, which Mythril runs as one process); else ``LOCAL_RANK`` (one process per GPU)."""
     global _engine
     if _engine is None:
         import os
-        dev = device if device is not None else int(os.environ.get("LOCAL_RANK", "0"))
-        _engine = Engine(dev)
+        if device is not None:
+            _engine = Engine(device)
+        else:
+            spec = os.environ.get("PF_DEVICES", "").strip()
+            if spec == "all":
+                _engine = Engine(devices=list(range(_lib.lib().pf_device_count())))
+            elif spec:
+                _engine = Engine(devices=[int(x) for x in spec.split(",")])
+            else:
+                _engine = Engine(int(os.environ.get("LOCAL_RANK", "0")))
     return _engine

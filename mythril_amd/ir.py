@@ -242,6 +242,16 @@ class Program:
     def reach_cost(self) -> int:
         return sum(reach_cost(i.op, i.width) for i in self.code)
 
+    def sched_cost(self) -> int:
+        """Relative device time of one candidate evaluation: measured SIMD cycles per
+        instruction (EXP ~11x, division ~4x, MUL ~1.2x a cheap op) — the model
+        pf_batch_create orders waves by, used here to balance shards across devices."""
+        c = 0
+        for i in self.code:
+            c += (110 if i.op == W_EXP else 12 if i.op == W_MUL
+                  else 40 if (W_UDIV <= i.op <= W_SMOD or i.op == B_UMUL_NOOVF) else 10)
+        return c
+
     def validate(self) -> None:
         """Host-side shape check run before anything is launched (kernel assumes these)."""
         spilled = set()

@@ -222,11 +222,26 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
     res = None
     if progs:
         eng = get_engine()
-        db = eng.upload(progs)
-        res = eng.check(db, budget=cfg.budget, seed=cfg.seed, flags=cfg.flags, timeout_ms=cfg.timeout_ms)
+        # one batch per device of the engine (cost-balanced shards), searched concurrently
+        dbs = eng.upload_sharded(progs) if hasattr(eng, "upload_sharded") else [eng.upload(progs)]
+        if len(dbs) == 1:
+            res = eng.check(dbs[0], budget=cfg.budget, seed=cfg.seed, flags=cfg.flags,
+                            timeout_ms=cfg.timeout_ms)
+        else:
+            res = eng.check_many(dbs, budget=cfg.budget, seed=cfg.seed, flags=cfg.flags,
+                                 timeout_ms=cfg.timeout_ms)
         sat = [k for k in range(len(progs)) if res.found[k] != 0xFFFFFFFF]
-        vals = eng.materialize(db, sat, [int(res.found[k]) for k in sat], seed=cfg.seed) if sat else []
-        db.free()
+        vals_of = {}
+        base = 0
+        for db in dbs:
+            mine = [k for k in sat if base <= k < base + len(db)]
+            if mine:
+                got = eng.materialize(db, [k - base for k in mine], [int(res.found[k]) for k in mine],
+                                      seed=cfg.seed)
+                vals_of.update(zip(mine, got))
+            base += len(db)
+            db.free()
+        vals = [vals_of[k] for k in sat]
         for k in range(len(progs)):
             found[keys[k]] = None
         if not res.timed_out:  # a deadline-cut search is not a complete answer

@@ -1,0 +1,121 @@
+"""One process driving several GPUs (SURVEY §8e partitioning for the live analysis: Mythril is
+one process, so a tx-boundary batch is split across the node's devices inside
+libpathfeas.so — pf_init(device_mask), pf_batch_create_on, pf_check_batches).
+
+CPU: the size-balanced split and the gather logic of Engine.upload_sharded / check_many and
+of gpu_check.check_sets on a stand-in engine with several "devices" (the C oracle per shard)
+give exactly the single-device verdicts and witnesses.
+GPU: on the one visible device, a one-bit mask engine and two batches searched through
+pf_check_batches give identical results to the single-batch path.
+"""
+
+import numpy as np
+import pytest
+
+import oracle_engine
+from mythril_amd import engine as E
+from mythril_amd import ir, synth
+from mythril_amd.dist import shard_bounds
+from mythril_amd.smt import gpu_check
+
+
+def _progs(n, first=0, plant=True):
+    return [synth.random_dag_set(first + i, plant=plant)[0] for i in range(n)]
+
+
+def test_shards_balance_the_cost_model():
+    progs = _progs(24)
+    costs = [p.sched_cost() for p in progs]
+    b = shard_bounds(costs, 4)
+    assert b[0][0] == 0 and b[-1][1] == len(progs)
+    assert all(b[i][1] == b[i + 1][0] for i in range(3))
+    loads = [sum(costs[lo:hi]) for lo, hi in b]
+    assert max(loads) - min(loads) <= max(costs) + 1
+
+
+class _MultiOracle(oracle_engine.OracleEngine):
+    """The oracle engine with n "devices": upload_sharded / check_many follow Engine's code."""
+
+    def __init__(self, n):
+        super().__init__()
+        self.devices = list(range(n))
+        self.device = 0
+        self.uploads = []
+
+    def upload(self, programs, device=None):
+        db = super().upload(programs)
+        db.device = self.device if device is None else device
+        self.uploads.append((db.device, len(db)))
+        return db
+
+    upload_sharded = E.Engine.upload_sharded
+
+    def check_many(self, dbs, budget=65536, seed=0, flags=2, timeout_ms=0):
+        rs = [self.check(db, budget, seed, flags, timeout_ms) for db in dbs]
+        return E.CheckResult(np.concatenate([r.found for r in rs]), 0, 0, 0, 0.0, False)
+
+
+def test_check_sets_sharded_equals_single(monkeypatch):
+    """The same constraint sets through check_sets on 1 and on 3 stand-in devices: identical
+    verdicts and witness values; each device got one contiguous shard."""
+    import pyoracle as O
+    from mythril_amd import corpus
+    from mythril_amd import keccak_manager as KM
+    from mythril_amd.smt import symbol_factory
+
+    # concrete hashes from the oracle's Keccak (the product computes them on the GPU)
+    monkeypatch.setattr(KM.KeccakFunctionManager, "find_concrete_keccak", staticmethod(
+        lambda data: symbol_factory.BitVecVal(
+            int.from_bytes(O.keccak256(data.value.to_bytes(data.size() // 8, "big")), "big"), 256)))
+    c = corpus.build(6, 2, seed=7)
+    sets = [q.constraints for q in c.queries][:60]
+    results = {}
+    for n in (1, 3):
+        eng = _MultiOracle(n)
+        monkeypatch.setattr(E, "get_engine", lambda device=None, eng=eng: eng)
+        monkeypatch.setattr(gpu_check.CONFIG, "workers", 1)
+        monkeypatch.setattr(gpu_check.CONFIG, "budget", 2048)
+        gpu_check.reset_cache()
+        ms = gpu_check.check_sets(sets, registry=c.kfm.registry)
+        results[n] = [None if m is None else sorted(m.w.vars.items()) for m in ms]
+        if n == 3:
+            assert sorted(d for d, _ in eng.uploads) == [0, 1, 2]
+    assert results[1] == results[3]
+    assert any(r is not None for r in results[1])
+    gpu_check.reset_cache()
+
+
+def test_device_spec_from_environment(monkeypatch):
+    seen = {}
+
+    class _E:
+        def __init__(self, device=0, devices=None):
+            seen["devices"] = devices if devices is not None else [device]
+
+    monkeypatch.setattr(E, "Engine", _E)
+    monkeypatch.setattr(E, "_engine", None)
+    monkeypatch.setenv("PF_DEVICES", "0,2,5")
+    E.get_engine()
+    assert seen["devices"] == [0, 2, 5]
+    monkeypatch.setattr(E, "_engine", None)
+    monkeypatch.delenv("PF_DEVICES")
+    monkeypatch.setenv("LOCAL_RANK", "3")
+    E.get_engine()
+    assert seen["devices"] == [3]
+    monkeypatch.setattr(E, "_engine", None)
+
+
+@pytest.mark.gpu
+def test_gpu_mask_engine_and_check_many(engine):
+    """A one-bit device-mask engine (the visible GPU) and pf_check_batches over two batches
+    on it reproduce the single-batch verdicts exactly."""
+    progs = _progs(96, first=500, plant=False)
+    eng = E.Engine(devices=[0])
+    whole = eng.upload(progs)
+    r1 = eng.check(whole, budget=4096, seed=0, flags=ir.FLAG_EARLY_EXIT | ir.FLAG_SHORTCIRCUIT)
+    a, b = eng.upload(progs[:40], device=0), eng.upload(progs[40:], device=0)
+    r2 = eng.check_many([a, b], budget=4096, seed=0, flags=ir.FLAG_EARLY_EXIT | ir.FLAG_SHORTCIRCUIT)
+    assert np.array_equal(r1.found, r2.found)
+    assert r2.cands_decided > 0
+    for db in (whole, a, b):
+        db.free()

@@ -175,6 +175,9 @@ def test_check_sets_caches_witnessless_buckets(monkeypatch):
         def __init__(self, n):
             self.n = n
 
+        def __len__(self):
+            return self.n
+
         def free(self):
             pass
 
@@ -230,6 +233,9 @@ def test_parallel_lowering_matches_sequential(monkeypatch):
     class _DB:
         def __init__(self, n):
             self.n = n
+
+        def __len__(self):
+            return self.n
 
         def free(self):
             pass

@@ -34,7 +34,7 @@ def run(args):
     from mythril_amd import _lib, ir, synth
 
     L = _lib.load_library(PROF_SO)
-    L.pf_prof_read.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
+    L.pf_prof_read.argtypes = [ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]
     L.pf_prof_read.restype = ctypes.c_int
     from mythril_amd.engine import Engine
 
@@ -48,7 +48,7 @@ def run(args):
     eng.check(db, budget=args.budget, seed=1, flags=ir.FLAG_COUNT_OPS)  # warm
     r = eng.check(db, budget=args.budget, seed=1, flags=ir.FLAG_COUNT_OPS)
     out = (ctypes.c_uint64 * 11)()
-    _lib.check(L.pf_prof_read(out), "pf_prof_read")
+    _lib.check(L.pf_prof_read(db.handle, out), "pf_prof_read")
     tot_ins = sum(out[:10])
     wave = out[10]
     res = {"kernel_ms": r.kernel_ms, "wave_cycles": wave, "instr_cycles": tot_ins,
