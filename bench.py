@@ -84,13 +84,23 @@ def cpu_baseline(programs, budget, seed, target_s):
 
 
 def discharge(args):
-    """The metric's second half: % of objective-free feasibility queries answered on the GPU.
+    """The metric's second half, measured on the builder's LASER-shaped corpus — NOT the
+    BASELINE population (z3 queries of ``myth analyze solidity_examples -t 3``, which needs
+    z3 + solc, absent here): % of objective-free feasibility queries answered on the GPU.
 
     Queries: mythril_amd/corpus.py — LASER-shaped sets (both successors of every JUMPI fork
     and every tx-boundary state, svm.py:266-286,351-358) along planted 2-transaction
     scenarios over token / BECToken / EtherStore / Rubixi / KillBilly / WalletLibrary
     logic; the planted side of each fork is SAT by construction, the other side is open
-    (z3 would decide it).  All queries go through the drop-in batched funnel in one call."""
+    (z3 would decide it).  All queries go through the drop-in batched funnel in one call.
+    Reported beside the rate:
+    * provenance of the witnesses: ``hint_only`` (every bucket answered by candidate 0, the
+      host's constraint-directed hint model) vs ``searched`` (a bucket's witness came from
+      the GPU candidate search);
+    * a labelled-UNSAT slice (the reference's UNSAT KATs + planted contradictions,
+      corpus.labelled_unsat): ``unsat_labelled_false_positives`` must be 0;
+    * ``single_query_ms``: cold latency of one query through check_sets (lowering + one
+      launch + re-check), the live fork-prune path, beside the batched throughput."""
     from mythril_amd import corpus
     from mythril_amd.smt import gpu_check
 
@@ -105,13 +115,39 @@ def discharge(args):
     got = [m is not None for m in models]
     planted_hit = sum(1 for g, q in zip(got, c.queries) if g and q.label == "sat")
     n = len(c.queries)
-    return {"queries": n, "planted_sat": n_planted, "gpu_sat": sum(got),
+    kinds = [m.origin for m in models if m is not None]
+    stats_batch = (gpu_check.STATS.buckets - s0[1], gpu_check.STATS.kernel_ms - s0[0],
+                   gpu_check.STATS.host_s - s0[2])
+    # soundness slice: UNSAT by construction, never answered sat
+    unsat = corpus.labelled_unsat(c, n=256)
+    fps = []
+    for reg in {id(r): r for _, _, r in unsat}.values():
+        group = [(cs, o) for cs, o, r in unsat if r is reg]
+        ms = gpu_check.check_sets([cs for cs, _ in group], registry=reg)
+        fps += [o for (cs, o), m in zip(group, ms) if m is not None]
+    # cold single-query latency (the fork-prune call site answers one query at a time)
+    sample = [q for q in c.queries if q.label == "sat"][:24]
+    lat = []
+    for q in sample:
+        gpu_check.reset_cache()
+        ts = time.perf_counter()
+        gpu_check.check_sets([q.constraints], registry=c.kfm.registry)
+        lat.append(1e3 * (time.perf_counter() - ts))
+    gpu_check.reset_cache()
+    return {"population": "builder corpus (mythril_amd/corpus.py), not BASELINE's "
+                          "solidity_examples -t 3 z3 queries (needs z3 + solc)",
+            "queries": n, "planted_sat": n_planted, "gpu_sat": sum(got),
             "gpu_sat_planted": planted_hit,
-            "pct_discharged": 100.0 * sum(got) / max(n, 1),
+            "pct_discharged_builder_corpus": 100.0 * sum(got) / max(n, 1),
             "pct_planted_discharged": 100.0 * planted_hit / max(n_planted, 1),
-            "buckets_searched": gpu_check.STATS.buckets - s0[1],
-            "kernel_ms": gpu_check.STATS.kernel_ms - s0[0],
-            "host_s": gpu_check.STATS.host_s - s0[2], "wall_s": t2 - t1, "corpus_build_s": t1 - t0,
+            "hint_only": kinds.count("hint"), "searched": kinds.count("search"),
+            "from_cache": kinds.count("cache"),
+            "unsat_labelled": len(unsat), "unsat_labelled_false_positives": len(fps),
+            "false_positive_origins": fps[:5],
+            "single_query_ms": {"median": float(np.median(lat)) if lat else None,
+                                "mean": float(np.mean(lat)) if lat else None, "queries": len(lat)},
+            "buckets_searched": stats_batch[0], "kernel_ms": stats_batch[1], "host_s": stats_batch[2],
+            "wall_s": t2 - t1, "corpus_build_s": t1 - t0,
             "queries_per_s": n / max(t2 - t1, 1e-9),
             "corpus": f"mythril_amd/corpus.py, {args.corpus_scenarios} planted 2-tx scenarios "
                       f"(config-2 substitute: no z3/solc for --solver-log dumps)"}

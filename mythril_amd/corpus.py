@@ -503,3 +503,100 @@ def validate(corpus: Corpus) -> int:
             raise AssertionError(f"{q.origin}: planted model violates {T.to_sexpr(bad[0])[:200]}")
         n += 1
     return n
+
+
+# ---- queries that are UNSAT by construction (the soundness half of "% discharged") ------
+def _symbol_terms(cs: List[T.Term]) -> List[T.Term]:
+    seen, out, stack = set(), [], list(cs)
+    while stack:
+        t = stack.pop()
+        if t in seen:
+            continue
+        seen.add(t)
+        if t.op == "var":
+            out.append(t)
+        stack.extend(t.args)
+    return sorted(out, key=lambda t: t.val)
+
+
+def _reference_unsat_kats() -> List[Tuple[List[T.Term], str, UFRegistry]]:
+    """The UNSAT labels of the reference's own SMT tests, rebuilt with the facade:
+    tests/laser/keccak_tests.py (keccak equality of different values / widths, a symbol
+    pinned to another value, keccak(keccak(a)*2) collisions with a != b, keccak == 10) and
+    tests/laser/state/calldata_test.py (a read past calldatasize, equal indices with
+    different bytes)."""
+    from .smt import Array, If
+
+    out = []
+
+    def kat(name, build):
+        kfm = KeccakFunctionManager(UFRegistry())
+        cs = build(kfm)
+        out.append(([c.raw if isinstance(c, Bool) else c for c in cs], f"kat:{name}", kfm.registry))
+
+    def basic(i1, i2):
+        def b(kfm):
+            o1, o2 = kfm.create_keccak(i1), kfm.create_keccak(i2)
+            return [kfm.create_conditions(), o1 == o2]
+        return b
+
+    kat("keccak_100_101", basic(BVV(100, 8), BVV(101, 8)))
+    kat("keccak_w8_w16", basic(BVV(100, 8), BVV(100, 16)))
+    kat("keccak_val8_sym256", basic(BVV(100, 8), BV("N1", 256)))
+
+    def sym_and_val(kfm):
+        n = BV("n", 256)
+        o1, o2 = kfm.create_keccak(BVV(100, 256)), kfm.create_keccak(n)
+        return [kfm.create_conditions(), o1 == o2, n == BVV(10, 256)]
+
+    def complex_eq(kfm):
+        a, b = BV("a", 160), BV("b", 160)
+        o1 = kfm.create_keccak(BVV(2, 256) * kfm.create_keccak(a))
+        o2 = kfm.create_keccak(BVV(2, 256) * kfm.create_keccak(b))
+        return [kfm.create_conditions(), o1 == o2, a != b]
+
+    def simple_number(kfm):
+        o = kfm.create_keccak(BV("a", 160))
+        return [kfm.create_conditions(), BVV(10, 256) == o]
+
+    def calldata_past_size(kfm):
+        cd, size = Array("1_calldata", 256, 8), BV("1_calldatasize", 256)
+        read = If(BVV(51, 256) < size, cd[BVV(51, 256)], BVV(0, 8))
+        return [read == BVV(1, 8), size == BVV(50, 256)]
+
+    def calldata_equal_indices(kfm):
+        cd = Array("0_calldata", 256, 8)
+        ia, ib = BV("index_a", 256), BV("index_b", 256)
+        return [ia == ib, cd[ia] != cd[ib]]
+
+    for name, fn in (("keccak_symbol_and_val", sym_and_val), ("keccak_complex_eq", complex_eq),
+                     ("keccak_simple_number", simple_number), ("calldata_past_size", calldata_past_size),
+                     ("calldata_equal_indices", calldata_equal_indices)):
+        kat(name, fn)
+    return out
+
+
+def labelled_unsat(corpus: Corpus, n: int = 256, seed: int = 99) -> List[Tuple[List[T.Term], str, UFRegistry]]:
+    """Queries whose label is UNSAT by construction: the reference's UNSAT KATs plus ``n``
+    planted contradictions over the corpus' SAT queries — half add ``not c`` for one of the
+    query's own conjuncts, half pin one of its symbols to two different values (its planted
+    value and that value + 1, so the hint pass meets a near-miss).  A GPU "sat" on any of
+    them would be a soundness bug."""
+    rng = np.random.default_rng(seed)
+    out = _reference_unsat_kats()
+    sat_qs = [q for q in corpus.queries if q.label == "sat"]
+    for i in range(n if sat_qs else 0):
+        q = sat_qs[int(rng.integers(0, len(sat_qs)))]
+        cs = list(q.constraints)
+        syms = [v for v in _symbol_terms(cs) if v.val in q.planted.vars]
+        if i % 2 == 0 or not syms:
+            c = cs[int(rng.integers(0, len(cs)))]
+            extra = [T.not_(c)]
+            kind = "negated-conjunct"
+        else:
+            v = syms[int(rng.integers(0, len(syms)))]
+            pv = q.planted.vars[v.val]
+            extra = [T.eq(v, T.const(pv, v.width)), T.eq(v, T.const(pv + 1, v.width))]
+            kind = "two-values"
+        out.append((cs + extra, f"contra:{kind}:{q.origin}", corpus.kfm.registry))
+    return out

@@ -171,6 +171,7 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
     found: Dict[tuple, Optional[Tuple[Lowered, List[int]]]] = {}   # bucket key -> witness
     todo: Dict[tuple, int] = {}                                     # bucket key -> program idx
     progs, lows, keys = [], [], []
+    origin: Dict[tuple, str] = {}   # bucket key -> "hint" / "search" (this call's searches)
     n_lowered = hits = 0
     # the keccak interpretation depends on the registry (intervals, concrete hashes): a
     # cached witness is only valid for the registry state it was found under
@@ -254,6 +255,9 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
                     _NEG.popitem(last=False)
         for k, v in zip(sat, vals):
             key = keys[k]
+            # provenance of the witness: candidate 0 of a hinted program is the host's
+            # constraint-directed hint model itself; any other index was found by the search
+            origin[key] = "hint" if (int(res.found[k]) == 0 and progs[k].has_parent) else "search"
             w = Witness(lows[k], v, reg)
             # re-check on the host under the same interpretation before trusting it
             if all(w.ev(c) for c in key[0]):
@@ -274,6 +278,11 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
         cs = [c for c in sets[i] if c is not T.TRUE]
         if all(w.ev(c) for c in cs):
             out[i] = WitnessModel(w, list(sets[i]))
+            # "search" if any bucket's witness came from the search, "hint" if every bucket
+            # was answered by its hint model (candidate 0), "cache" for earlier witnesses
+            kinds = {origin.get(k, "cache") for k in ks}
+            out[i].origin = ("search" if "search" in kinds else
+                             "hint" if kinds == {"hint"} else "cache")
             n_sat += 1
     with _lock:
         STATS.sets += len(sets)
