@@ -109,6 +109,7 @@ def discharge(args):
     n_planted = corpus.validate(c)
     t1 = time.perf_counter()
     gpu_check.reset_cache()
+    gpu_check.STATS.bucket_origin.clear()
     s0 = (gpu_check.STATS.kernel_ms, gpu_check.STATS.buckets, gpu_check.STATS.host_s)
     models = gpu_check.check_sets([q.constraints for q in c.queries], registry=c.kfm.registry)
     t2 = time.perf_counter()
@@ -118,6 +119,7 @@ def discharge(args):
     kinds = [m.origin for m in models if m is not None]
     stats_batch = (gpu_check.STATS.buckets - s0[1], gpu_check.STATS.kernel_ms - s0[0],
                    gpu_check.STATS.host_s - s0[2])
+    bucket_origin = dict(gpu_check.STATS.bucket_origin)
     # soundness slice: UNSAT by construction, never answered sat
     unsat = corpus.labelled_unsat(c, n=256)
     fps = []
@@ -140,8 +142,12 @@ def discharge(args):
             "gpu_sat_planted": planted_hit,
             "pct_discharged_builder_corpus": 100.0 * sum(got) / max(n, 1),
             "pct_planted_discharged": 100.0 * planted_hit / max(n_planted, 1),
+            # per set: "searched" = some bucket's witness is a later GPU candidate (index > 0);
+            # "hint_only" = every bucket answered by candidate 0, at least one of them the
+            # host hint model (the rest: an unhinted bucket's first generated candidate)
             "hint_only": kinds.count("hint"), "searched": kinds.count("search"),
-            "from_cache": kinds.count("cache"),
+            "first_candidate_only": kinds.count("first"), "from_cache": kinds.count("cache"),
+            "bucket_witness_origin": bucket_origin,
             "unsat_labelled": len(unsat), "unsat_labelled_false_positives": len(fps),
             "false_positive_origins": fps[:5],
             "single_query_ms": {"median": float(np.median(lat)) if lat else None,

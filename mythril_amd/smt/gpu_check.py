@@ -62,6 +62,7 @@ class GpuStats:
     buckets: int = 0         # distinct buckets searched on the GPU
     bucket_hits: int = 0     # buckets answered from the witness cache
     lowering_failures: Dict[str, int] = field(default_factory=dict)
+    bucket_origin: Dict[str, int] = field(default_factory=dict)  # witness provenance per bucket
     kernel_ms: float = 0.0
     evals: int = 0
     host_s: float = 0.0      # lowering + hints + witness re-checks
@@ -257,7 +258,8 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
             key = keys[k]
             # provenance of the witness: candidate 0 of a hinted program is the host's
             # constraint-directed hint model itself; any other index was found by the search
-            origin[key] = "hint" if (int(res.found[k]) == 0 and progs[k].has_parent) else "search"
+            idx = int(res.found[k])
+            origin[key] = "search" if idx > 0 else ("hint" if progs[k].has_parent else "first")
             w = Witness(lows[k], v, reg)
             # re-check on the host under the same interpretation before trusting it
             if all(w.ev(c) for c in key[0]):
@@ -278,13 +280,17 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
         cs = [c for c in sets[i] if c is not T.TRUE]
         if all(w.ev(c) for c in cs):
             out[i] = WitnessModel(w, list(sets[i]))
-            # "search" if any bucket's witness came from the search, "hint" if every bucket
-            # was answered by its hint model (candidate 0), "cache" for earlier witnesses
+            # per bucket: "hint" = candidate 0 of a hinted program (the host hint model),
+            # "first" = candidate 0 of an unhinted one (the generator's first candidate),
+            # "search" = a later candidate; the set takes the strongest of its buckets
+            # the set: "search" if some bucket needed a later candidate, else "hint" if a
+            # host hint model answered some bucket, else "first" / "cache"
             kinds = {origin.get(k, "cache") for k in ks}
-            out[i].origin = ("search" if "search" in kinds else
-                             "hint" if kinds == {"hint"} else "cache")
+            out[i].origin = next((c for c in ("search", "hint", "first") if c in kinds), "cache")
             n_sat += 1
     with _lock:
+        for o in origin.values():
+            STATS.bucket_origin[o] = STATS.bucket_origin.get(o, 0) + 1
         STATS.sets += len(sets)
         STATS.lowered += n_lowered
         STATS.sat += n_sat

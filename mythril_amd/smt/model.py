@@ -104,7 +104,7 @@ class WitnessModel:
     def __init__(self, witness: Witness, constraints: List[T.Term]):
         self.w = witness
         self.constraints = constraints
-        self.origin = "search"   # set by check_sets: "hint" / "search" / "cache"
+        self.origin = "search"   # set by check_sets: "hint" / "first" / "search" / "cache"
 
     def decls(self) -> List[Decl]:
         out: List[Decl] = []

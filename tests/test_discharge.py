@@ -41,7 +41,7 @@ def test_labelled_unsat_never_sat_cpu(monkeypatch):
     assert n == len(unsat) and fps == []
     ms = gpu_check.check_sets([q.constraints for q in c.queries], registry=c.kfm.registry)
     kinds = {m.origin for m in ms if m is not None}
-    assert kinds <= {"hint", "search", "cache"} and kinds
+    assert kinds <= {"hint", "first", "search", "cache"} and kinds
     gpu_check.reset_cache()
 
 
