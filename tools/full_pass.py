@@ -1,0 +1,141 @@
+#!/usr/bin/env python3
+"""Config 3 as specified: ONE full pass over the 1,000,000 synthetic DAGs
+(depth 32, MUL/DIV/EXP-heavy mix, dag ids 0..999,999, DAG generator seed 20260101, candidate
+seed 0x4D595448 ^ dag_id), 65,536 candidates each = 6.55e10 constraint-candidate evals.
+
+The DAGs are generated and lowered on the host by a pool of worker processes (chunks of
+`--chunk` DAGs; the engine never sees the host side), each chunk is uploaded and swept
+(early exit off, like bench.py's timed steps) while the workers build the next chunks.
+Reported: total kernel time, wall time, evals/s over the kernel time and over the wall time,
+sets with a witness among the 65,536 candidates, and a planted early-exit pass over the same
+DAG ids (witness attached as the parent model, so every set stops at candidate 0).
+
+    python tools/full_pass.py [--dags 1000000] [--chunk 65536] [--workers 16]
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from concurrent.futures import ProcessPoolExecutor
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def _build(args):
+    """DAGs [first, first+n): packed arrays of the unplanted programs and of the same
+    programs with their planted witness attached as the parent model (identical code)."""
+    import copy
+
+    first, n = args
+    from mythril_amd import ir, synth
+
+    progs, planted = [], []
+    for i in range(n):
+        p, wit = synth.random_dag_set(first + i, plant=False)
+        q = copy.copy(p)
+        q.vars = [copy.copy(v) for v in p.vars]
+        for v, x in zip(q.vars, wit):
+            v.parent = x
+        progs.append(p)
+        planted.append(q)
+    out = []
+    for ps in (progs, planted):
+        b = ir.Batch(ps)
+        out.append((b.code, b.consts, b.schema, b.parents, b.descs))
+    return first, n, out
+
+
+def _arrays_batch(arrs, n):
+    from mythril_amd import ir
+
+    b = ir.Batch.__new__(ir.Batch)
+    b.programs = [None] * n
+    b.code, b.consts, b.schema, b.parents, b.descs = arrs
+    return b
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--dags", type=int, default=1_000_000)
+    ap.add_argument("--chunk", type=int, default=65536)
+    ap.add_argument("--piece", type=int, default=2048, help="DAGs per worker task")
+    ap.add_argument("--workers", type=int, default=16)
+    ap.add_argument("--budget", type=int, default=65536)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+
+    import numpy as np
+
+    from mythril_amd import ir
+    from mythril_amd.engine import Engine
+
+    # the workers are forked before this process touches the GPU
+    pool = ProcessPoolExecutor(args.workers)
+    list(pool.map(_build, [(0, 1)] * args.workers))
+    eng = Engine(0)
+    t_wall = time.perf_counter()
+    res = {"dags": args.dags, "candidates_per_dag": args.budget,
+           "seeds": "DAG generator 20260101 (Philox key (seed << 32) | dag_id), candidate key "
+                    "0x4D595448 ^ dag_id (global seed 0)"}
+    legs = {"full_sweep": (0, 0), "planted_early_exit": (1, ir.FLAG_EARLY_EXIT | ir.FLAG_SHORTCIRCUIT)}
+    acc = {k: dict(kernel_ms=0.0, evals=0, decided=0, sat=0) for k in legs}
+    chunks = 0
+    with pool:
+        tasks = [(f, min(args.piece, args.dags - f)) for f in range(0, args.dags, args.piece)]
+        futs = [pool.submit(_build, t) for t in tasks]
+        pending, n_pending = [], 0
+        for i, fu in enumerate(futs):
+            pending.append(fu.result())
+            n_pending += pending[-1][1]
+            if n_pending < args.chunk and i + 1 < len(futs):
+                continue
+            chunks += 1
+            for leg, (which, flags) in legs.items():
+                codes, consts, schemas, parents, descs = [], [], [], [], []
+                oc = ok = os_ = op = 0
+                for (_, nn, both) in pending:
+                    c, k, s_, p, d = both[which]
+                    d = d.copy()
+                    d[:, 0] += oc
+                    d[:, 2] += ok
+                    d[:, 4] += os_
+                    has = d[:, 7] != ir.NO_PARENT
+                    d[has, 7] += op
+                    codes.append(c); consts.append(k); schemas.append(s_); parents.append(p); descs.append(d)
+                    oc += len(c); ok += len(k); os_ += len(s_); op += len(p)
+                arrs = tuple(np.concatenate(x) for x in (codes, consts, schemas, parents, descs))
+                db = eng.upload(_arrays_batch(arrs, n_pending))
+                r = eng.check(db, budget=args.budget, seed=args.seed, flags=flags)
+                db.free()
+                a = acc[leg]
+                a["kernel_ms"] += r.kernel_ms
+                a["evals"] += r.evals_full
+                a["decided"] += r.cands_decided
+                a["sat"] += int(r.sat.sum())
+                print(json.dumps({"leg": leg, "chunk": chunks, "sets": n_pending,
+                                  "kernel_ms": r.kernel_ms, "sat": int(r.sat.sum())}), flush=True)
+            pending, n_pending = [], 0
+    for leg, a in acc.items():
+        ks = a["kernel_ms"] / 1e3
+        units = a["evals"] if leg == "full_sweep" else a["decided"]
+        res[leg] = {"kernel_s": ks, "chunks": chunks, "evals_full": a["evals"],
+                    "cands_decided": a["decided"], "sets_with_witness": a["sat"],
+                    "evals_per_s_kernel": units / ks if ks else None,
+                    "set_verdicts_per_s_kernel": args.dags / ks if ks else None}
+    res["total_wall_s"] = time.perf_counter() - t_wall
+    res["full_sweep"]["evals_per_s_wall"] = res["full_sweep"]["evals_full"] / res["total_wall_s"]
+    line = json.dumps(res)
+    print(line, flush=True)
+    if args.out:
+        with open(args.out, "w") as f:
+            f.write(line + "\n")
+
+
+if __name__ == "__main__":
+    main()

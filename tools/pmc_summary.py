@@ -16,9 +16,8 @@ import sys
 
 KERNEL = "pf_check_kernel"
 KECCAK = "pf_keccak_fixed_kernel"
-# bench.py --steps 2 --warmup 1 launches the full sweep 3 times, then its early-exit leg twice:
-# the summary covers the full-sweep launches only (the workload the roofline line is quoted on)
-N_FULL = 3
+# pf_check_kernel is the full sweep only (the early-exit legs launch pf_check_early_kernel):
+# every one of its dispatches is the workload the roofline line is quoted on
 
 
 def per_dispatch(path, kernel=KERNEL):
@@ -30,8 +29,7 @@ def per_dispatch(path, kernel=KERNEL):
             continue
         d = agg.setdefault(r["Dispatch_Id"], {})
         d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-    rows = list(agg.values())
-    return rows[:N_FULL] if kernel == KERNEL else rows
+    return list(agg.values())
 
 
 def mean(rows, key):

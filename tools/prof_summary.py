@@ -17,6 +17,19 @@ def summarize(src, out, title):
         for r in c.execute("select name, total_calls, total_duration, average, percentage from top_kernels"):
             lines.append(f"| {r[0]} | {r[1]} | {r[2] / 1e3:.3f} | {r[3] / 1e3:.3f} | {r[4]:.2f} |")
         lines.append("")
+        skip = int(os.environ.get("PROF_SKIP", "0"))
+        if skip:
+            lines.append(f"timed launches only (first {skip} launches of each kernel skipped: warm-up):")
+            lines.append("")
+            lines.append("| kernel | launches | average (ms) | min (ms) | max (ms) |")
+            lines.append("|---|---|---|---|---|")
+            per = {}
+            for r in c.execute("select name, duration from kernels order by start"):
+                per.setdefault(r[0], []).append(r[1] / 1e6)
+            for name, ds in per.items():
+                ds = ds[skip:] if len(ds) > skip else ds
+                lines.append(f"| {name} | {len(ds)} | {sum(ds) / len(ds):.3f} | {min(ds):.3f} | {max(ds):.3f} |")
+            lines.append("")
         lines.append("per-dispatch resources (first dispatch of each kernel):")
         lines.append("")
         lines.append("| kernel | grid_x | wg_x | vgpr | agpr | sgpr | lds | scratch | duration (ms) |")
