@@ -107,6 +107,9 @@ def main():
                     d[:, 4] += os_
                     has = d[:, 7] != ir.NO_PARENT
                     d[has, 7] += op
+                    s_ = s_.copy()   # schema parent slots are absolute parent indices
+                    sp = s_[:, 3] != ir.NO_PARENT
+                    s_[sp, 3] += op
                     codes.append(c); consts.append(k); schemas.append(s_); parents.append(p); descs.append(d)
                     oc += len(c); ok += len(k); os_ += len(s_); op += len(p)
                 arrs = tuple(np.concatenate(x) for x in (codes, consts, schemas, parents, descs))

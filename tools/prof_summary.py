@@ -15,7 +15,7 @@ def summarize(src, out, title):
         lines.append("| kernel | calls | total (ms) | average (ms) | % |")
         lines.append("|---|---|---|---|---|")
         for r in c.execute("select name, total_calls, total_duration, average, percentage from top_kernels"):
-            lines.append(f"| {r[0]} | {r[1]} | {r[2] / 1e3:.3f} | {r[3] / 1e3:.3f} | {r[4]:.2f} |")
+            lines.append(f"| {r[0][:60]} | {r[1]} | {r[2] / 1e3:.3f} | {r[3] / 1e3:.3f} | {r[4]:.2f} |")
         lines.append("")
         skip = int(os.environ.get("PROF_SKIP", "0"))
         if skip:
@@ -28,7 +28,7 @@ def summarize(src, out, title):
                 per.setdefault(r[0], []).append(r[1] / 1e6)
             for name, ds in per.items():
                 ds = ds[skip:] if len(ds) > skip else ds
-                lines.append(f"| {name} | {len(ds)} | {sum(ds) / len(ds):.3f} | {min(ds):.3f} | {max(ds):.3f} |")
+                lines.append(f"| {name[:60]} | {len(ds)} | {sum(ds) / len(ds):.3f} | {min(ds):.3f} | {max(ds):.3f} |")
             lines.append("")
         lines.append("per-dispatch resources (first dispatch of each kernel):")
         lines.append("")
@@ -40,7 +40,7 @@ def summarize(src, out, title):
             if r[0] in seen:
                 continue
             seen.add(r[0])
-            lines.append("| " + " | ".join(str(x) for x in r[:8]) + f" | {r[8] / 1e6:.3f} |")
+            lines.append("| " + " | ".join(str(x)[:60] for x in r[:8]) + f" | {r[8] / 1e6:.3f} |")
         lines.append("")
     os.makedirs(os.path.dirname(out), exist_ok=True)
     with open(out, "w") as f:
