@@ -102,13 +102,9 @@ PF_INL uint64_t mul_wide(uint32_t a, uint32_t m) {
     return r;
 }
 
-#ifndef PF_GEN_ROUNDS
-#define PF_GEN_ROUNDS 10
-#endif
-template <int ROUNDS = 10>
 PF_INL uint4 philox(uint4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
-    for (int i = 0; i < ROUNDS; i++) {
+    for (int i = 0; i < 10; i++) {
         const uint64_t p0 = mul_wide(c.x, PF_PHILOX_M0), p1 = mul_wide(c.z, PF_PHILOX_M1);
         const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
         const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
@@ -135,9 +131,9 @@ struct SetCtx {
 // computed for every lane and selected, so the wave runs one straight sequence instead of
 // walking a lane-divergent if-chain; the per-variable kind stays a (uniform) branch.
 PF_INL u256 gen_var(const SetCtx& S, uint32_t v, uint32_t cand) {
-    const uint4 m = philox<PF_GEN_ROUNDS>(make_uint4(cand, v, 2u, 0u), S.k0, S.k1);
-    const uint4 r0 = philox<PF_GEN_ROUNDS>(make_uint4(cand, v, 0u, 0u), S.k0, S.k1);
-    const uint4 r1 = philox<PF_GEN_ROUNDS>(make_uint4(cand, v, 1u, 0u), S.k0, S.k1);
+    const uint4 m = philox(make_uint4(cand, v, 2u, 0u), S.k0, S.k1);
+    const uint4 r0 = philox(make_uint4(cand, v, 0u, 0u), S.k0, S.k1);
+    const uint4 r1 = philox(make_uint4(cand, v, 1u, 0u), S.k0, S.k1);
     const uint4 sc = S.schema[v];  // uniform -> scalar load
     const uint32_t kind = sc.x & 0xffu, w = (sc.x >> 8) & 0x3ffu;
     const uint32_t hint0 = sc.y, hint1 = sc.z, pslot = sc.w;
@@ -172,11 +168,7 @@ PF_INL u256 gen_var(const SetCtx& S, uint32_t v, uint32_t cand) {
         // constant +-1 arm (sel 9..11): per-lane gather, issued early
         u256 cst = rv;
         if (S.n_const > 0u) {
-#ifdef PF_GEN_UNIFORM_CONST
-            const uint32_t* c = S.consts + (size_t)(__builtin_amdgcn_readfirstlane(m.y) % S.n_const) * 8u;
-#else
             const uint32_t* c = S.consts + (size_t)(m.y % S.n_const) * 8u;
-#endif
 #pragma unroll
             for (int i = 0; i < 8; i++) cst.l[i] = c[i];
             const uint32_t dsel = m.z % 3u;  // +0, +1, -1
