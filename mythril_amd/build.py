@@ -24,6 +24,25 @@ def _stale() -> bool:
     return any(os.path.getmtime(os.path.join(CSRC, s)) > t for s in SOURCES)
 
 
+LOWER_OUT = os.path.join(HERE, "libpflower.so")
+LOWER_SOURCES = ["pf_lower.cpp", os.path.join("..", "..", "include", "pf_lower.h"),
+                 os.path.join("..", "..", "include", "pf_bytecode.h")]
+
+
+def build_lower(force: bool = False, verbose: bool = False) -> str:
+    """libpflower.so: the host-only native lowering (g++, no HIP runtime)."""
+    if not force and os.path.exists(LOWER_OUT) and all(
+            os.path.getmtime(os.path.join(CSRC, s)) <= os.path.getmtime(LOWER_OUT) for s in LOWER_SOURCES):
+        return LOWER_OUT
+    cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-o", LOWER_OUT + ".tmp",
+           os.path.join(CSRC, "pf_lower.cpp")]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True, cwd=CSRC)
+    os.replace(LOWER_OUT + ".tmp", LOWER_OUT)
+    return LOWER_OUT
+
+
 def build_library(force: bool = False, verbose: bool = False) -> str:
     if not force and not _stale():
         return OUT
@@ -36,4 +55,5 @@ def build_library(force: bool = False, verbose: bool = False) -> str:
 
 
 if __name__ == "__main__":
+    print(build_lower(force="--force" in sys.argv, verbose=True))
     print(build_library(force="--force" in sys.argv, verbose=True))

@@ -313,20 +313,53 @@ def _reg_classes(op):
     return (lambda i: ()), (lambda i: ())
 
 
+class PackedProgram(Program):
+    """A Program whose instructions are held packed, 4 x u32 each (the native lowering's
+    output, include/pf_lower.h); ``code`` decodes them into :class:`Ins` on first use."""
+
+    def __init__(self, words: np.ndarray, consts: List[int], vars: List[Var], seed: int = 0,
+                 name: str = ""):
+        self.words = np.ascontiguousarray(words, dtype=np.uint32).reshape(-1, 4)
+        self.consts = consts
+        self.vars = vars
+        self.seed = seed
+        self.name = name
+        self._code: Optional[List[Ins]] = None
+
+    @property
+    def code(self) -> List[Ins]:  # type: ignore[override]
+        if self._code is None:
+            out = []
+            for w0, w1, a0, a1 in self.words.tolist():
+                out.append(Ins(w0 & 0xFF, (w0 >> 8) & 0x3FF, w1 & 0xFF, (w1 >> 8) & 0xFF,
+                               (w1 >> 16) & 0xFF, (w1 >> 24) & 0xFF, a0, a1, (w0 >> 18) & 0x3FFF))
+            self._code = out
+        return self._code
+
+    def __len__(self):
+        return len(self.words)
+
+
 class Batch:
     """Many programs packed into the flat arrays of the C ABI (pf_set_desc et al.)."""
 
     def __init__(self, programs: Sequence[Program]):
         self.programs = list(programs)
         code, consts, schema, parents, descs = [], [], [], [], []
+        packed = []   # (offset in code, words) of natively lowered programs
         for p in self.programs:
-            p.validate()
             d_code = len(code)
-            for ins in p.code:
-                w0, w1, a0, _ = ins.words()
-                # aux1 carries the node's int32-op cost at the kernel's algorithms
-                # (PF_FLAG_COUNT_OPS; reach_cost, so the roofline's achieved <= peak)
-                code.append((w0, w1, a0, reach_cost(ins.op, ins.width) if ins.op != END else 0))
+            if isinstance(p, PackedProgram):
+                # validated by pf_batch_create (ranges, def-before-use, spill slots)
+                packed.append((d_code, p.words))
+                code.extend([None] * len(p.words))
+            else:
+                p.validate()
+                for ins in p.code:
+                    w0, w1, a0, _ = ins.words()
+                    # aux1 carries the node's int32-op cost at the kernel's algorithms
+                    # (PF_FLAG_COUNT_OPS; reach_cost, so the roofline's achieved <= peak)
+                    code.append((w0, w1, a0, reach_cost(ins.op, ins.width) if ins.op != END else 0))
             d_const = len(consts)
             for c in p.consts:
                 consts.append(to_limbs(c))
@@ -340,9 +373,20 @@ class Batch:
                     parents.append(to_limbs(v.parent & mask(v.width)))
                 schema.append((v.kind | (v.width << 8), v.hint0 & 0xFFFFFFFF,
                                v.hint1 & 0xFFFFFFFF, slot))
-            descs.append((d_code, len(p.code), d_const, len(p.consts), d_var, len(p.vars),
+            descs.append((d_code, len(code) - d_code, d_const, len(p.consts), d_var, len(p.vars),
                           p.seed & 0xFFFFFFFF, d_par))
-        self.code = np.asarray(code, dtype=np.uint32).reshape(-1, 4)
+        if packed:
+            arr = np.zeros((len(code), 4), dtype=np.uint32)
+            rows = [i for i, c in enumerate(code) if c is not None]
+            if rows:
+                arr[rows] = np.asarray([code[i] for i in rows], dtype=np.uint32)
+            for off, words in packed:
+                w = words.copy()
+                w[:, 3] = _reach_cost_words(w)
+                arr[off:off + len(w)] = w
+            self.code = arr
+        else:
+            self.code = np.asarray(code, dtype=np.uint32).reshape(-1, 4)
         self.consts = np.asarray(consts, dtype=np.uint32).reshape(-1, LIMBS)
         self.schema = np.asarray(schema, dtype=np.uint32).reshape(-1, 4)
         self.parents = np.asarray(parents, dtype=np.uint32).reshape(-1, LIMBS)
@@ -353,6 +397,23 @@ class Batch:
 
     def node_costs(self) -> np.ndarray:
         return np.array([p.node_cost() for p in self.programs], dtype=np.int64)
+
+
+_REACH_LUT = None
+
+
+def _reach_cost_words(words: np.ndarray) -> np.ndarray:
+    """reach_cost of packed instructions, vectorised: a (op, width) lookup table."""
+    global _REACH_LUT
+    if _REACH_LUT is None:
+        lut = np.zeros((256, 1024), dtype=np.uint32)
+        for op in _COST256_REACH:
+            for w in range(1, MAX_WIDTH + 1):
+                lut[op, w] = reach_cost(op, w)
+        _REACH_LUT = lut
+    op = words[:, 0] & 0xFF
+    w = (words[:, 0] >> 8) & 0x3FF
+    return _REACH_LUT[op, w]
 
 
 def pack_assignments(prog: Program, cands: Sequence[Sequence[int]]) -> np.ndarray:

@@ -263,7 +263,82 @@ _REMAT_MAX = 6     # nodes re-emitted to restore one evicted interior value
 _REMAT_OPCOST = 16  # only cheap ops (compare/ite/logic/extract/concat) are recomputed
 
 
+# ---- native lowering (libpflower.so, include/pf_lower.h) ----------------------------------
+_KIND_CODE = {K_VAR: 200, K_CONST: 201, K_BCONST: 202, K_BVAR: 203}
+_NATIVE = None
+
+
+def _native():
+    """ctypes handle of libpflower.so (host-only C ABI), or False if it is not built."""
+    global _NATIVE
+    if _NATIVE is None:
+        import ctypes
+        import os
+
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpflower.so")
+        if os.environ.get("PF_LOWER_PY") or not os.path.exists(path):
+            _NATIVE = False
+        else:
+            L = ctypes.CDLL(path)
+            u32p, szp = ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_size_t)
+            L.pfl_lower.argtypes = [u32p, ctypes.c_size_t, u32p, ctypes.c_size_t, u32p,
+                                    ctypes.c_size_t, u32p, ctypes.c_size_t, u32p, ctypes.c_size_t,
+                                    szp, u32p, ctypes.c_size_t, szp]
+            L.pfl_lower.restype = ctypes.c_int
+            L.pfl_last_error.restype = ctypes.c_char_p
+            _NATIVE = L
+    return _NATIVE
+
+
 def lower(dag: Dag, seed: int = 0, name: str = "") -> Program:
+    """Register allocation + emission: the native library when built (identical output,
+    tests/test_native_lower.py), else the Python reference :func:`lower_py`."""
+    L = _native()
+    if not L:
+        return lower_py(dag, seed, name)
+    import ctypes
+
+    import numpy as np
+
+    nn = len(dag.nodes)
+    flat: List[int] = []
+    pool: List[int] = []
+    kc = _KIND_CODE
+    for n in dag.nodes:
+        aux = n.aux
+        if n.kind == K_CONST:
+            aux = len(pool)
+            pool.append(n.aux)
+        a = n.args
+        la = len(a)
+        flat += (kc.get(n.kind, n.kind), n.width, la, a[0] if la > 0 else 0, a[1] if la > 1 else 0,
+                 a[2] if la > 2 else 0, aux & 0xFFFFFFFF, 1 if n.is_bool else 0)
+    arr = np.array(flat or [0] * 8, dtype=np.uint32)
+    limbs = lambda vals: np.array([[(v >> (32 * j)) & 0xFFFFFFFF for j in range(8)] for v in vals] or
+                                  [[0] * 8], dtype=np.uint32)
+    pool_a, forced_a = limbs(pool), limbs(dag.forced)
+    roots = np.array(dag.roots or [0], dtype=np.uint32)
+    cap_i = 16 * nn + 64 + 4 * len(dag.roots)
+    code = np.zeros((cap_i, 4), dtype=np.uint32)
+    cap_c = len(pool) + len(dag.forced) + 1
+    consts = np.zeros((cap_c, 8), dtype=np.uint32)
+    ni, nc = ctypes.c_size_t(), ctypes.c_size_t()
+    p = lambda x: x.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))  # noqa: E731
+    rc = L.pfl_lower(p(arr), nn, p(pool_a), len(pool), p(roots), len(dag.roots), p(forced_a),
+                     len(dag.forced), p(code), cap_i, ctypes.byref(ni), p(consts), cap_c,
+                     ctypes.byref(nc))
+    if rc != 0:
+        msg = L.pfl_last_error().decode(errors="replace")
+        if rc == -2:
+            raise LoweringError(msg)
+        raise ValueError(f"pfl_lower failed ({rc}): {msg}")
+    cv = consts[:nc.value].astype(np.uint64)
+    cvals = [sum(int(x) << (32 * j) for j, x in enumerate(row)) for row in cv]
+    return ir.PackedProgram(code[:ni.value].copy(), cvals, list(dag.vars), seed, name)
+
+
+def lower_py(dag: Dag, seed: int = 0, name: str = "") -> Program:
+    """Python reference of the lowering (the native library reproduces it exactly)."""
     prog = Program(vars=list(dag.vars), seed=seed, name=name)
     prog.consts.extend(dag.forced)  # schema hints index these (actor tables, keccak bases)
     events = _emission_order(dag)
@@ -371,7 +446,7 @@ def lower(dag: Dag, seed: int = 0, name: str = "") -> Program:
             (pb if dag.nodes[a].is_bool else pw).add(r)
             regs.append(r)
         # operands whose last use is this node may be reused as destination
-        for a in set(n.args):
+        for a in dict.fromkeys(n.args):   # distinct operands, in argument order
             if next_use(a, t) >= (1 << 30):
                 done(a)
                 (pb if dag.nodes[a].is_bool else pw).discard(regs[n.args.index(a)])
