@@ -127,6 +127,14 @@ def discharge(args):
         group = [(cs, o) for cs, o, r in unsat if r is reg]
         ms = gpu_check.check_sets([cs for cs, _ in group], registry=reg)
         fps += [o for (cs, o), m in zip(group, ms) if m is not None]
+    # the GPU search on its own: the same corpus with the host hint models switched off
+    # (candidate 0 is then just the generator's first candidate)
+    from dataclasses import replace as _replace
+
+    gpu_check.reset_cache()
+    ms_nh = gpu_check.check_sets([q.constraints for q in c.queries], registry=c.kfm.registry,
+                                 config=_replace(gpu_check.CONFIG, hints=False))
+    no_hints = sum(m is not None for m in ms_nh)
     # cold single-query latency (the fork-prune call site answers one query at a time)
     sample = [q for q in c.queries if q.label == "sat"][:24]
     lat = []
@@ -148,6 +156,7 @@ def discharge(args):
             "hint_only": kinds.count("hint"), "searched": kinds.count("search"),
             "first_candidate_only": kinds.count("first"), "from_cache": kinds.count("cache"),
             "bucket_witness_origin": bucket_origin,
+            "pct_discharged_without_hints": 100.0 * no_hints / max(n, 1),
             "unsat_labelled": len(unsat), "unsat_labelled_false_positives": len(fps),
             "false_positive_origins": fps[:5],
             "single_query_ms": {"median": float(np.median(lat)) if lat else None,
