@@ -38,6 +38,15 @@ int pfl_lower(const uint32_t* nodes, size_t n_nodes, const uint32_t* const_pool,
               uint32_t* code_out, size_t cap_ins, size_t* n_ins_out, uint32_t* consts_out,
               size_t cap_const, size_t* n_const_out);
 const char* pfl_last_error(void);
+
+/* Hint model of one DAG (the native form of mythril_amd/seed.py:Seeder.run, identical
+ * values): nodes / const_pool / roots as for pfl_lower; var_widths[n_vars]; soft = the
+ * caller's parent values (n_vars x 8 u32, the bits no constraint fixes).  hints_out gets
+ * n_vars x 8 u32; n_sat_out the number of distinct roots the hint model satisfies.
+ * Returns 0, or -1 on malformed input.                                                  */
+int pfl_hints(const uint32_t* nodes, size_t n_nodes, const uint32_t* const_pool, size_t n_pool,
+              const uint32_t* roots, size_t n_roots, const uint32_t* var_widths, size_t n_vars,
+              const uint32_t* soft, uint32_t* hints_out, int* n_sat_out);
 int pfl_version(void);
 
 #ifdef __cplusplus

@@ -285,9 +285,46 @@ def _native():
                                     ctypes.c_size_t, u32p, ctypes.c_size_t, u32p, ctypes.c_size_t,
                                     szp, u32p, ctypes.c_size_t, szp]
             L.pfl_lower.restype = ctypes.c_int
+            L.pfl_hints.argtypes = [u32p, ctypes.c_size_t, u32p, ctypes.c_size_t, u32p,
+                                    ctypes.c_size_t, u32p, ctypes.c_size_t, u32p, u32p,
+                                    ctypes.POINTER(ctypes.c_int)]
+            L.pfl_hints.restype = ctypes.c_int
             L.pfl_last_error.restype = ctypes.c_char_p
             _NATIVE = L
     return _NATIVE
+
+
+def limbs(vals):
+    """256-bit values as rows of 8 little-endian u32 limbs (one zero row if empty)."""
+    import numpy as np
+
+    return np.array([[(v >> (32 * j)) & 0xFFFFFFFF for j in range(8)] for v in vals] or [[0] * 8],
+                    dtype=np.uint32)
+
+
+def pack_nodes(dag: Dag):
+    """The node table of include/pf_lower.h (8 u32 per node; constants moved to a pool):
+    (nodes array, pool limbs, pool values)."""
+    import numpy as np
+
+    cached = getattr(dag, "_packed", None)
+    if cached is not None and cached[0] == len(dag.nodes):
+        return cached[1]
+    flat: List[int] = []
+    pool: List[int] = []
+    kc = _KIND_CODE
+    for n in dag.nodes:
+        aux = n.aux
+        if n.kind == K_CONST:
+            aux = len(pool)
+            pool.append(n.aux)
+        a = n.args
+        la = len(a)
+        flat += (kc.get(n.kind, n.kind), n.width, la, a[0] if la > 0 else 0, a[1] if la > 1 else 0,
+                 a[2] if la > 2 else 0, aux & 0xFFFFFFFF, 1 if n.is_bool else 0)
+    out = (np.array(flat or [0] * 8, dtype=np.uint32), limbs(pool), pool)
+    dag._packed = (len(dag.nodes), out)  # nodes are append-only: hints and lower share it
+    return out
 
 
 def lower(dag: Dag, seed: int = 0, name: str = "") -> Program:
@@ -301,22 +338,8 @@ def lower(dag: Dag, seed: int = 0, name: str = "") -> Program:
     import numpy as np
 
     nn = len(dag.nodes)
-    flat: List[int] = []
-    pool: List[int] = []
-    kc = _KIND_CODE
-    for n in dag.nodes:
-        aux = n.aux
-        if n.kind == K_CONST:
-            aux = len(pool)
-            pool.append(n.aux)
-        a = n.args
-        la = len(a)
-        flat += (kc.get(n.kind, n.kind), n.width, la, a[0] if la > 0 else 0, a[1] if la > 1 else 0,
-                 a[2] if la > 2 else 0, aux & 0xFFFFFFFF, 1 if n.is_bool else 0)
-    arr = np.array(flat or [0] * 8, dtype=np.uint32)
-    limbs = lambda vals: np.array([[(v >> (32 * j)) & 0xFFFFFFFF for j in range(8)] for v in vals] or
-                                  [[0] * 8], dtype=np.uint32)
-    pool_a, forced_a = limbs(pool), limbs(dag.forced)
+    arr, pool_a, pool = pack_nodes(dag)
+    forced_a = limbs(dag.forced)
     roots = np.array(dag.roots or [0], dtype=np.uint32)
     cap_i = 16 * nn + 64 + 4 * len(dag.roots)
     code = np.zeros((cap_i, 4), dtype=np.uint32)

@@ -632,10 +632,46 @@ class Seeder:
         return [self.value_of_var(v) for v in range(len(self.dag.vars))]
 
 
+def hints_py(dag: Dag) -> Tuple[List[int], int]:
+    """Python reference: (hint value of every variable, number of distinct roots the hint
+    model satisfies).  Caller parents seed the bits no constraint fixes."""
+    s = Seeder(dag, [v.parent for v in dag.vars])
+    vals = s.run()
+    return vals, sum(1 for r in dict.fromkeys(dag.roots) if s.ev(r))
+
+
+def hints(dag: Dag) -> Tuple[List[int], int]:
+    """:func:`hints_py`, computed by libpflower.so (pfl_hints) when it is built — the same
+    values decision for decision (tests/test_native_seed.py)."""
+    from .lower import _native, limbs, pack_nodes
+
+    L = _native()
+    if not L or any(v.width > 256 for v in dag.vars):
+        return hints_py(dag)
+    import ctypes
+
+    import numpy as np
+
+    nodes, pool_a, pool = pack_nodes(dag)
+    nv = len(dag.vars)
+    widths = np.array([v.width for v in dag.vars], dtype=np.uint32)
+    soft = limbs([(v.parent or 0) & M(v.width) for v in dag.vars])
+    roots = np.array(dag.roots or [0], dtype=np.uint32)
+    out = np.zeros((nv, 8), dtype=np.uint32)
+    n_sat = ctypes.c_int()
+    p = lambda x: x.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))  # noqa: E731
+    rc = L.pfl_hints(p(nodes), len(dag.nodes), p(pool_a), len(pool), p(roots), len(dag.roots),
+                     p(widths), nv, p(soft), p(out), ctypes.byref(n_sat))
+    if rc != 0:
+        raise ValueError(f"pfl_hints failed ({rc})")
+    o = out.astype(np.uint64)
+    vals = [sum(int(x) << (32 * j) for j, x in enumerate(row)) for row in o]
+    return vals, n_sat.value
+
+
 def derive_hints(dag: Dag) -> List[int]:
     """Hint value of every variable of ``dag`` (caller parents seed the unfixed bits)."""
-    soft = [v.parent for v in dag.vars]
-    return Seeder(dag, soft).run()
+    return hints(dag)[0]
 
 
 def apply_hints(dag: Dag) -> int:
@@ -643,8 +679,7 @@ def apply_hints(dag: Dag) -> int:
     of roots the hint model itself satisfies (diagnostic)."""
     if not dag.vars:
         return 0
-    s = Seeder(dag, [v.parent for v in dag.vars])
-    vals = s.run()
+    vals, n_sat = hints(dag)
     for var, val in zip(dag.vars, vals):
         var.parent = val & M(var.width)
-    return sum(1 for r in dict.fromkeys(dag.roots) if s.ev(r))
+    return n_sat
