@@ -41,10 +41,16 @@ namespace {
         _Pragma("unroll") for (int k_ = 0; k_ < 8; k_++) (W)[k_][(r)] = (src).l[k_]; \
     } while (0)
 
-// per-limb mask for width w (w uniform -> scalar arithmetic)
+// per-limb mask for width w.  w is wave-uniform (it comes from the scalar-loaded
+// instruction); the mask is formed from the top limb index and its partial mask with
+// scalar selects, and readfirstlane pins the result to an SGPR — the plain expression was
+// compiled to ~6 VALU instructions per limb (~56 per masked op: as much as a cheap op
+// itself, on every op narrower than 256 bits — LASER's bytes and addresses).
 PF_INL uint32_t limb_mask(uint32_t w, int i) {
-    uint32_t lo = (uint32_t)i * 32u;
-    return w >= lo + 32u ? 0xffffffffu : (w <= lo ? 0u : ((1u << (w - lo)) - 1u));
+    const uint32_t li = (w - 1u) >> 5, r = w & 31u;
+    const uint32_t top = r ? ((1u << r) - 1u) : 0xffffffffu;
+    const uint32_t m = (uint32_t)i < li ? 0xffffffffu : ((uint32_t)i == li ? top : 0u);
+    return __builtin_amdgcn_readfirstlane(m);
 }
 
 PF_INL void maskw(u256& x, uint32_t w) {
