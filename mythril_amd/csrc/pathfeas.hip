@@ -133,8 +133,8 @@ Dev* use_dev(int device) {
 }
 
 template <typename T>
-int upload(T** dst, const void* src, size_t bytes) {
-    size_t alloc = bytes ? bytes : 16;
+int upload(T** dst, const void* src, size_t bytes, size_t pad = 0) {
+    size_t alloc = bytes + pad ? bytes + pad : 16;
     HIPCHK(hipMalloc((void**)dst, alloc));
     HIPCHK(hipMemset(*dst, 0, alloc));
     if (bytes && src) HIPCHK(hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice));
@@ -369,7 +369,10 @@ int pf_batch_create_on(int device, const uint32_t* code, size_t n_ins, const uin
     B->h_descs.assign(descs, descs + n_sets);
     int rc = 0;
     rc |= upload(&B->d_code, code, n_ins * 16);
-    rc |= upload(&B->d_consts, consts, n_const * 32);
+    // one zero entry past the pool: the generator's constant gather is issued before it
+    // knows whether the set has constants (pf_eval.hip gen_var), so a set with none reads
+    // the entry at its own const_off, which may be the pool's end
+    rc |= upload(&B->d_consts, consts, n_const * 32, 32);
     rc |= upload(&B->d_schema, schema, n_vars * 16);
     rc |= upload(&B->d_parents, parents, n_parents * 32);
     rc |= upload(&B->d_descs, descs, n_sets * sizeof(pf_set_desc));

@@ -24,7 +24,12 @@ using pf::u256;
 #define PF_PROF_BUCKETS 10
 #define PF_PROF_SLOT 16
 
-typedef uint32_t v16u __attribute__((ext_vector_type(16)));
+// register-bank size (a diagnostic build knob: the bytecode's register count PF_NW + 1 is the
+// product's; smaller banks only serve VGPR-footprint experiments)
+#ifndef PF_BANK
+#define PF_BANK 16
+#endif
+typedef uint32_t vbank __attribute__((ext_vector_type(PF_BANK)));
 typedef uint32_t v32u __attribute__((ext_vector_type(32)));
 
 namespace {
@@ -40,6 +45,13 @@ namespace {
     do {                                                       \
         _Pragma("unroll") for (int k_ = 0; k_ < 8; k_++) (W)[k_][(r)] = (src).l[k_]; \
     } while (0)
+
+// Explicit waits at the end of the datapath arms that load (constants, generator, spill
+// fills, EXP's LDS table): the arms join at the write-back, and a load still pending there on
+// ANY incoming path makes the compiler put `s_waitcnt vmcnt(0) lgkmcnt(0)` in the shared
+// write-back, where lgkmcnt(0) also waits for the next instruction's scalar fetch issued at
+// the top of this one — every bytecode instruction then paid the fetch latency.
+#define PF_WAIT_ALL() __builtin_amdgcn_s_waitcnt(0)
 
 // per-limb mask for width w.  w is wave-uniform (it comes from the scalar-loaded
 // instruction); the mask is formed from the top limb index and its partial mask with
@@ -137,12 +149,24 @@ struct SetCtx {
 // computed for every lane and selected, so the wave runs one straight sequence instead of
 // walking a lane-divergent if-chain; the per-variable kind stays a (uniform) branch.
 PF_INL u256 gen_var(const SetCtx& S, uint32_t v, uint32_t cand) {
-    const uint4 m = philox(make_uint4(cand, v, 2u, 0u), S.k0, S.k1);
-    const uint4 r0 = philox(make_uint4(cand, v, 0u, 0u), S.k0, S.k1);
-    const uint4 r1 = philox(make_uint4(cand, v, 1u, 0u), S.k0, S.k1);
     const uint4 sc = S.schema[v];  // uniform -> scalar load
+    const uint4 m = philox(make_uint4(cand, v, 2u, 0u), S.k0, S.k1);
     const uint32_t kind = sc.x & 0xffu, w = (sc.x >> 8) & 0x3ffu;
     const uint32_t hint0 = sc.y, hint1 = sc.z, pslot = sc.w;
+    // The one per-lane gather (a constant of the set for the +-1 arm, or the actor table
+    // entry) is issued here, in the entry block, so the two Philox blocks below cover its
+    // latency; inside the strategy branches it was waited for a dozen instructions after
+    // issue.  Its address is always in bounds: the pool carries one zero entry past its end
+    // (pathfeas.hip), so a set without constants reads that.
+    const uint32_t ai = m.y & 3u;
+    const bool act = kind == PF_VK_ACTOR && ai < hint1;
+    const uint32_t ci = S.n_const ? (m.y % S.n_const) : 0u;
+    const uint32_t* gp = S.consts + (size_t)(act ? hint0 + ai : ci) * 8u;
+    u256 g;
+#pragma unroll
+    for (int i = 0; i < 8; i++) g.l[i] = gp[i];
+    const uint4 r0 = philox(make_uint4(cand, v, 0u, 0u), S.k0, S.k1);
+    const uint4 r1 = philox(make_uint4(cand, v, 1u, 0u), S.k0, S.k1);
     const bool has_parent = pslot != PF_NO_PARENT;
     u256 par = pf::zero256();
     if (has_parent) {
@@ -171,18 +195,15 @@ PF_INL u256 gen_var(const SetCtx& S, uint32_t v, uint32_t cand) {
         out.l[0] = r0.x & 1u;
     } else {
         const uint32_t sel = m.x & 15u;
-        // constant +-1 arm (sel 9..11): per-lane gather, issued early
+        // constant +-1 arm (sel 9..11)
         u256 cst = rv;
         if (S.n_const > 0u) {
-            const uint32_t* c = S.consts + (size_t)(m.y % S.n_const) * 8u;
-#pragma unroll
-            for (int i = 0; i < 8; i++) cst.l[i] = c[i];
             const uint32_t dsel = m.z % 3u;  // +0, +1, -1
             u256 dl;
             dl.l[0] = dsel == 0u ? 0u : (dsel == 1u ? 1u : 0xffffffffu);
 #pragma unroll
             for (int i = 1; i < 8; i++) dl.l[i] = dsel == 2u ? 0xffffffffu : 0u;
-            cst = pf::add256(cst, dl);
+            cst = pf::add256(g, dl);
         }
         // boundary arm (sel 5..8): {0, 1, 2, 3, 2^w-1, 2^w-2, 2^(w-1), 2^(w-1)-1, 2^k, 2^k-1,
         // 2^k+1, 2^160-1}[j] mod 2^w as one formula, (j >= 6 ? 2^p : 0) + delta
@@ -221,15 +242,8 @@ PF_INL u256 gen_var(const SetCtx& S, uint32_t v, uint32_t cand) {
             const uint32_t sm = i == 0 ? small : 0u;
             out.l[i] = sel <= 4u ? rv.l[i]
                      : (sel <= 8u ? bnd.l[i] : (sel <= 11u ? cst.l[i] : (sel <= 13u ? mut.l[i] : sm)));
-        }
-        if (kind == PF_VK_ACTOR) {
             // the actor set (transaction/symbolic.py:215) in most lanes
-            const uint32_t ai = m.y & 3u;
-            if (ai < hint1) {
-                const uint32_t* ap = S.consts + (size_t)(hint0 + ai) * 8u;
-#pragma unroll
-                for (int i = 0; i < 8; i++) out.l[i] = ap[i];
-            }
+            out.l[i] = act ? g.l[i] : out.l[i];
         }
     }
     // the parent model itself (candidate 0) and its neighbourhood (odd candidates keep the
@@ -278,7 +292,7 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
                             uint2* exp_tbl, uint32_t* complete, uint64_t* ops, UnitProf* prof) {
     // No initialisation: pf_batch_create rejects programs that read a register before
     // writing it, so the banks never leak values between candidates.
-    v16u W[8];
+    vbank W[8];
     // the 32 bool registers are the bits of one VGPR (bit r = B register r)
     uint32_t Bk = 0u;
     // spill slots (lowering under register pressure): dynamically indexed, so the compiler
@@ -316,8 +330,8 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
             break;
         }
         u256 x, y, z;
-        if (tr & PF_TR_RA) RD_W(x, W, a & 15u);
-        if (tr & PF_TR_RB) RD_W(y, W, b & 15u);
+        if (tr & PF_TR_RA) RD_W(x, W, a & (PF_BANK - 1u));
+        if (tr & PF_TR_RB) RD_W(y, W, b & (PF_BANK - 1u));
         uint32_t bres = 0;  // bool result for B ops
         // Dispatch on the datapath unit (w0 bits 21..23) first.  The heavy datapaths exist
         // once each (multiplier, divider, shifter, generator) and are shared by every
@@ -331,7 +345,12 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
                 if (op == PF_W_MUL) {
                     z = pf::mul256(x, y);
                 } else {
+#ifdef PF_DIAG_NO_EXP
+                    z = pf::add256(x, y);
+#else
                     z = pf::exp256_split(x, y, exp_tbl, 64u);
+#endif
+                    PF_WAIT_ALL();
                 }
                 break;
             case PF_U_DIV: {
@@ -349,7 +368,11 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
                 }
                 const u256 ub = sb ? pf::neg256(ys) : ys;
                 u256 q, rr;
+#ifdef PF_DIAG_NO_DIV
+                q = ua; rr = ub;
+#else
                 pf::udivrem256(ua, ub, &q, &rr);
+#endif
                 const bool want_q = op == PF_W_UDIV || op == PF_W_SDIV;
                 const u256 v = want_q ? q : rr;
                 const uint32_t neg = want_q ? (sa ^ sb) : sa;
@@ -359,6 +382,9 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
                 break;
             }
             case PF_U_SHIFT: {
+#ifdef PF_DIAG_NO_SHIFT
+                z = pf::add256(x, y); break;
+#endif
                 const bool by_reg = op <= PF_W_ASHR;
                 const uint32_t big = by_reg ? ge_width(y, w) : (aux >= 256u);
                 const uint32_t amt = by_reg ? y.l[0] : aux;
@@ -380,13 +406,18 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
             case PF_U_GEN:
                 // ---- candidate generator (one site for W and B variables)
                 if (MODE == MODE_GEN) {
+#ifdef PF_DIAG_NO_GEN
+                    z = pf::zero256(); z.l[0] = cand ^ aux;
+#else
                     z = gen_var(S, aux, cand);
+#endif
                 } else {
 #pragma unroll
                     for (int i = 0; i < 8; i++)
                         z.l[i] = active ? soa[((size_t)aux * 8u + i) * soa_n + cand] : 0u;
                 }
                 bres = z.l[0] & 1u;
+                PF_WAIT_ALL();
                 break;
             case PF_U_CMP:
                 switch (op) {
@@ -419,7 +450,10 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
                     case PF_B_XOR: bres = BGET(a) ^ BGET(b); break;
                     case PF_B_NOT: bres = BGET(a) ^ 1u; break;
                     case PF_B_ITE: bres = BGET(c) ? BGET(a) : BGET(b); break;
-                    case PF_B_FILL: bres = spill[(aux & (PF_MAX_SPILL - 1u)) * 8u] & 1u; break;
+                    case PF_B_FILL:
+                        bres = spill[(aux & (PF_MAX_SPILL - 1u)) * 8u] & 1u;
+                        PF_WAIT_ALL();
+                        break;
                     case PF_B_SPILL: spill[(aux & (PF_MAX_SPILL - 1u)) * 8u] = BGET(a); break;
                     default:  // PF_ASSERT
                         root &= BGET(a);
@@ -448,6 +482,7 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
                         const uint32_t* cp = S.consts + (size_t)aux * 8u;
 #pragma unroll
                         for (int i = 0; i < 8; i++) z.l[i] = cp[i];
+                        PF_WAIT_ALL();
                         break;
                     }
                     case PF_W_MOV: z = x; break;
@@ -459,12 +494,16 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
                     case PF_W_FILL:
 #pragma unroll
                         for (int i = 0; i < 8; i++) z.l[i] = spill[(aux & (PF_MAX_SPILL - 1u)) * 8u + i];
+                        PF_WAIT_ALL();
                         break;
                     case PF_W_NOT: z = pf::not256(x); break;
                     case PF_W_NEG: z = pf::neg256(x); break;
                     case PF_W_SEXT: z = sextw(x, aux); break;
                     case PF_W_ITE: z = pf::sel256(BGET(c), x, y); break;
                     case PF_W_HASH: {
+#ifdef PF_DIAG_NO_HASH
+                        z = pf::sub256(x, y); break;
+#endif
                         uint4 h = philox(make_uint4(x.l[0], x.l[1], x.l[2], x.l[3]), aux, PF_HASH_K1A);
                         uint4 g = philox(make_uint4(x.l[4] ^ h.x, x.l[5] ^ h.y, x.l[6] ^ h.z, x.l[7] ^ h.w),
                                          aux, PF_HASH_K1B);
@@ -481,7 +520,7 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
             // PF_W_SINK.  A conditional insert would make the loop-carried banks a phi of
             // old/new values, which costs a full bank copy (~100 extra VGPRs, spills).
             maskw(z, w);
-            const uint32_t dd = (tr & PF_TR_WW) ? (d & 15u) : (uint32_t)PF_W_SINK;
+            const uint32_t dd = (tr & PF_TR_WW) ? (d & (PF_BANK - 1u)) : (uint32_t)(PF_BANK - 1);
             WR_W(W, dd, z);
         }
         if (PF_OP_WRITES_B(op)) {
