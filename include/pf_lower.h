@@ -29,14 +29,16 @@ extern "C" {
 /* One node = 8 x u32: kind, width, nargs, arg0, arg1, arg2, aux, is_bool.  Nodes are in
  * topological order (operands first).  roots: the asserted Bool nodes, in order.
  * forced: constants pinned at pool indices 0.. (schema hints refer to them).
+ * n_wregs: W registers the allocation may use (3..PF_NW; 0 = PF_NW).  PF_NW_NARROW makes a
+ * program the 8-register search kernels run (3 waves/SIMD, pf_eval.hip).
  * Outputs: code_out (cap_ins x 4 u32; aux1 left 0), consts_out (cap_const x 8 u32).
  * Returns 0; -2 when the set needs more live values than the register file and spill
  * slots hold (LoweringError: the query goes to z3); -3 when an output is too small;
  * -1 on malformed input.  The message is in pfl_last_error().                          */
 int pfl_lower(const uint32_t* nodes, size_t n_nodes, const uint32_t* const_pool, size_t n_pool,
               const uint32_t* roots, size_t n_roots, const uint32_t* forced, size_t n_forced,
-              uint32_t* code_out, size_t cap_ins, size_t* n_ins_out, uint32_t* consts_out,
-              size_t cap_const, size_t* n_const_out);
+              uint32_t n_wregs, uint32_t* code_out, size_t cap_ins, size_t* n_ins_out,
+              uint32_t* consts_out, size_t cap_const, size_t* n_const_out);
 const char* pfl_last_error(void);
 
 /* Hint model of one DAG (the native form of mythril_amd/seed.py:Seeder.run, identical

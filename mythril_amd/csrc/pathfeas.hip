@@ -66,6 +66,9 @@ struct Batch {
     int device;
     size_t n_ins, n_const, n_vars, n_parents, n_sets;
     uint32_t max_vars;
+    size_t n_narrow = 0;    // d_order[0, n_narrow): sets whose programs write only W registers
+                            // < PF_NW_NARROW (8-register kernels, 3 waves/SIMD); the rest run
+                            // the 16-register kernels in a second launch
     std::vector<pf_set_desc> h_descs;
     pf_set_desc* d_descs = nullptr;
     uint4* d_code = nullptr;
@@ -173,16 +176,22 @@ int check_enqueue(Batch* B, uint64_t gseed, uint32_t budget, uint32_t flags, uin
 #endif
     HIPCHK(hipMemsetAsync(d_found, 0xff, std::max<size_t>(B->n_sets, 1) * sizeof(uint32_t), st));
     HIPCHK(hipEventRecord(B->ev0, st));
-    if (B->n_sets > 0 && budget > 0) {
+    const uint64_t deadline = timeout_ms ? (uint64_t)timeout_ms * 100000ull : 0ull;  // 100 MHz
+    const bool early = flags & PF_FLAG_EARLY_EXIT;
+    // the 8-register sets first, then the 16-register ones (usually none)
+    for (int part = 0; part < 2; ++part) {
+        const size_t first = part ? B->n_narrow : 0;
+        const size_t n = part ? B->n_sets - B->n_narrow : B->n_narrow;
+        if (n == 0 || budget == 0) continue;
         uint32_t per_wave, slices;
-        geometry(D->num_cus, (uint32_t)B->n_sets, budget, flags, &per_wave, &slices);
-        const uint64_t waves = (uint64_t)B->n_sets * slices;
+        geometry(D->num_cus, (uint32_t)n, budget, flags, &per_wave, &slices);
+        const uint64_t waves = (uint64_t)n * slices;
         if (waves > 0xffffffffull) return fail("batch too large: %llu waves", (unsigned long long)waves);
         const uint32_t blocks = (uint32_t)((waves + 3) / 4);
-        const uint64_t deadline = timeout_ms ? (uint64_t)timeout_ms * 100000ull : 0ull;  // 100 MHz
-        hipLaunchKernelGGL((flags & PF_FLAG_EARLY_EXIT) ? pf_check_early_kernel : pf_check_kernel,
-                           dim3(blocks), dim3(256), 0, st, B->d_descs, B->d_order,
-                           (uint32_t)B->n_sets, B->d_code, B->d_consts, B->d_schema, B->d_parents,
+        hipLaunchKernelGGL(part == 0 ? (early ? pf_check_early_kernel : pf_check_kernel)
+                                     : (early ? pf_check_early_r16_kernel : pf_check_r16_kernel),
+                           dim3(blocks), dim3(256), 0, st, B->d_descs, B->d_order + first,
+                           (uint32_t)n, B->d_code, B->d_consts, B->d_schema, B->d_parents,
                            gseed, budget, per_wave, slices, flags, deadline, d_t0, d_found, d_counters);
         HIPCHK(hipGetLastError());
     }
@@ -327,9 +336,10 @@ int pf_batch_create_on(int device, const uint32_t* code, size_t n_ins, const uin
     // traffic bits and register def-before-use, recomputed here so the kernel can trust
     // them whatever the caller packed (w0 bits 18..23)
     std::vector<uint32_t> code_fixed(code, code + 4 * n_ins);
+    std::vector<uint8_t> wide(n_sets, 0);
     for (size_t s = 0; s < n_sets; s++) {
         const pf_set_desc& d = descs[s];
-        uint32_t wdef = 1u << PF_W_SINK, bdef = 0u;
+        uint32_t wdef = 0u, bdef = 0u, max_wreg = 0u;
         uint64_t sdef = 0ull;
         for (uint32_t i = 0; i < d.n_ins; i++) {
             uint32_t* I = code_fixed.data() + 4 * ((size_t)d.code_off + i);
@@ -338,7 +348,8 @@ int pf_batch_create_on(int device, const uint32_t* code, size_t n_ins, const uin
             const uint32_t rd = I[1] & 0xffu, ra = (I[1] >> 8) & 0xffu, rb = (I[1] >> 16) & 0xffu,
                            rc = (I[1] >> 24) & 0xffu;
             if ((tr & PF_TR_WW) && rd >= PF_NW) return fail("set %zu ins %u: W dst %u", s, i, rd);
-            if (((tr & PF_TR_RA) && !(wdef >> (ra & 15u) & 1u)) || ((tr & PF_TR_RB) && !(wdef >> (rb & 15u) & 1u)))
+            if (((tr & PF_TR_RA) && (ra >= PF_NW || !(wdef >> ra & 1u))) ||
+                ((tr & PF_TR_RB) && (rb >= PF_NW || !(wdef >> rb & 1u))))
                 return fail("set %zu ins %u: W register read before write", s, i);
             const bool bres = PF_OP_WRITES_B(op);
             const bool breads_ab = op >= PF_B_AND && op <= PF_B_XOR;
@@ -353,7 +364,11 @@ int pf_batch_create_on(int device, const uint32_t* code, size_t n_ins, const uin
             if (op == PF_W_SPILL || op == PF_B_SPILL) sdef |= 1ull << I[2];
             if ((op == PF_W_FILL || op == PF_B_FILL) && !(sdef >> I[2] & 1ull))
                 return fail("set %zu ins %u: spill slot %u filled before it was spilled", s, i, I[2]);
-            if (tr & PF_TR_WW) wdef |= 1u << rd;
+            if (tr & PF_TR_WW) {
+                wdef |= 1u << rd;
+                max_wreg = std::max(max_wreg, rd);
+            }
+            if (i + 1 == d.n_ins) wide[s] = max_wreg >= PF_NW_NARROW;
             if (bres) bdef |= 1u << (rd & 31u);
         }
     }
@@ -398,8 +413,10 @@ int pf_batch_create_on(int device, const uint32_t* code, size_t n_ins, const uin
         }
         std::vector<uint32_t> order(n_sets);
         for (size_t s = 0; s < n_sets; ++s) order[s] = (uint32_t)s;
-        std::stable_sort(order.begin(), order.end(),
-                         [&](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
+        std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+            return wide[a] != wide[b] ? wide[a] < wide[b] : cost[a] > cost[b];
+        });
+        B->n_narrow = (size_t)std::count(wide.begin(), wide.end(), (uint8_t)0);
         rc |= upload(&B->d_order, order.data(), n_sets * 4);
     }
     if (rc) {

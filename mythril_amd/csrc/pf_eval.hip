@@ -24,26 +24,30 @@ using pf::u256;
 #define PF_PROF_BUCKETS 10
 #define PF_PROF_SLOT 16
 
-// register-bank size (a diagnostic build knob: the bytecode's register count PF_NW + 1 is the
-// product's; smaller banks only serve VGPR-footprint experiments)
-#ifndef PF_BANK
-#define PF_BANK 16
-#endif
-typedef uint32_t vbank __attribute__((ext_vector_type(PF_BANK)));
+// Register file: NREG wide registers (NREG - 1 usable + the write sink), limb-sliced into
+// 16-dword vectors.  NREG 16: vector k holds limb k of every register (8 vectors).  NREG 8:
+// vector j holds limbs 2j and 2j+1 (element 2r + (k & 1)), 4 vectors — 64 VGPRs instead of
+// 128, which is what lets that build run 3 waves per SIMD.  The vectors stay 16 wide either
+// way: hipcc expands a dynamic index into a vector of 8 or fewer dwords into a v_cndmask
+// tree (56 VALU per operand read) but indexes a 16-dword vector with s_set_gpr_idx (one
+// v_mov per limb).
+typedef uint32_t vbank __attribute__((ext_vector_type(16)));
 typedef uint32_t v32u __attribute__((ext_vector_type(32)));
 
 namespace {
 
-// W bank k holds limb k of all 16 wide registers.  These are macros, not functions: taking
-// the bank array by reference defeats AMDGPUPromoteAlloca (the banks land in scratch), while
-// direct element accesses become one s_set_gpr_idx_on + 8 v_mov per operand.
-#define RD_W(dst, W, r)                                        \
-    do {                                                       \
-        _Pragma("unroll") for (int k_ = 0; k_ < 8; k_++) (dst).l[k_] = (W)[k_][(r)]; \
+// These are macros, not functions: taking the vector array by reference defeats
+// AMDGPUPromoteAlloca (the banks land in scratch), while direct element accesses become one
+// s_set_gpr_idx_on + 8 v_mov per operand.
+#define RD_W(dst, W, r, LPB)                                                                  \
+    do {                                                                                      \
+        _Pragma("unroll") for (int k_ = 0; k_ < 8; k_++)                                    \
+            (dst).l[k_] = (W)[k_ / (LPB)][(r) * (LPB) + (k_ % (LPB))];                         \
     } while (0)
-#define WR_W(W, r, src)                                        \
-    do {                                                       \
-        _Pragma("unroll") for (int k_ = 0; k_ < 8; k_++) (W)[k_][(r)] = (src).l[k_]; \
+#define WR_W(W, r, src, LPB)                                                                  \
+    do {                                                                                      \
+        _Pragma("unroll") for (int k_ = 0; k_ < 8; k_++)                                    \
+            (W)[k_ / (LPB)][(r) * (LPB) + (k_ % (LPB))] = (src).l[k_];                         \
     } while (0)
 
 // Explicit waits at the end of the datapath arms that load (constants, generator, spill
@@ -279,6 +283,9 @@ PF_INL void prof_add(UnitProf* P, uint32_t b, uint64_t dt) {
 PF_INL uint2* exp_tbl_of(uint2* lds) {
     return lds + (threadIdx.x >> 6) * (PF_EXP_TBL_ENTRIES * 4 * 64) + (threadIdx.x & 63u);
 }
+#ifndef PF_WG_PER_CU_NARROW
+#define PF_WG_PER_CU_NARROW 3
+#endif
 #ifndef PF_WG_PER_CU
 #define PF_WG_PER_CU 2
 #endif
@@ -286,13 +293,14 @@ PF_INL uint2* exp_tbl_of(uint2* lds) {
 // Run one set's program for this lane's candidate.  Returns the lane's root (0/1);
 // *complete = 1 if the program ran to END (not short-circuited).  `ops` accumulates
 // aux1 (per-lane algorithmic cost) of every executed instruction.
-template <int MODE>
+template <int MODE, int NREG>
 PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_t flags,
                             const uint32_t* __restrict__ soa, uint32_t soa_n,
                             uint2* exp_tbl, uint32_t* complete, uint64_t* ops, UnitProf* prof) {
     // No initialisation: pf_batch_create rejects programs that read a register before
     // writing it, so the banks never leak values between candidates.
-    vbank W[8];
+    constexpr int LPB = 16 / NREG;  // limbs per vector
+    vbank W[8 / LPB];
     // the 32 bool registers are the bits of one VGPR (bit r = B register r)
     uint32_t Bk = 0u;
     // spill slots (lowering under register pressure): dynamically indexed, so the compiler
@@ -330,8 +338,8 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
             break;
         }
         u256 x, y, z;
-        if (tr & PF_TR_RA) RD_W(x, W, a & (PF_BANK - 1u));
-        if (tr & PF_TR_RB) RD_W(y, W, b & (PF_BANK - 1u));
+        if (tr & PF_TR_RA) RD_W(x, W, min(a, NREG - 1u), LPB);
+        if (tr & PF_TR_RB) RD_W(y, W, min(b, NREG - 1u), LPB);
         uint32_t bres = 0;  // bool result for B ops
         // Dispatch on the datapath unit (w0 bits 21..23) first.  The heavy datapaths exist
         // once each (multiplier, divider, shifter, generator) and are shared by every
@@ -520,8 +528,8 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
             // PF_W_SINK.  A conditional insert would make the loop-carried banks a phi of
             // old/new values, which costs a full bank copy (~100 extra VGPRs, spills).
             maskw(z, w);
-            const uint32_t dd = (tr & PF_TR_WW) ? (d & (PF_BANK - 1u)) : (uint32_t)(PF_BANK - 1);
-            WR_W(W, dd, z);
+            const uint32_t dd = (tr & PF_TR_WW) ? min(d, NREG - 1u) : (uint32_t)(NREG - 1);
+            WR_W(W, dd, z, LPB);
         }
         if (PF_OP_WRITES_B(op)) {
             const uint32_t bit = 1u << (d & 31u);
@@ -565,7 +573,7 @@ PF_INL SetCtx make_ctx(const pf_set_desc* __restrict__ descs, uint32_t set,
 // Two entry points over one body: the full sweep (pf_check_kernel) and the production
 // early-exit search (pf_check_early_kernel).  EARLY is a template constant so the full sweep
 // carries no found[] polling, and the two launches are separate rows in a rocprof trace.
-template <bool EARLY>
+template <bool EARLY, int NREG>
 PF_INL void check_body(const pf_set_desc* __restrict__ descs, const uint32_t* __restrict__ order,
                        uint32_t n_sets,
                        const uint4* __restrict__ code, const uint32_t* __restrict__ consts,
@@ -617,7 +625,7 @@ PF_INL void check_body(const pf_set_desc* __restrict__ descs, const uint32_t* __
         const bool active = cand < end;
         uint32_t complete = 0;
         uint64_t lane_ops = 0;
-        uint32_t sat = run_program<MODE_GEN>(S, cand, active, flags, nullptr, 0u, exp_tbl, &complete,
+        uint32_t sat = run_program<MODE_GEN, NREG>(S, cand, active, flags, nullptr, 0u, exp_tbl, &complete,
                                              &lane_ops, &prof);
         const uint64_t m_act = __ballot(active);
         const uint64_t m_sat = __ballot(active && sat);
@@ -657,11 +665,22 @@ PF_INL void check_body(const pf_set_desc* __restrict__ descs, const uint32_t* __
     descs, order, n_sets, code, consts, schema, parents, gseed, budget, per_wave, slices, flags, \
         deadline_ticks, t0_slot, found, counters
 
-extern "C" __global__ void __launch_bounds__(256, PF_WG_PER_CU) pf_check_kernel(PF_CHECK_PARAMS) {
-    check_body<false>(PF_CHECK_ARGS);
+// The search kernels exist twice: over 8 registers at 3 waves per SIMD (programs whose
+// lowering fits PF_NW_NARROW registers — the host picks per batch, pathfeas.hip) and over 16
+// at 2 waves.  Occupancy is the lever: config 3 runs +22 % faster on the 8-register build
+// (DESIGN.md §3), the interpreter's scalar dispatch and memory latency being what a third
+// wave hides.
+extern "C" __global__ void __launch_bounds__(256, PF_WG_PER_CU_NARROW) pf_check_kernel(PF_CHECK_PARAMS) {
+    check_body<false, PF_NW_NARROW + 1>(PF_CHECK_ARGS);
 }
-extern "C" __global__ void __launch_bounds__(256, PF_WG_PER_CU) pf_check_early_kernel(PF_CHECK_PARAMS) {
-    check_body<true>(PF_CHECK_ARGS);
+extern "C" __global__ void __launch_bounds__(256, PF_WG_PER_CU_NARROW) pf_check_early_kernel(PF_CHECK_PARAMS) {
+    check_body<true, PF_NW_NARROW + 1>(PF_CHECK_ARGS);
+}
+extern "C" __global__ void __launch_bounds__(256, PF_WG_PER_CU) pf_check_r16_kernel(PF_CHECK_PARAMS) {
+    check_body<false, 16>(PF_CHECK_ARGS);
+}
+extern "C" __global__ void __launch_bounds__(256, PF_WG_PER_CU) pf_check_early_r16_kernel(PF_CHECK_PARAMS) {
+    check_body<true, 16>(PF_CHECK_ARGS);
 }
 
 // ---- explicit-assignment evaluation (SoA [var][limb][cand]) --------------------------
@@ -677,7 +696,7 @@ pf_eval_soa_kernel(const pf_set_desc* __restrict__ descs, uint32_t set,
     uint32_t complete = 0;
     uint64_t ops = 0;
     UnitProf prof;
-    uint32_t sat = run_program<MODE_SOA>(S, active ? cand : 0u, active, 0u, soa, n_cand,
+    uint32_t sat = run_program<MODE_SOA, 16>(S, active ? cand : 0u, active, 0u, soa, n_cand,
                                          exp_tbl_of(pf_exp_lds), &complete, &ops, &prof);
     if (active) out[cand] = (uint8_t)sat;
 }

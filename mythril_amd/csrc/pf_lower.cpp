@@ -79,9 +79,9 @@ struct RegFile {
 
 class Lowerer {
    public:
-    Lowerer(const Node* nodes, size_t n_nodes, const Const8* pool, size_t n_pool)
+    Lowerer(const Node* nodes, size_t n_nodes, const Const8* pool, size_t n_pool, int n_wregs)
         : N(nodes), nn(n_nodes), pool(pool), n_pool(n_pool), where(n_nodes, NONE),
-          slot_of(n_nodes, NONE), remat(n_nodes, -2), W(PF_NW, &where), B(PF_NB, &where) {
+          slot_of(n_nodes, NONE), remat(n_nodes, -2), W(n_wregs, &where), B(PF_NB, &where) {
         for (int s = PF_MAX_SPILL - 1; s >= 0; --s) free_slots.push_back(s);
     }
 
@@ -348,15 +348,17 @@ class Lowerer {
 
 extern "C" {
 
-int pfl_version(void) { return 1; }
+int pfl_version(void) { return 2; }
 
 const char* pfl_last_error(void) { return g_err.c_str(); }
 
 int pfl_lower(const uint32_t* nodes, size_t n_nodes, const uint32_t* const_pool, size_t n_pool,
               const uint32_t* roots, size_t n_roots, const uint32_t* forced, size_t n_forced,
-              uint32_t* code_out, size_t cap_ins, size_t* n_ins_out, uint32_t* consts_out,
-              size_t cap_const, size_t* n_const_out) {
+              uint32_t n_wregs, uint32_t* code_out, size_t cap_ins, size_t* n_ins_out,
+              uint32_t* consts_out, size_t cap_const, size_t* n_const_out) {
     const Node* N = reinterpret_cast<const Node*>(nodes);
+    if (n_wregs == 0) n_wregs = PF_NW;
+    if (n_wregs < 3 || n_wregs > PF_NW) return fail(-1, "n_wregs %u outside [3, %d]", n_wregs, PF_NW);
     for (size_t i = 0; i < n_nodes; ++i) {  // shape checks: indices the lowering follows
         const Node& n = N[i];
         if (n.nargs > 3) return fail(-1, "node %zu: %u operands", i, n.nargs);
@@ -366,7 +368,7 @@ int pfl_lower(const uint32_t* nodes, size_t n_nodes, const uint32_t* const_pool,
     for (size_t r = 0; r < n_roots; ++r)
         if (roots[r] >= n_nodes || !N[roots[r]].is_bool) return fail(-1, "root %zu is not a Bool node", r);
     try {
-        Lowerer L(N, n_nodes, reinterpret_cast<const Const8*>(const_pool), n_pool);
+        Lowerer L(N, n_nodes, reinterpret_cast<const Const8*>(const_pool), n_pool, (int)n_wregs);
         for (size_t f = 0; f < n_forced; ++f) {
             Const8 c;
             memcpy(c.l, forced + 8 * f, 32);

@@ -17,6 +17,7 @@ from typing import List, Optional, Sequence
 import numpy as np
 
 NW = 15  # usable W registers; register 15 is the kernel's write sink
+NW_NARROW = 7  # PF_NW_NARROW: programs within it run the 8-register, 3-waves/SIMD kernels
 NB = 32
 LIMBS = 8
 MAX_WIDTH = 256

@@ -275,15 +275,16 @@ def _native():
         import ctypes
         import os
 
-        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpflower.so")
+        path = os.environ.get("PF_LOWER_SO") or os.path.join(
+            os.path.dirname(os.path.abspath(__file__)), "libpflower.so")  # override: diagnostics
         if os.environ.get("PF_LOWER_PY") or not os.path.exists(path):
             _NATIVE = False
         else:
             L = ctypes.CDLL(path)
             u32p, szp = ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_size_t)
             L.pfl_lower.argtypes = [u32p, ctypes.c_size_t, u32p, ctypes.c_size_t, u32p,
-                                    ctypes.c_size_t, u32p, ctypes.c_size_t, u32p, ctypes.c_size_t,
-                                    szp, u32p, ctypes.c_size_t, szp]
+                                    ctypes.c_size_t, u32p, ctypes.c_size_t, ctypes.c_uint32, u32p,
+                                    ctypes.c_size_t, szp, u32p, ctypes.c_size_t, szp]
             L.pfl_lower.restype = ctypes.c_int
             L.pfl_hints.argtypes = [u32p, ctypes.c_size_t, u32p, ctypes.c_size_t, u32p,
                                     ctypes.c_size_t, u32p, ctypes.c_size_t, u32p, u32p,
@@ -327,12 +328,29 @@ def pack_nodes(dag: Dag):
     return out
 
 
-def lower(dag: Dag, seed: int = 0, name: str = "") -> Program:
-    """Register allocation + emission: the native library when built (identical output,
-    tests/test_native_lower.py), else the Python reference :func:`lower_py`."""
+def _spills(prog) -> bool:
+    if isinstance(prog, ir.PackedProgram):
+        return bool(((prog.words[:, 0] & 0xFF) == ir.W_SPILL).any())
+    return any(ins.op == ir.W_SPILL for ins in prog.code)
+
+
+def lower(dag: Dag, seed: int = 0, name: str = "", nw: Optional[int] = None) -> Program:
+    """Register allocation + emission.  Without ``nw``: over ir.NW_NARROW registers first —
+    such a program runs the 8-register, 3-waves/SIMD search kernels — and over all ir.NW
+    when that would spill a W value or cannot fit (the 16-register kernels then run its
+    batch).  The native library when built (identical output, tests/test_native_lower.py),
+    else the Python reference :func:`lower_py`."""
+    if nw is None:
+        try:
+            prog = lower(dag, seed, name, ir.NW_NARROW)
+            if not _spills(prog):
+                return prog
+        except LoweringError:
+            pass
+        return lower(dag, seed, name, ir.NW)
     L = _native()
     if not L:
-        return lower_py(dag, seed, name)
+        return lower_py(dag, seed, name, nw)
     import ctypes
 
     import numpy as np
@@ -348,7 +366,7 @@ def lower(dag: Dag, seed: int = 0, name: str = "") -> Program:
     ni, nc = ctypes.c_size_t(), ctypes.c_size_t()
     p = lambda x: x.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))  # noqa: E731
     rc = L.pfl_lower(p(arr), nn, p(pool_a), len(pool), p(roots), len(dag.roots), p(forced_a),
-                     len(dag.forced), p(code), cap_i, ctypes.byref(ni), p(consts), cap_c,
+                     len(dag.forced), nw, p(code), cap_i, ctypes.byref(ni), p(consts), cap_c,
                      ctypes.byref(nc))
     if rc != 0:
         msg = L.pfl_last_error().decode(errors="replace")
@@ -360,7 +378,7 @@ def lower(dag: Dag, seed: int = 0, name: str = "") -> Program:
     return ir.PackedProgram(code[:ni.value].copy(), cvals, list(dag.vars), seed, name)
 
 
-def lower_py(dag: Dag, seed: int = 0, name: str = "") -> Program:
+def lower_py(dag: Dag, seed: int = 0, name: str = "", nw: int = ir.NW) -> Program:
     """Python reference of the lowering (the native library reproduces it exactly)."""
     prog = Program(vars=list(dag.vars), seed=seed, name=name)
     prog.consts.extend(dag.forced)  # schema hints index these (actor tables, keccak bases)
@@ -407,7 +425,7 @@ def lower_py(dag: Dag, seed: int = 0, name: str = "") -> Program:
         remat_memo[nd] = res
         return res
 
-    W = _RegFile(ir.NW, "W")
+    W = _RegFile(nw, "W")
     B = _RegFile(ir.NB, "B")
     # spill slots (PF_W_SPILL / PF_B_SPILL): values that can neither stay resident nor be
     # recomputed cheaply; a spilled value keeps its slot until its last use, so evicting

@@ -117,6 +117,49 @@ def test_search_matches_oracle(engine, flags):
     assert res.cands_decided > 0
 
 
+def _pressure_program(n_live=14):
+    dag = Dag()
+    x, y = dag.var("x", 256), dag.var("y", 256)
+    prods = [dag.op(ir.W_MUL, 256, x, dag.op(ir.W_ADD, 256, y, dag.const(k + 1, 256))) for k in range(n_live)]
+    acc = prods[0]
+    for p in prods[1:]:
+        acc = dag.op(ir.W_XOR, 256, acc, p)
+    for p in prods:
+        dag.assert_(dag.op(ir.B_ULT, 256, p, acc))
+    return lower(dag, nw=ir.NW)
+
+
+@pytest.mark.parametrize("flags", [0, ir.FLAG_EARLY_EXIT | ir.FLAG_SHORTCIRCUIT])
+def test_narrow_and_wide_register_files_agree(engine, flags):
+    """The same sets lowered over 7 registers (8-register, 3-waves/SIMD kernels) and over 15
+    (16-register kernels: the batch also holds a program that writes register 14) give the
+    oracle's smallest witness in both."""
+    budget, seed = 1024, 0xABCD_0123
+    ids = [(700 + i, i % 3 == 0) for i in range(12)]
+    narrow, wide = [], []
+    for d, plant in ids:
+        got = {}
+        orig = synth.lower
+        synth.lower = lambda dag, **k: got.setdefault("dag", dag) and orig(dag, **k)
+        try:
+            synth.random_dag_set(d, plant=plant)
+        finally:
+            synth.lower = orig
+        narrow.append(lower(got["dag"], nw=ir.NW_NARROW))
+        wide.append(lower(got["dag"], nw=ir.NW))
+    pw = _pressure_program()
+    assert max(int(ins[1] & 0xFF) for ins in ir.Batch([pw]).code.reshape(-1, 4)) >= ir.NW_NARROW
+    rn = engine.check(engine.upload(narrow), budget=budget, seed=seed, flags=flags)
+    rw = engine.check(engine.upload(wide + [pw]), budget=budget, seed=seed, flags=flags)
+    for i, p in enumerate(narrow):
+        want = _oracle_first(p, budget, seed)
+        gn = None if rn.found[i] == 0xFFFFFFFF else int(rn.found[i])
+        gw = None if rw.found[i] == 0xFFFFFFFF else int(rw.found[i])
+        assert gn == want and gw == want, (i, gn, gw, want)
+    if flags == 0:
+        assert rn.evals_full == len(narrow) * budget
+
+
 def test_planted_witness_found_at_candidate_zero(engine):
     progs = [synth.random_dag_set(300 + i, plant=True)[0] for i in range(16)]
     db = engine.upload(progs)
