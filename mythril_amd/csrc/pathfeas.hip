@@ -34,6 +34,10 @@ struct Dev {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     int num_cus = 256;
     hipStream_t last_stream = nullptr;  // see switch_stream
+    // device blocks of freed batches, reused by later batches that fit: a query's batch is
+    // created and freed per call, and hipMalloc + hipFree (which synchronises the device)
+    // per buffer were a millisecond of the single-query latency
+    std::vector<std::pair<void*, size_t>> pool;
 };
 std::vector<Dev> g_devs;  // ascending device ids
 int g_default = -1;       // index in g_devs of the default device (lowest id)
@@ -64,6 +68,8 @@ int fail(const char* fmt, ...) {
 
 struct Batch {
     int device;
+    void* d_mem = nullptr;  // one device block holding every array below
+    size_t mem_cap = 0;
     size_t n_ins, n_const, n_vars, n_parents, n_sets;
     uint32_t max_vars;
     size_t n_narrow = 0;    // d_order[0, n_narrow): sets whose programs write only W registers
@@ -79,15 +85,8 @@ struct Batch {
     uint32_t* d_order = nullptr;    // set ids, most expensive first (search-kernel wave order)
     uint32_t* d_scratch = nullptr;  // this batch's launch counters (u64 [0..3]) and t0 (u64 [4])
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    ~Batch() {  // also the error path of pf_batch_create: frees whatever was allocated
-        hipFree(d_code);
-        hipFree(d_consts);
-        hipFree(d_schema);
-        hipFree(d_parents);
-        hipFree(d_descs);
-        hipFree(d_found);
-        hipFree(d_order);
-        hipFree(d_scratch);
+    ~Batch() {  // the device block goes back to its device's pool first (release_batch)
+        if (d_mem) hipFree(d_mem);
         if (ev0) hipEventDestroy(ev0);
         if (ev1) hipEventDestroy(ev1);
     }
@@ -105,6 +104,42 @@ Dev* find_dev(int id) {
     for (auto& d : g_devs)
         if (d.id == id) return &d;
     return nullptr;
+}
+
+constexpr size_t kPoolBlocks = 8;
+
+// a device block of at least `bytes` from the device's pool (smallest that fits and wastes
+// at most 4x), else a new one
+void* pool_acquire(Dev* D, size_t bytes, size_t* cap) {
+    size_t best = SIZE_MAX;
+    for (size_t i = 0; i < D->pool.size(); ++i)
+        if (D->pool[i].second >= bytes && D->pool[i].second <= 4 * bytes + (1u << 20) &&
+            (best == SIZE_MAX || D->pool[i].second < D->pool[best].second))
+            best = i;
+    if (best != SIZE_MAX) {
+        void* p = D->pool[best].first;
+        *cap = D->pool[best].second;
+        D->pool.erase(D->pool.begin() + best);
+        return p;
+    }
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+    *cap = bytes;
+    return p;
+}
+
+// free a batch: its block is kept for reuse (the oldest block is released when the pool is
+// full).  Called with no launch of the batch in flight (pf_batch_free drains the device).
+void release_batch(Dev* D, Batch* B) {
+    if (D && B->d_mem) {
+        if (D->pool.size() >= kPoolBlocks) {
+            hipFree(D->pool.front().first);
+            D->pool.erase(D->pool.begin());
+        }
+        D->pool.emplace_back(B->d_mem, B->mem_cap);
+        B->d_mem = nullptr;
+    }
+    delete B;
 }
 
 // A launch on a caller's stream (the *_dev entry points) returns without waiting; before the
@@ -133,15 +168,6 @@ Dev* use_dev(int device) {
         return nullptr;
     }
     return D;
-}
-
-template <typename T>
-int upload(T** dst, const void* src, size_t bytes, size_t pad = 0) {
-    size_t alloc = bytes + pad ? bytes + pad : 16;
-    HIPCHK(hipMalloc((void**)dst, alloc));
-    HIPCHK(hipMemset(*dst, 0, alloc));
-    if (bytes && src) HIPCHK(hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice));
-    return 0;
 }
 
 Batch* as_batch(uint64_t h) { return reinterpret_cast<Batch*>(static_cast<uintptr_t>(h)); }
@@ -284,6 +310,8 @@ int pf_shutdown(void) {
     for (auto& D : g_devs) {
         hipSetDevice(D.id);
         hipDeviceSynchronize();
+        for (auto& b : D.pool) hipFree(b.first);
+        D.pool.clear();
         hipEventDestroy(D.ev0);
         hipEventDestroy(D.ev1);
         hipStreamDestroy(D.stream);
@@ -373,6 +401,48 @@ int pf_batch_create_on(int device, const uint32_t* code, size_t n_ins, const uin
         }
     }
     code = code_fixed.data();
+    // Longest-first wave order: waves are dispatched in index order, so mapping the first
+    // waves to the most expensive sets leaves the cheap ones for the last, partly filled
+    // round.  Weights are measured SIMD cycles per instruction relative to a cheap op
+    // (EXP ~7.1k, a division ~2.6k, MUL ~750, cheap ~650).  8-register sets
+    // come first (their launch precedes the 16-register one's).
+    std::vector<uint64_t> cost(n_sets, 0);
+    for (size_t s = 0; s < n_sets; ++s) {
+        const uint4* I = reinterpret_cast<const uint4*>(code) + descs[s].code_off;
+        uint64_t c = 0;
+        for (uint32_t i = 0; i < descs[s].n_ins; ++i) {
+            const uint32_t op = I[i].x & 0xffu;
+            c += op == PF_W_EXP ? 110u : op == PF_W_MUL ? 12u : pf_op_unit(op) == PF_U_DIV ? 40u : 10u;
+        }
+        cost[s] = c;
+    }
+    std::vector<uint32_t> order(n_sets);
+    for (size_t s = 0; s < n_sets; ++s) order[s] = (uint32_t)s;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+        return wide[a] != wide[b] ? wide[a] < wide[b] : cost[a] > cost[b];
+    });
+
+    // One device block, one copy: [code | consts + one zero entry | schema | parents | descs |
+    // order | found | scratch], each region 256-byte aligned.  The zero entry past the
+    // constant pool: the generator's constant gather is issued before it knows whether the
+    // set has constants (pf_eval.hip gen_var), so a set with none reads the entry at its own
+    // const_off, which may be the pool's end.
+    auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+    const size_t o_code = 0, o_const = o_code + al(n_ins * 16), o_schema = o_const + al(n_const * 32 + 32),
+                 o_par = o_schema + al(n_vars * 16), o_desc = o_par + al(n_parents * 32),
+                 o_order = o_desc + al(n_sets * sizeof(pf_set_desc)), o_found = o_order + al(n_sets * 4),
+                 o_scr = o_found + al(std::max<size_t>(n_sets, 1) * 4), total = o_scr + 256;
+    std::vector<uint8_t> stage(o_found, 0);  // found / scratch are cleared by every search
+    auto put = [&](size_t off, const void* src, size_t bytes) {
+        if (bytes && src) memcpy(stage.data() + off, src, bytes);
+    };
+    put(o_code, code, n_ins * 16);
+    put(o_const, consts, n_const * 32);
+    put(o_schema, schema, n_vars * 16);
+    put(o_par, parents, n_parents * 32);
+    put(o_desc, descs, n_sets * sizeof(pf_set_desc));
+    put(o_order, order.data(), n_sets * 4);
+
     Batch* B = new Batch();
     B->device = Dv->id;
     B->n_ins = n_ins;
@@ -381,46 +451,29 @@ int pf_batch_create_on(int device, const uint32_t* code, size_t n_ins, const uin
     B->n_parents = n_parents;
     B->n_sets = n_sets;
     B->max_vars = max_vars;
+    B->n_narrow = (size_t)std::count(wide.begin(), wide.end(), (uint8_t)0);
     B->h_descs.assign(descs, descs + n_sets);
+    B->d_mem = pool_acquire(Dv, total, &B->mem_cap);
+    if (!B->d_mem) {
+        delete B;
+        return fail("pf_batch_create: hipMalloc(%zu) failed", total);
+    }
+    uint8_t* base = static_cast<uint8_t*>(B->d_mem);
+    B->d_code = reinterpret_cast<uint4*>(base + o_code);
+    B->d_consts = reinterpret_cast<uint32_t*>(base + o_const);
+    B->d_schema = reinterpret_cast<uint4*>(base + o_schema);
+    B->d_parents = reinterpret_cast<uint32_t*>(base + o_par);
+    B->d_descs = reinterpret_cast<pf_set_desc*>(base + o_desc);
+    B->d_order = reinterpret_cast<uint32_t*>(base + o_order);
+    B->d_found = reinterpret_cast<uint32_t*>(base + o_found);
+    B->d_scratch = reinterpret_cast<uint32_t*>(base + o_scr);
     int rc = 0;
-    rc |= upload(&B->d_code, code, n_ins * 16);
-    // one zero entry past the pool: the generator's constant gather is issued before it
-    // knows whether the set has constants (pf_eval.hip gen_var), so a set with none reads
-    // the entry at its own const_off, which may be the pool's end
-    rc |= upload(&B->d_consts, consts, n_const * 32, 32);
-    rc |= upload(&B->d_schema, schema, n_vars * 16);
-    rc |= upload(&B->d_parents, parents, n_parents * 32);
-    rc |= upload(&B->d_descs, descs, n_sets * sizeof(pf_set_desc));
-    rc |= upload(&B->d_found, nullptr, n_sets * 4);
-    rc |= upload(&B->d_scratch, nullptr, 256);
+    if (hipMemcpy(B->d_mem, stage.data(), stage.size(), hipMemcpyHostToDevice) != hipSuccess)
+        rc = fail("pf_batch_create: hipMemcpy of %zu bytes failed", stage.size());
     if (!rc && (hipEventCreate(&B->ev0) != hipSuccess || hipEventCreate(&B->ev1) != hipSuccess))
         rc = fail("pf_batch_create: hipEventCreate failed");
-    // Longest-first wave order: waves are dispatched in index order, so mapping the first
-    // waves to the most expensive sets leaves the cheap ones for the last, partly filled
-    // round.  Weights are measured SIMD cycles per instruction relative to a cheap op
-    // (EXP ~7.1k, a division ~2.6k, MUL ~750, cheap ~650).
-    {
-        std::vector<uint64_t> cost(n_sets, 0);
-        for (size_t s = 0; s < n_sets; ++s) {
-            const uint4* I = reinterpret_cast<const uint4*>(code) + descs[s].code_off;
-            uint64_t c = 0;
-            for (uint32_t i = 0; i < descs[s].n_ins; ++i) {
-                const uint32_t op = I[i].x & 0xffu;
-                c += op == PF_W_EXP ? 110u : op == PF_W_MUL ? 12u
-                     : pf_op_unit(op) == PF_U_DIV ? 40u : 10u;
-            }
-            cost[s] = c;
-        }
-        std::vector<uint32_t> order(n_sets);
-        for (size_t s = 0; s < n_sets; ++s) order[s] = (uint32_t)s;
-        std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
-            return wide[a] != wide[b] ? wide[a] < wide[b] : cost[a] > cost[b];
-        });
-        B->n_narrow = (size_t)std::count(wide.begin(), wide.end(), (uint8_t)0);
-        rc |= upload(&B->d_order, order.data(), n_sets * 4);
-    }
     if (rc) {
-        delete B;
+        release_batch(Dv, B);
         return -1;
     }
     *handle_out = (uint64_t)(uintptr_t)B;
@@ -443,7 +496,7 @@ int pf_batch_free(uint64_t handle) {
     // a *_dev launch may still be reading the batch on a caller's stream: drain the device
     hipDeviceSynchronize();
     if (D) D->last_stream = nullptr;
-    delete B;
+    release_batch(D, B);
     return 0;
 }
 

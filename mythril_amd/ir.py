@@ -161,6 +161,15 @@ def to_limbs(v: int, n: int = LIMBS) -> List[int]:
     return [(v >> (32 * i)) & 0xFFFFFFFF for i in range(n)]
 
 
+def limbs_array(values: Sequence[int]) -> np.ndarray:
+    """Many 256-bit values as rows of 8 little-endian u32 limbs (bulk to_limbs)."""
+    if not values:
+        return np.zeros((0, LIMBS), dtype=np.uint32)
+    m = (1 << (32 * LIMBS)) - 1
+    buf = b"".join((int(v) & m).to_bytes(4 * LIMBS, "little") for v in values)
+    return np.frombuffer(buf, dtype="<u4").reshape(-1, LIMBS).astype(np.uint32)
+
+
 def from_limbs(limbs: Sequence[int]) -> int:
     v = 0
     for i, x in enumerate(limbs):
@@ -362,8 +371,7 @@ class Batch:
                     # (PF_FLAG_COUNT_OPS; reach_cost, so the roofline's achieved <= peak)
                     code.append((w0, w1, a0, reach_cost(ins.op, ins.width) if ins.op != END else 0))
             d_const = len(consts)
-            for c in p.consts:
-                consts.append(to_limbs(c))
+            consts.extend(p.consts)
             d_var = len(schema)
             has_par = p.has_parent
             d_par = len(parents) if has_par else NO_PARENT
@@ -371,7 +379,7 @@ class Batch:
                 slot = NO_PARENT
                 if has_par and v.parent is not None:
                     slot = len(parents)
-                    parents.append(to_limbs(v.parent & mask(v.width)))
+                    parents.append(v.parent & mask(v.width))
                 schema.append((v.kind | (v.width << 8), v.hint0 & 0xFFFFFFFF,
                                v.hint1 & 0xFFFFFFFF, slot))
             descs.append((d_code, len(code) - d_code, d_const, len(p.consts), d_var, len(p.vars),
@@ -388,9 +396,9 @@ class Batch:
             self.code = arr
         else:
             self.code = np.asarray(code, dtype=np.uint32).reshape(-1, 4)
-        self.consts = np.asarray(consts, dtype=np.uint32).reshape(-1, LIMBS)
+        self.consts = limbs_array(consts)
         self.schema = np.asarray(schema, dtype=np.uint32).reshape(-1, 4)
-        self.parents = np.asarray(parents, dtype=np.uint32).reshape(-1, LIMBS)
+        self.parents = limbs_array(parents)
         self.descs = np.asarray(descs, dtype=np.uint32).reshape(-1, 8)
 
     def __len__(self):

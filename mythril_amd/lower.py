@@ -17,7 +17,7 @@ and is left to z3 (the engine never guesses).
 from __future__ import annotations
 
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Sequence, Tuple  # noqa: F401
+from typing import Dict, List, NamedTuple, Optional, Sequence, Tuple  # noqa: F401
 
 from . import ir
 from .ir import Ins, Program, Var
@@ -33,8 +33,8 @@ class LoweringError(ValueError):
     """The set uses a shape the GPU bytecode does not cover; it falls back to z3."""
 
 
-@dataclass
-class Node:
+class Node(NamedTuple):
+    """One DAG node; a tuple, so it is its own hash-consing key (Dag.add)."""
     kind: object          # IR opcode (int) or one of the K_* leaf kinds
     width: int            # result width for W nodes, operand width for compares, 1 for bools
     args: Tuple[int, ...] = ()
@@ -58,12 +58,12 @@ class Dag:
         return start
 
     def add(self, kind, width, args=(), aux=0, is_bool=False) -> int:
-        key = (kind, width, tuple(args), aux, is_bool)
-        i = self._memo.get(key)
+        node = Node(kind, width, args if type(args) is tuple else tuple(args), aux, is_bool)
+        i = self._memo.get(node)
         if i is None:
             i = len(self.nodes)
-            self.nodes.append(Node(kind, width, tuple(args), aux, is_bool))
-            self._memo[key] = i
+            self.nodes.append(node)
+            self._memo[node] = i
         return i
 
     # ---- leaves --------------------------------------------------------------------
@@ -299,8 +299,7 @@ def limbs(vals):
     """256-bit values as rows of 8 little-endian u32 limbs (one zero row if empty)."""
     import numpy as np
 
-    return np.array([[(v >> (32 * j)) & 0xFFFFFFFF for j in range(8)] for v in vals] or [[0] * 8],
-                    dtype=np.uint32)
+    return ir.limbs_array(vals) if vals else np.zeros((1, 8), dtype=np.uint32)
 
 
 def pack_nodes(dag: Dag):
@@ -373,8 +372,8 @@ def lower(dag: Dag, seed: int = 0, name: str = "", nw: Optional[int] = None) -> 
         if rc == -2:
             raise LoweringError(msg)
         raise ValueError(f"pfl_lower failed ({rc}): {msg}")
-    cv = consts[:nc.value].astype(np.uint64)
-    cvals = [sum(int(x) << (32 * j) for j, x in enumerate(row)) for row in cv]
+    raw = consts[:nc.value].astype("<u4").tobytes()
+    cvals = [int.from_bytes(raw[32 * i:32 * i + 32], "little") for i in range(nc.value)]
     return ir.PackedProgram(code[:ni.value].copy(), cvals, list(dag.vars), seed, name)
 
 

@@ -44,6 +44,12 @@ class GpuConfig:
     split: bool = True           # independence buckets
     hints: bool = True           # constraint-directed parent (hint) models
     cache_size: int = 1 << 16    # bucket witnesses kept
+    # re-evaluate every constraint of a multi-bucket set under the union of its bucket
+    # witnesses.  Off by default: each bucket witness is re-checked on exactly its bucket's
+    # constraints, and buckets share no symbol, array or inverse-keccak family
+    # (independence.py), so the union satisfies the set by construction; the tests switch
+    # it on to check that construction (tests/test_discharge.py).
+    recheck_union: bool = False
     # host lowering workers (spawned processes; terms re-intern on unpickling): used for a
     # call with at least `parallel_min` new buckets — the lowering is pure Python and was
     # 95 % of the corpus' wall time on one core
@@ -66,6 +72,7 @@ class GpuStats:
     kernel_ms: float = 0.0
     evals: int = 0
     host_s: float = 0.0      # lowering + hints + witness re-checks
+    phase_s: Dict[str, float] = field(default_factory=dict)  # wall time per check_sets phase
 
 
 STATS = GpuStats()
@@ -136,6 +143,22 @@ def _pool(n: int):
     return _POOL
 
 
+def _warm(_):
+    from . import to_dag  # noqa: F401  (the worker's imports, paid once)
+
+    return 0
+
+
+def warm_pool(cfg: Optional[GpuConfig] = None) -> int:
+    """Start the lowering workers now (a long-lived analysis pays their spawn once; a
+    latency-sensitive caller can do it up front).  Returns the worker count."""
+    cfg = cfg or CONFIG
+    n = max(1, cfg.workers)
+    if n > 1:
+        _pool(n).map(_warm, range(n), chunksize=1)
+    return n
+
+
 def _shutdown_pool() -> None:
     global _POOL
     if _POOL is not None:
@@ -178,6 +201,14 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
     # cached witness is only valid for the registry state it was found under
     reg_sig = tuple(sorted((n, s.lo, len(s.concrete)) for n, s in reg.keccak.items()))
     jobs, job_keys, pending = [], [], set()
+    phases: Dict[str, float] = {}
+    tp = [t0]
+
+    def lap(name):
+        now = time.perf_counter()
+        phases[name] = phases.get(name, 0.0) + now - tp[0]
+        tp[0] = now
+
     for i, cs in enumerate(sets):
         cs = [c for c in cs if c is not T.TRUE]
         if any(c is T.FALSE for c in cs):
@@ -204,8 +235,11 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
             jobs.append((b, parent))
             job_keys.append(key)
         set_buckets.append(ks)
+    lap("bucket")
     failed = set()
-    for key, (lo, prog, err) in zip(job_keys, _lower_all(jobs, reg, cfg)):
+    lowered_all = _lower_all(jobs, reg, cfg)
+    lap("lower")
+    for key, (lo, prog, err) in zip(job_keys, lowered_all):
         if err is not None:
             err = err.split(":")[0][:60]
             with _lock:
@@ -226,12 +260,14 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
         eng = get_engine()
         # one batch per device of the engine (cost-balanced shards), searched concurrently
         dbs = eng.upload_sharded(progs) if hasattr(eng, "upload_sharded") else [eng.upload(progs)]
+        lap("upload")
         if len(dbs) == 1:
             res = eng.check(dbs[0], budget=cfg.budget, seed=cfg.seed, flags=cfg.flags,
                             timeout_ms=cfg.timeout_ms)
         else:
             res = eng.check_many(dbs, budget=cfg.budget, seed=cfg.seed, flags=cfg.flags,
                                  timeout_ms=cfg.timeout_ms)
+        lap("search")
         sat = [k for k in range(len(progs)) if res.found[k] != 0xFFFFFFFF]
         vals_of = {}
         base = 0
@@ -244,6 +280,7 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
             base += len(db)
             db.free()
         vals = [vals_of[k] for k in sat]
+        lap("materialize")
         for k in range(len(progs)):
             found[keys[k]] = None
         if not res.timed_out:  # a deadline-cut search is not a complete answer
@@ -268,6 +305,7 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
                     _CACHE[key] = (lows[k], v)
                     while len(_CACHE) > cfg.cache_size:
                         _CACHE.popitem(last=False)
+        lap("recheck")
 
     n_sat = 0
     for i, ks in enumerate(set_buckets):
@@ -276,9 +314,14 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
         parts = [found.get(k) for k in ks]
         if any(p is None for p in parts):
             continue
-        w = Witness.union([Witness(lo, v, reg) for lo, v in parts], reg)
         cs = [c for c in sets[i] if c is not T.TRUE]
-        if all(w.ev(c) for c in cs):
+        # buckets() partitions every conjunct of the set: each bucket's witness was
+        # re-checked on exactly its conjuncts above (or when it entered the cache)
+        w = Witness.union([Witness(lo, v, reg) for lo, v in parts], reg)
+        ok = True
+        if cfg.recheck_union and len(parts) > 1:
+            ok = all(w.ev(c) for c in cs)
+        if ok:
             out[i] = WitnessModel(w, list(sets[i]))
             # per bucket: "hint" = candidate 0 of a hinted program (the host hint model),
             # "first" = candidate 0 of an unhinted one (the generator's first candidate),
@@ -288,7 +331,10 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
             kinds = {origin.get(k, "cache") for k in ks}
             out[i].origin = next((c for c in ("search", "hint", "first") if c in kinds), "cache")
             n_sat += 1
+    lap("models")
     with _lock:
+        for name, v in phases.items():
+            STATS.phase_s[name] = STATS.phase_s.get(name, 0.0) + v
         for o in origin.values():
             STATS.bucket_origin[o] = STATS.bucket_origin.get(o, 0) + 1
         STATS.sets += len(sets)

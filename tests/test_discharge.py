@@ -12,6 +12,7 @@ import pyoracle as O
 from mythril_amd import corpus
 from mythril_amd import keccak_manager as KM
 from mythril_amd.smt import gpu_check, symbol_factory
+from mythril_amd.smt import terms as T
 
 
 def _host_keccak(monkeypatch):
@@ -52,4 +53,25 @@ def test_labelled_unsat_never_sat_gpu(engine):
     unsat = corpus.labelled_unsat(c, n=256, seed=5)
     fps, n = _run(c, unsat)
     assert fps == [], fps[:3]
+    gpu_check.reset_cache()
+
+
+def test_union_of_bucket_witnesses_satisfies_the_set(monkeypatch):
+    """check_sets trusts the union of per-bucket re-checked witnesses (independence makes
+    it a model of the set); re-evaluating every constraint under the union changes nothing."""
+    _host_keccak(monkeypatch)
+    oracle_engine.install(monkeypatch)
+    monkeypatch.setattr(gpu_check.CONFIG, "budget", 1024)
+    c = corpus.build(6, 2, seed=23)
+    qs = [q.constraints for q in c.queries]
+    gpu_check.reset_cache()
+    fast = gpu_check.check_sets(qs, registry=c.kfm.registry)
+    gpu_check.reset_cache()
+    monkeypatch.setattr(gpu_check.CONFIG, "recheck_union", True)
+    full = gpu_check.check_sets(qs, registry=c.kfm.registry)
+    got = [m is not None for m in fast]
+    assert got == [m is not None for m in full] and sum(got) > len(qs) // 2
+    for m in fast:
+        if m is not None:
+            assert all(m.w.ev(cs) for cs in m.constraints if cs is not T.TRUE)
     gpu_check.reset_cache()
