@@ -81,7 +81,7 @@ class Lowerer {
    public:
     Lowerer(const Node* nodes, size_t n_nodes, const Const8* pool, size_t n_pool, int n_wregs)
         : N(nodes), nn(n_nodes), pool(pool), n_pool(n_pool), where(n_nodes, NONE),
-          slot_of(n_nodes, NONE), remat(n_nodes, -2), W(n_wregs, &where), B(PF_NB, &where) {
+          slot_of(n_nodes, NONE), remat(n_nodes, -2), cost(n_nodes, -1), W(n_wregs, &where), B(PF_NB, &where) {
         for (int s = PF_MAX_SPILL - 1; s >= 0; --s) free_slots.push_back(s);
     }
 
@@ -122,7 +122,7 @@ class Lowerer {
     size_t n_pool;
     std::vector<std::pair<bool, int>> events;  // (is_assert, node)
     std::vector<std::vector<int>> uses;
-    std::vector<int> where, slot_of, remat, free_slots;
+    std::vector<int> where, slot_of, remat, cost, free_slots;
     RegFile W, B;
 
     void order(const uint32_t* roots, size_t n_roots) {
@@ -186,6 +186,24 @@ class Lowerer {
         return res;
     }
 
+    // GPU price of re-emitting nd in cheap instructions (only for rematerialisable nd): a
+    // variable is a generator run, ~6 cheap ops (lower.py _VAR_REMAT_COST)
+    int remat_cost(int nd) {
+        if (cost[nd] >= 0) return cost[nd];
+        const Node& n = N[nd];
+        int c;
+        if (n.kind == PFL_K_VAR || n.kind == PFL_K_BVAR) {
+            c = 6;
+        } else if (is_leaf(n.kind)) {
+            c = 1;
+        } else {
+            c = 1;
+            for (uint32_t k = 0; k < n.nargs; ++k) c += remat_cost(n.args[k]);
+        }
+        cost[nd] = c;
+        return c;
+    }
+
     RegFile& rf_of(int nd) { return N[nd].is_bool ? B : W; }
 
     void emit(uint32_t op, uint32_t width, uint32_t dst, uint32_t a, uint32_t b, uint32_t c, uint32_t aux0) {
@@ -227,8 +245,8 @@ class Lowerer {
             for (int rg = 0; rg < rf.n; ++rg) {
                 const int nd = rf.holder[rg];
                 if (nd == NONE || ((pinned >> rg) & 1u)) continue;
-                const int sz = slot_of[nd] != NONE ? 1 : remat_size(nd);
-                if (sz == NONE) continue;
+                if (slot_of[nd] == NONE && remat_size(nd) == NONE) continue;
+                const int sz = slot_of[nd] != NONE ? 1 : remat_cost(nd);
                 const long long nu = -(long long)next_use(nd, t);
                 if (!have || sz < best_sz || (sz == best_sz && (nu < best_nu || (nu == best_nu && rg < best_r)))) {
                     have = true;

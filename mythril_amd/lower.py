@@ -261,6 +261,10 @@ class _RegFile:
 
 _REMAT_MAX = 6     # nodes re-emitted to restore one evicted interior value
 _REMAT_OPCOST = 16  # only cheap ops (compare/ite/logic/extract/concat) are recomputed
+# eviction price of re-emitting a variable, in cheap instructions: a generator run (three
+# Philox blocks + the strategy arms) measured ~6x a cheap op's time on the GPU, so under the
+# 7-register file a constant or a short recomputation is evicted before a variable
+_VAR_REMAT_COST = 6
 
 
 # ---- native lowering (libpflower.so, include/pf_lower.h) ----------------------------------
@@ -424,6 +428,22 @@ def lower_py(dag: Dag, seed: int = 0, name: str = "", nw: int = ir.NW) -> Progra
         remat_memo[nd] = res
         return res
 
+    cost_memo: Dict[int, int] = {}
+
+    def remat_cost(nd: int) -> int:
+        """GPU price of re-emitting nd (only called when remat_size(nd) is not None)."""
+        c = cost_memo.get(nd)
+        if c is None:
+            n = dag.nodes[nd]
+            if n.kind in (K_VAR, K_BVAR):
+                c = _VAR_REMAT_COST
+            elif n.kind in _LEAF_KINDS:
+                c = 1
+            else:
+                c = 1 + sum(remat_cost(a) for a in n.args)
+            cost_memo[nd] = c
+        return c
+
     W = _RegFile(nw, "W")
     B = _RegFile(ir.NB, "B")
     # spill slots (PF_W_SPILL / PF_B_SPILL): values that can neither stay resident nor be
@@ -434,11 +454,14 @@ def lower_py(dag: Dag, seed: int = 0, name: str = "", nw: int = ir.NW) -> Progra
 
     def rank(t):
         def f(nd):
-            sz = 1 if nd in slot_of else remat_size(nd)
-            if sz is None:
+            if nd in slot_of:
+                cost = 1
+            elif remat_size(nd) is None:
                 return None
+            else:
+                cost = remat_cost(nd)
             # cheapest restore first, then farthest next use (Belady)
-            return (sz, -next_use(nd, t))
+            return (cost, -next_use(nd, t))
         return f
 
     def spill(rg: int, nd: int) -> bool:
