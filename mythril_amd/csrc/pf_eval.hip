@@ -19,9 +19,10 @@
 
 using pf::u256;
 
-// profiling buckets: the 8 datapath units, EXP (8), W_CONST (9); slot = u64 index in the
-// launch's counter scratch; bucket PF_PROF_BUCKETS = whole-wave time
-#define PF_PROF_BUCKETS 10
+// profiling buckets: the 8 datapath units, EXP (8), W_CONST (9), waiting for the next
+// instruction's scalar fetch (10); slot = u64 index in the launch's counter scratch; bucket
+// PF_PROF_BUCKETS = whole-wave time
+#define PF_PROF_BUCKETS 11
 #define PF_PROF_SLOT 16
 
 // Register file: NREG wide registers (NREG - 1 usable + the write sink), limb-sliced into
@@ -315,6 +316,13 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
     uint4 In = S.code[0];
     uint32_t pc = 0;
     while (pc < S.n_ins) {
+#ifdef PF_PROFILE_UNITS
+        {
+            const uint64_t t_f = __builtin_amdgcn_s_memtime();
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the fetch of this instruction
+            prof_add(prof, 10u, __builtin_amdgcn_s_memtime() - t_f);
+        }
+#endif
         const uint4 I = In;
         const uint32_t op = I.x & 0xffu;
         const uint32_t w = (I.x >> 8) & 0x3ffu;
@@ -364,29 +372,40 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
             case PF_U_DIV: {
                 // ---- divider: bvudiv/bvurem/bvsdiv/bvsrem/bvsmod (SMT-LIB2 definitions on
                 // magnitudes) and bvumul_noovfl (a*b < 2^w  <=>  b == 0 || a <= (2^w-1)/b)
+                // The signed / overflow pre- and post-processing sit under wave-uniform branches
+                // on the opcode: computed for every division and selected away, the
+                // negations, the SMOD fix-up and the overflow compare cost ~70 VALU per
+                // unsigned division (config 3: 10.7 divisions per set).
                 const bool sgn = op >= PF_W_SDIV && op <= PF_W_SMOD;
-                const bool ovf = op == PF_B_UMUL_NOOVF;
-                const u256 xs = sgn ? sextw(x, w) : x;
-                const u256 ys = sgn ? sextw(y, w) : y;
-                const uint32_t sa = sgn ? (xs.l[7] >> 31) : 0u, sb = sgn ? (ys.l[7] >> 31) : 0u;
-                u256 ua = sa ? pf::neg256(xs) : xs;
-                if (ovf) {
+                u256 ua = x, ub = y;
+                uint32_t sa = 0u, sb = 0u;
+                if (sgn) {
+                    const u256 xs = sextw(x, w), ys = sextw(y, w);
+                    sa = xs.l[7] >> 31;
+                    sb = ys.l[7] >> 31;
+                    ua = sa ? pf::neg256(xs) : xs;
+                    ub = sb ? pf::neg256(ys) : ys;
+                    y = ys;
+                } else if (op == PF_B_UMUL_NOOVF) {
                     ua = pf::ones256();
                     maskw(ua, w);
                 }
-                const u256 ub = sb ? pf::neg256(ys) : ys;
                 u256 q, rr;
 #ifdef PF_DIAG_NO_DIV
                 q = ua; rr = ub;
 #else
                 pf::udivrem256(ua, ub, &q, &rr);
 #endif
-                const bool want_q = op == PF_W_UDIV || op == PF_W_SDIV;
-                const u256 v = want_q ? q : rr;
-                const uint32_t neg = want_q ? (sa ^ sb) : sa;
-                z = neg ? pf::neg256(v) : v;
-                if (op == PF_W_SMOD && !pf::iszero256(rr) && (sa ^ sb)) z = pf::add256(z, ys);
-                bres = pf::iszero256(y) || !pf::ult256(q, x);
+                if (op == PF_B_UMUL_NOOVF) {
+                    bres = pf::iszero256(y) || !pf::ult256(q, x);
+                } else if (!sgn) {
+                    z = op == PF_W_UDIV ? q : rr;
+                } else if (op == PF_W_SDIV) {
+                    z = (sa ^ sb) ? pf::neg256(q) : q;
+                } else {
+                    z = sa ? pf::neg256(rr) : rr;
+                    if (op == PF_W_SMOD && !pf::iszero256(rr) && (sa ^ sb)) z = pf::add256(z, y);
+                }
                 break;
             }
             case PF_U_SHIFT: {

@@ -19,7 +19,7 @@ from collections import Counter
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 PROF_SO = os.path.join(ROOT, "mythril_amd", "libpathfeas_prof.so")
-BUCKETS = ["ALU", "MUL", "DIV", "SHIFT", "GEN", "CMP", "BOOL", "END", "EXP", "CONST"]
+BUCKETS = ["ALU", "MUL", "DIV", "SHIFT", "GEN", "CMP", "BOOL", "END", "EXP", "CONST", "FETCH"]
 
 
 def build():
@@ -47,12 +47,13 @@ def run(args):
     db = eng.upload(progs)
     eng.check(db, budget=args.budget, seed=1, flags=ir.FLAG_COUNT_OPS)  # warm
     r = eng.check(db, budget=args.budget, seed=1, flags=ir.FLAG_COUNT_OPS)
-    out = (ctypes.c_uint64 * 11)()
+    nb = len(BUCKETS)
+    out = (ctypes.c_uint64 * (nb + 1))()
     _lib.check(L.pf_prof_read(db.handle, out), "pf_prof_read")
-    tot_ins = sum(out[:10])
-    wave = out[10]
+    tot_ins = sum(out[:nb])
+    wave = out[nb]
     res = {"kernel_ms": r.kernel_ms, "wave_cycles": wave, "instr_cycles": tot_ins,
-           "share": {BUCKETS[i]: round(out[i] / max(tot_ins, 1), 4) for i in range(10)},
+           "share": {BUCKETS[i]: round(out[i] / max(tot_ins, 1), 4) for i in range(len(BUCKETS))},
            "mix_per_set": {k: round(v / len(progs), 2) for k, v in mix.most_common()}}
     print(json.dumps(res, indent=1))
 
