@@ -14,7 +14,12 @@ SOURCES = ["pathfeas.hip", "pf_eval.hip", "pf_keccak.hip", "u256.h", "u256_cols.
            os.path.join("..", "..", "include", "pf_bytecode.h")]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-value"]
+# -structurizecfg-skip-uniform-regions: the interpreter loop's dispatch is wave-uniform (the
+# kernels keep every per-lane condition a select, pf_eval.hip / u256.h lane_mask), so the
+# structurizer may leave its regions as plain scalar branches instead of flag-driven flow
+# blocks (fewer SALU and branches per bytecode instruction)
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-value",
+         "-mllvm", "-structurizecfg-skip-uniform-regions=true"]
 
 
 def _stale() -> bool:

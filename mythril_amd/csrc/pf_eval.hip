@@ -96,7 +96,7 @@ PF_INL uint32_t ge_width(const u256& b, uint32_t w) {
     uint32_t hi = 0;
 #pragma unroll
     for (int i = 1; i < 8; i++) hi |= b.l[i];
-    return (hi != 0u) || (b.l[0] >= w);
+    return (uint32_t)(hi != 0u) | (uint32_t)(b.l[0] >= w);
 }
 
 PF_INL u256 pow2(uint32_t k) {  // 2^k, k < 256 (per lane)
@@ -115,6 +115,9 @@ PF_INL u256 pow2m1(uint32_t k) {  // 2^k - 1
     }
     return r;
 }
+
+// boundary-arm deltas (gen_var): entry j in bits 3j..3j+2, biased by 2
+#define PF_BND_DELTA 0x2ca281b1aull
 
 // ---- Philox4x32-10 -------------------------------------------------------------------
 // 32 x 32 -> 64 product as ONE v_mad_u64_u32 (addend 0): the backend otherwise emits a
@@ -164,7 +167,7 @@ PF_INL u256 gen_var(const SetCtx& S, uint32_t v, uint32_t cand) {
     // issue.  Its address is always in bounds: the pool carries one zero entry past its end
     // (pathfeas.hip), so a set without constants reads that.
     const uint32_t ai = m.y & 3u;
-    const bool act = kind == PF_VK_ACTOR && ai < hint1;
+    const uint32_t act = (uint32_t)(kind == PF_VK_ACTOR) & (uint32_t)(ai < hint1);
     const uint32_t ci = S.n_const ? (m.y % S.n_const) : 0u;
     const uint32_t* gp = S.consts + (size_t)(act ? hint0 + ai : ci) * 8u;
     u256 g;
@@ -216,8 +219,9 @@ PF_INL u256 gen_var(const SetCtx& S, uint32_t v, uint32_t cand) {
         {
             const uint32_t j = m.y % 12u, k = m.z % w;
             const uint32_t p = j <= 7u ? w - 1u : (j <= 10u ? k : 160u);
-            const int32_t delta = j < 4u ? (int32_t)j
-                                : (j == 5u ? -2 : ((j == 6u || j == 8u) ? 0 : (j == 10u ? 1 : -1)));
+            // delta by j, 3 bits per entry biased by 2 (a ternary chain here became a
+            // divergent if-chain): j 0..11 -> 0 1 2 3 -1 -2 0 -1 0 -1 1 -1
+            const int32_t delta = (int32_t)((PF_BND_DELTA >> (3u * j)) & 7ull) - 2;
             u256 base = pow2(p);
             const uint32_t usepow = j >= 6u ? 0xffffffffu : 0u;
             u256 dl;
@@ -254,9 +258,9 @@ PF_INL u256 gen_var(const SetCtx& S, uint32_t v, uint32_t cand) {
     // the parent model itself (candidate 0) and its neighbourhood (odd candidates keep the
     // parent value of most variables)
     if (has_parent) {
-        const bool keep = cand == 0u || ((cand & 1u) && (m.w & ((4u << ((cand >> 1) & 3u)) - 1u)) != 0u);
-#pragma unroll
-        for (int i = 0; i < 8; i++) out.l[i] = keep ? par.l[i] : out.l[i];
+        const uint32_t keep = (uint32_t)(cand == 0u) |
+                              ((cand & 1u) & (uint32_t)((m.w & ((4u << ((cand >> 1) & 3u)) - 1u)) != 0u));
+        out = pf::sel256(keep, par, out);
     }
     maskw(out, w);
     return out;
@@ -383,8 +387,8 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
                     const u256 xs = sextw(x, w), ys = sextw(y, w);
                     sa = xs.l[7] >> 31;
                     sb = ys.l[7] >> 31;
-                    ua = sa ? pf::neg256(xs) : xs;
-                    ub = sb ? pf::neg256(ys) : ys;
+                    ua = pf::sel256(sa, pf::neg256(xs), xs);
+                    ub = pf::sel256(sb, pf::neg256(ys), ys);
                     y = ys;
                 } else if (op == PF_B_UMUL_NOOVF) {
                     ua = pf::ones256();
@@ -397,14 +401,15 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
                 pf::udivrem256(ua, ub, &q, &rr);
 #endif
                 if (op == PF_B_UMUL_NOOVF) {
-                    bres = pf::iszero256(y) || !pf::ult256(q, x);
+                    bres = pf::iszero256(y) | (pf::ult256(q, x) ^ 1u);
                 } else if (!sgn) {
                     z = op == PF_W_UDIV ? q : rr;
                 } else if (op == PF_W_SDIV) {
-                    z = (sa ^ sb) ? pf::neg256(q) : q;
+                    z = pf::sel256(sa ^ sb, pf::neg256(q), q);
                 } else {
-                    z = sa ? pf::neg256(rr) : rr;
-                    if (op == PF_W_SMOD && !pf::iszero256(rr) && (sa ^ sb)) z = pf::add256(z, y);
+                    z = pf::sel256(sa, pf::neg256(rr), rr);
+                    if (op == PF_W_SMOD)  // uniform; the fix-up itself is a per-lane select
+                        z = pf::sel256((pf::iszero256(rr) ^ 1u) & (sa ^ sb), pf::add256(z, y), z);
                 }
                 break;
             }
@@ -426,7 +431,7 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
                     const u256 src = ar ? sextw(x, w) : x;
                     const uint32_t f = ar ? 0u - (src.l[7] >> 31) : 0u;
                     z = pf::shr256(src, big ? (ar ? 255u : 0u) : (amt & 255u), f);
-                    if (big && !ar) z = pf::zero256();
+                    if (!ar) z = pf::sel256(big, pf::zero256(), z);
                 }
                 break;
             }
@@ -464,7 +469,7 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
                         u256 sm = pf::add256c(x, y, &co);
                         u256 s2 = sm;
                         maskw(s2, w);  // no overflow iff the sum fits in w bits
-                        bres = (co == 0u) && pf::eq256(sm, s2);
+                        bres = (uint32_t)(co == 0u) & pf::eq256(sm, s2);
                         break;
                     }
                 }
@@ -616,7 +621,10 @@ PF_INL void check_body(const pf_set_desc* __restrict__ descs, const uint32_t* __
         uint64_t now = __builtin_amdgcn_s_memrealtime();
         uint64_t prev = __hip_atomic_load(t0_slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (prev == 0) prev = atomicCAS((unsigned long long*)t0_slot, 0ull, (unsigned long long)now);
-        t0 = prev ? prev : now;
+        // wave-uniform (both halves read from lane 0): the deadline exit stays a scalar branch
+        const uint64_t t = prev ? prev : now;
+        t0 = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)t) |
+             ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(t >> 32)) << 32);
     }
     UnitProf prof;
 #pragma unroll
@@ -647,8 +655,8 @@ PF_INL void check_body(const pf_set_desc* __restrict__ descs, const uint32_t* __
         uint32_t sat = run_program<MODE_GEN, NREG>(S, cand, active, flags, nullptr, 0u, exp_tbl, &complete,
                                              &lane_ops, &prof);
         const uint64_t m_act = __ballot(active);
-        const uint64_t m_sat = __ballot(active && sat);
-        const uint64_t m_full = __ballot(active && complete);
+        const uint64_t m_sat = __ballot((uint32_t)active & sat);
+        const uint64_t m_full = __ballot((uint32_t)active & complete);
         decided += __popcll(m_act);
         evals_full += __popcll(m_full);
         ops += lane_ops * (uint64_t)__popcll(m_act);
