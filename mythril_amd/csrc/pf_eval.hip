@@ -312,14 +312,15 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
     // keeps them in private scratch memory, never in the VGPR banks
     uint32_t spill[PF_MAX_SPILL * 8];
 #define BGET(r) ((Bk >> ((r) & 31u)) & 1u)
-    uint32_t root = 1u;
+    uint32_t root = 1u, sc = 0u;
     uint64_t cost = 0;
-    *complete = 0u;
-    // Software-pipelined fetch: the scalar load of instruction pc+1 is issued while
-    // instruction pc executes (the last slot re-reads END, never past the program).
-    uint4 In = S.code[0];
-    uint32_t pc = 0;
-    while (pc < S.n_ins) {
+    // Software-pipelined fetch: the scalar load of instruction i+1 is issued while
+    // instruction i executes.  The loop ends at PF_END (pf_batch_create checks that every
+    // program ends with it), which is decoded before the next fetch, so no load reads past
+    // the program and the loop needs no instruction counter.
+    const uint4* ip = S.code;
+    uint4 In = *ip;
+    for (;;) {
 #ifdef PF_PROFILE_UNITS
         {
             const uint64_t t_f = __builtin_amdgcn_s_memtime();
@@ -339,19 +340,17 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
 #ifdef PF_PROFILE_UNITS
         const uint64_t t_ins = __builtin_amdgcn_s_memtime();
 #endif
+        if (unit == PF_U_END) break;
         // Issue the next fetch only after this instruction's words are decoded: scalar
         // loads return out of order, so a fetch issued before the decode would be waited
         // for together with the one being consumed (lgkmcnt(0)).
         __builtin_amdgcn_sched_barrier(0);
-        In = S.code[min(pc + 1u, S.n_ins - 1u)];
-        pc++;
-        if (unit == PF_U_END) {
-            *complete = 1u;
-            break;
-        }
+        In = *(++ip);
         u256 x, y, z;
-        if (tr & PF_TR_RA) RD_W(x, W, min(a, NREG - 1u), LPB);
-        if (tr & PF_TR_RB) RD_W(y, W, min(b, NREG - 1u), LPB);
+        // register indices are trusted: pf_batch_create checks every read and write
+        // against the register file of the kernel that runs the set
+        if (tr & PF_TR_RA) RD_W(x, W, a, LPB);
+        if (tr & PF_TR_RB) RD_W(y, W, b, LPB);
         uint32_t bres = 0;  // bool result for B ops
         // Dispatch on the datapath unit (w0 bits 21..23) first.  The heavy datapaths exist
         // once each (multiplier, divider, shifter, generator) and are shared by every
@@ -489,8 +488,12 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
                     case PF_B_SPILL: spill[(aux & (PF_MAX_SPILL - 1u)) * 8u] = BGET(a); break;
                     default:  // PF_ASSERT
                         root &= BGET(a);
-                        if ((flags & PF_FLAG_SHORTCIRCUIT) && __ballot(root && active) == 0ull)
-                            pc = S.n_ins;  // every lane of the wave is decided: leave the program
+                        if ((flags & PF_FLAG_SHORTCIRCUIT) && __ballot(root & (uint32_t)active) == 0ull) {
+                            // every lane of the wave is decided: leave the program (the
+                            // next instruction becomes END; the fetch in flight is dropped)
+                            In = make_uint4(PF_U_END << 21, 0u, 0u, 0u);
+                            sc = 1u;
+                        }
                         break;
                 }
                 break;
@@ -552,8 +555,12 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
             // PF_W_SINK.  A conditional insert would make the loop-carried banks a phi of
             // old/new values, which costs a full bank copy (~100 extra VGPRs, spills).
             maskw(z, w);
-            const uint32_t dd = (tr & PF_TR_WW) ? min(d, NREG - 1u) : (uint32_t)(NREG - 1);
+            const uint32_t dd = (tr & PF_TR_WW) ? d : (uint32_t)(NREG - 1);
+            // keep the 8 indexed moves one s_set_gpr_idx block: the scheduler otherwise
+            // interleaves the B update into it and re-enters indexing mode per move
+            __builtin_amdgcn_sched_barrier(0);
             WR_W(W, dd, z, LPB);
+            __builtin_amdgcn_sched_barrier(0);
         }
         if (PF_OP_WRITES_B(op)) {
             const uint32_t bit = 1u << (d & 31u);
@@ -566,6 +573,7 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
         (void)prof;
 #endif
     }
+    *complete = sc ^ 1u;
     *ops += cost;
     return root;
 #undef BGET

@@ -31,6 +31,16 @@ def main():
     subprocess.check_call([CLANG, "-O2", "-std=c++17", *extra, "-o", exe, os.path.join(HERE, "u256_host_check.cpp")])
     rng = random.Random(1234)
     cases = [(vals(rng), vals(rng)) for _ in range(n)]
+    # adversarial divisions: a = b q + r with the remainder at the edges (r = 0, 1, b - 1,
+    # b - 2) and b, q of every limb length, so quotient-digit estimates land right at an
+    # integer boundary (the biased estimate's add-back path, and exact multiples)
+    for _ in range(n // 2):
+        b = rng.getrandbits(rng.randrange(1, 257)) | 1
+        q = rng.getrandbits(rng.randrange(1, 257))
+        r = rng.choice([0, 1, b - 1, b - 2, rng.randrange(b)]) % b
+        a = b * q + r
+        if a <= M:
+            cases.append((a, b))
     inp = "".join(f"x {a:064x} {b:064x}\n" for a, b in cases)
     out = subprocess.run([exe], input=inp, capture_output=True, text=True, check=True).stdout.split("\n")
     bad = 0
