@@ -70,10 +70,29 @@ PF_INL uint32_t limb_mask(uint32_t w, int i) {
     return __builtin_amdgcn_readfirstlane(m);
 }
 
+// Re-mask a W result to width w (wave-uniform).  A switch on the top limb: the limbs
+// above it are zeroed and only the top limb is and-ed — per-limb masks formed with scalar
+// selects cost ~35 SALU per narrow op.
 PF_INL void maskw(u256& x, uint32_t w) {
     if (w < 256u) {
-#pragma unroll
-        for (int i = 0; i < 8; i++) x.l[i] &= limb_mask(w, i);
+        const uint32_t r = w & 31u;
+        const uint32_t top = r ? ((1u << r) - 1u) : 0xffffffffu;
+#define PF_MASK_CASE(K)                                                   \
+    case K:                                                               \
+        x.l[K] &= top;                                                    \
+        _Pragma("unroll") for (int i_ = K + 1; i_ < 8; i_++) x.l[i_] = 0u; \
+        break;
+        switch ((w - 1u) >> 5) {
+            PF_MASK_CASE(0)
+            PF_MASK_CASE(1)
+            PF_MASK_CASE(2)
+            PF_MASK_CASE(3)
+            PF_MASK_CASE(4)
+            PF_MASK_CASE(5)
+            PF_MASK_CASE(6)
+            default: x.l[7] &= top; break;
+        }
+#undef PF_MASK_CASE
     }
 }
 
@@ -312,6 +331,18 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
     // keeps them in private scratch memory, never in the VGPR banks
     uint32_t spill[PF_MAX_SPILL * 8];
 #define BGET(r) ((Bk >> ((r) & 31u)) & 1u)
+#define BSET(r, v) (Bk = (Bk & ~(1u << ((r) & 31u))) | (((v) & 1u) << ((r) & 31u)))
+    // Ops with a B result (compares, bool logic, B_VAR, UMUL_NOOVF) set their bit and skip
+    // the W write-back: a uniform branch to the loop latch.
+#ifdef PF_PROFILE_UNITS
+#define PF_NEXT()                                                                      \
+    {                                                                                  \
+        prof_add(prof, unit, __builtin_amdgcn_s_memtime() - t_ins);                    \
+        continue;                                                                      \
+    }
+#else
+#define PF_NEXT() continue
+#endif
     uint32_t root = 1u, sc = 0u;
     uint64_t cost = 0;
     // Software-pipelined fetch: the scalar load of instruction i+1 is issued while
@@ -351,7 +382,6 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
         // against the register file of the kernel that runs the set
         if (tr & PF_TR_RA) RD_W(x, W, a, LPB);
         if (tr & PF_TR_RB) RD_W(y, W, b, LPB);
-        uint32_t bres = 0;  // bool result for B ops
         // Dispatch on the datapath unit (w0 bits 21..23) first.  The heavy datapaths exist
         // once each (multiplier, divider, shifter, generator) and are shared by every
         // opcode that needs them: the kernel's code must stay small enough for the
@@ -400,7 +430,8 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
                 pf::udivrem256(ua, ub, &q, &rr);
 #endif
                 if (op == PF_B_UMUL_NOOVF) {
-                    bres = pf::iszero256(y) | (pf::ult256(q, x) ^ 1u);
+                    BSET(d, pf::iszero256(y) | (pf::ult256(q, x) ^ 1u));
+                    PF_NEXT();
                 } else if (!sgn) {
                     z = op == PF_W_UDIV ? q : rr;
                 } else if (op == PF_W_SDIV) {
@@ -447,10 +478,14 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
                     for (int i = 0; i < 8; i++)
                         z.l[i] = active ? soa[((size_t)aux * 8u + i) * soa_n + cand] : 0u;
                 }
-                bres = z.l[0] & 1u;
                 PF_WAIT_ALL();
+                if (op == PF_B_VAR) {
+                    BSET(d, z.l[0]);
+                    PF_NEXT();
+                }
                 break;
-            case PF_U_CMP:
+            case PF_U_CMP: {
+                uint32_t bres;
                 switch (op) {
                     case PF_B_EQ: bres = pf::eq256(x, y); break;
                     case PF_B_ULT: bres = pf::ult256(x, y); break;
@@ -472,17 +507,19 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
                         break;
                     }
                 }
-                break;
+                BSET(d, bres);
+                PF_NEXT();
+            }
             case PF_U_BOOL:
                 switch (op) {
-                    case PF_B_CONST: bres = aux & 1u; break;
-                    case PF_B_AND: bres = BGET(a) & BGET(b); break;
-                    case PF_B_OR: bres = BGET(a) | BGET(b); break;
-                    case PF_B_XOR: bres = BGET(a) ^ BGET(b); break;
-                    case PF_B_NOT: bres = BGET(a) ^ 1u; break;
-                    case PF_B_ITE: bres = BGET(c) ? BGET(a) : BGET(b); break;
+                    case PF_B_CONST: BSET(d, aux); break;
+                    case PF_B_AND: BSET(d, BGET(a) & BGET(b)); break;
+                    case PF_B_OR: BSET(d, BGET(a) | BGET(b)); break;
+                    case PF_B_XOR: BSET(d, BGET(a) ^ BGET(b)); break;
+                    case PF_B_NOT: BSET(d, BGET(a) ^ 1u); break;
+                    case PF_B_ITE: BSET(d, BGET(c) ? BGET(a) : BGET(b)); break;
                     case PF_B_FILL:
-                        bres = spill[(aux & (PF_MAX_SPILL - 1u)) * 8u] & 1u;
+                        BSET(d, spill[(aux & (PF_MAX_SPILL - 1u)) * 8u]);
                         PF_WAIT_ALL();
                         break;
                     case PF_B_SPILL: spill[(aux & (PF_MAX_SPILL - 1u)) * 8u] = BGET(a); break;
@@ -496,7 +533,7 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
                         }
                         break;
                 }
-                break;
+                PF_NEXT();
             default:  // PF_U_ALU
                 switch (op) {
                     case PF_W_ADD: z = pf::add256(x, y); break;
@@ -551,9 +588,8 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
                 break;
         }
         {
-            // Unconditional write: ops without a W result write the sink register
-            // PF_W_SINK.  A conditional insert would make the loop-carried banks a phi of
-            // old/new values, which costs a full bank copy (~100 extra VGPRs, spills).
+            // W write-back of every op that reaches here (ops without a W result other than
+            // the B ops above — W_SPILL — write the sink register PF_W_SINK)
             maskw(z, w);
             const uint32_t dd = (tr & PF_TR_WW) ? d : (uint32_t)(NREG - 1);
             // keep the 8 indexed moves one s_set_gpr_idx block: the scheduler otherwise
@@ -561,10 +597,6 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
             __builtin_amdgcn_sched_barrier(0);
             WR_W(W, dd, z, LPB);
             __builtin_amdgcn_sched_barrier(0);
-        }
-        if (PF_OP_WRITES_B(op)) {
-            const uint32_t bit = 1u << (d & 31u);
-            Bk = (Bk & ~bit) | (bres ? bit : 0u);
         }
 #ifdef PF_PROFILE_UNITS
         prof_add(prof, op == PF_W_EXP ? 8u : (op == PF_W_CONST ? 9u : unit),

@@ -24,8 +24,9 @@ BUCKETS = ["ALU", "MUL", "DIV", "SHIFT", "GEN", "CMP", "BOOL", "END", "EXP", "CO
 
 def build():
     csrc = os.path.join(ROOT, "mythril_amd", "csrc")
-    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
-                    "-shared", "-Wno-unused-value", "-DPF_PROFILE_UNITS", "-o", PROF_SO,
+    from mythril_amd.build import FLAGS, HIPCC  # the product's flags + the profiling define
+
+    subprocess.run([HIPCC, *FLAGS, "-DPF_PROFILE_UNITS", "-o", PROF_SO,
                     os.path.join(csrc, "pathfeas.hip")], check=True, cwd=csrc)
     print(PROF_SO)
 
