@@ -22,7 +22,7 @@ using pf::u256;
 // profiling buckets: the 8 datapath units, EXP (8), W_CONST (9), waiting for the next
 // instruction's scalar fetch (10); slot = u64 index in the launch's counter scratch; bucket
 // PF_PROF_BUCKETS = whole-wave time
-#define PF_PROF_BUCKETS 11
+#define PF_PROF_BUCKETS 15  // + DIV by udivrem256 path: 11 zero, 12 short, 13 one-digit, 14 general
 #define PF_PROF_SLOT 16
 
 // Register file: NREG wide registers (NREG - 1 usable + the write sink), limb-sliced into
@@ -337,7 +337,7 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
 #ifdef PF_PROFILE_UNITS
 #define PF_NEXT()                                                                      \
     {                                                                                  \
-        prof_add(prof, unit, __builtin_amdgcn_s_memtime() - t_ins);                    \
+        prof_add(prof, pbucket, __builtin_amdgcn_s_memtime() - t_ins);                 \
         continue;                                                                      \
     }
 #else
@@ -370,6 +370,7 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
         cost += I.w;
 #ifdef PF_PROFILE_UNITS
         const uint64_t t_ins = __builtin_amdgcn_s_memtime();
+        uint32_t pbucket = op == PF_W_EXP ? 8u : (op == PF_W_CONST ? 9u : unit);
 #endif
         if (unit == PF_U_END) break;
         // Issue the next fetch only after this instruction's words are decoded: scalar
@@ -424,6 +425,14 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
                     maskw(ua, w);
                 }
                 u256 q, rr;
+#ifdef PF_PROFILE_UNITS
+                {
+                    const uint32_t bz = pf::iszero256(ub);
+                    pbucket = !pf::wave_any((bz ^ 1u) & (pf::ult256(ua, ub) ^ 1u)) ? 11u
+                            : !pf::wave_any((ub.l[1] | ub.l[2] | ub.l[3] | ub.l[4] | ub.l[5] | ub.l[6] | ub.l[7]) != 0u) ? 12u
+                            : !pf::wave_any((bz ^ 1u) & (uint32_t)(pf::clz256(ub) > pf::clz256(ua) + 31u)) ? 13u : 14u;
+                }
+#endif
 #ifdef PF_DIAG_NO_DIV
                 q = ua; rr = ub;
 #else
@@ -599,8 +608,7 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
             __builtin_amdgcn_sched_barrier(0);
         }
 #ifdef PF_PROFILE_UNITS
-        prof_add(prof, op == PF_W_EXP ? 8u : (op == PF_W_CONST ? 9u : unit),
-                 __builtin_amdgcn_s_memtime() - t_ins);
+        prof_add(prof, pbucket, __builtin_amdgcn_s_memtime() - t_ins);
 #else
         (void)prof;
 #endif

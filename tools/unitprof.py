@@ -19,7 +19,8 @@ from collections import Counter
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 PROF_SO = os.path.join(ROOT, "mythril_amd", "libpathfeas_prof.so")
-BUCKETS = ["ALU", "MUL", "DIV", "SHIFT", "GEN", "CMP", "BOOL", "END", "EXP", "CONST", "FETCH"]
+BUCKETS = ["ALU", "MUL", "DIV", "SHIFT", "GEN", "CMP", "BOOL", "END", "EXP", "CONST", "FETCH",
+           "DIV_zero", "DIV_short", "DIV_onedigit", "DIV_general"]
 
 
 def build():
