@@ -96,6 +96,11 @@ enum pf_opcode {
     PF_NUM_OPCODES = 64
 };
 
+/* w0 bit 24 on a compare or bool op: also PF_ASSERT its B result.  Set only by
+ * pf_batch_create's peephole (an ASSERT of the B register the previous instruction wrote),
+ * never by the host lowering, whose programs the oracles evaluate as written. */
+#define PF_I_ASSERT (1u << 24)
+
 /* operand traffic bits (w0 >> 18): reads W[a], reads W[b], writes W[d] */
 #define PF_TR_RA 1u
 #define PF_TR_RB 2u

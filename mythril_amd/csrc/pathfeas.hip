@@ -196,7 +196,7 @@ int check_enqueue(Batch* B, uint64_t gseed, uint32_t budget, uint32_t flags, uin
     unsigned long long* d_counters = reinterpret_cast<unsigned long long*>(B->d_scratch);
     uint64_t* d_t0 = reinterpret_cast<uint64_t*>(B->d_scratch + 8);
 #ifdef PF_PROFILE_UNITS
-    HIPCHK(hipMemsetAsync(B->d_scratch, 0, 256, st));
+    HIPCHK(hipMemsetAsync(B->d_scratch, 0, 512, st));
 #else
     HIPCHK(hipMemsetAsync(B->d_scratch, 0, 64, st));
 #endif
@@ -400,7 +400,38 @@ int pf_batch_create_on(int device, const uint32_t* code, size_t n_ins, const uin
             if (bres) bdef |= 1u << (rd & 31u);
         }
     }
-    code = code_fixed.data();
+    // Peephole (semantics-preserving): an ASSERT of the B register that the instruction just
+    // before it wrote — a compare or a bool op, the shape every root takes — becomes the
+    // PF_I_ASSERT flag of that instruction, one dispatched instruction less per asserted
+    // root.  The caller's arrays are unchanged; the device gets the compacted
+    // program with shifted code ranges.
+    std::vector<uint32_t> code_out;
+    code_out.reserve(code_fixed.size());
+    std::vector<pf_set_desc> descs_out(descs, descs + n_sets);
+    for (size_t s = 0; s < n_sets; s++) {
+        pf_set_desc& d = descs_out[s];
+        const uint32_t* src = code_fixed.data() + 4 * (size_t)d.code_off;
+        const size_t first = code_out.size() / 4;
+        for (uint32_t i = 0; i < d.n_ins; i++) {
+            const uint32_t* I = src + 4 * (size_t)i;
+            const uint32_t op = I[0] & 0xffu;
+            if (op == PF_ASSERT && code_out.size() / 4 > first) {
+                uint32_t* P = code_out.data() + code_out.size() - 4;
+                const uint32_t pop = P[0] & 0xffu, unit = pf_op_unit(pop);
+                if ((unit == PF_U_CMP || (unit == PF_U_BOOL && pop != PF_ASSERT && pop != PF_B_SPILL)) &&
+                    !(P[0] & PF_I_ASSERT) && (P[1] & 0xffu) == ((I[1] >> 8) & 0xffu)) {
+                    P[0] |= PF_I_ASSERT;
+                    continue;
+                }
+            }
+            code_out.insert(code_out.end(), I, I + 4);
+        }
+        d.code_off = (uint32_t)first;
+        d.n_ins = (uint32_t)(code_out.size() / 4 - first);
+    }
+    code = code_out.data();
+    n_ins = code_out.size() / 4;
+    descs = descs_out.data();
     // Longest-first wave order: waves are dispatched in index order, so mapping the first
     // waves to the most expensive sets leaves the cheap ones for the last, partly filled
     // round.  Weights are measured SIMD cycles per instruction relative to a cheap op
@@ -431,7 +462,7 @@ int pf_batch_create_on(int device, const uint32_t* code, size_t n_ins, const uin
     const size_t o_code = 0, o_const = o_code + al(n_ins * 16), o_schema = o_const + al(n_const * 32 + 32),
                  o_par = o_schema + al(n_vars * 16), o_desc = o_par + al(n_parents * 32),
                  o_order = o_desc + al(n_sets * sizeof(pf_set_desc)), o_found = o_order + al(n_sets * 4),
-                 o_scr = o_found + al(std::max<size_t>(n_sets, 1) * 4), total = o_scr + 256;
+                 o_scr = o_found + al(std::max<size_t>(n_sets, 1) * 4), total = o_scr + 512;
     std::vector<uint8_t> stage(o_found, 0);  // found / scratch are cleared by every search
     auto put = [&](size_t off, const void* src, size_t bytes) {
         if (bytes && src) memcpy(stage.data() + off, src, bytes);

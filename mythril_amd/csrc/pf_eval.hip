@@ -22,7 +22,8 @@ using pf::u256;
 // profiling buckets: the 8 datapath units, EXP (8), W_CONST (9), waiting for the next
 // instruction's scalar fetch (10); slot = u64 index in the launch's counter scratch; bucket
 // PF_PROF_BUCKETS = whole-wave time
-#define PF_PROF_BUCKETS 15  // + DIV by udivrem256 path: 11 zero, 12 short, 13 one-digit, 14 general
+#define PF_PROF_BUCKETS 18  // + DIV by udivrem256 path: 11 zero, 12 short, 13 one-digit, 14 general;
+                            // EXP parts: 15 window, 16 t recurrence, 17 Horner + product
 #define PF_PROF_SLOT 16
 
 // Register file: NREG wide registers (NREG - 1 usable + the write sink), limb-sliced into
@@ -334,6 +335,17 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
 #define BSET(r, v) (Bk = (Bk & ~(1u << ((r) & 31u))) | (((v) & 1u) << ((r) & 31u)))
     // Ops with a B result (compares, bool logic, B_VAR, UMUL_NOOVF) set their bit and skip
     // the W write-back: a uniform branch to the loop latch.
+    // PF_ASSERT (or a PF_I_ASSERT-flagged B op): and the lane's bit into the root; with
+    // PF_FLAG_SHORTCIRCUIT a wave whose every lane is decided leaves the program (the next
+    // instruction becomes END; the fetch in flight is dropped)
+#define PF_DO_ASSERT(v)                                                                       \
+    do {                                                                                      \
+        root &= (v);                                                                          \
+        if ((flags & PF_FLAG_SHORTCIRCUIT) && __ballot(root & (uint32_t)active) == 0ull) {   \
+            In = make_uint4(PF_U_END << 21, 0u, 0u, 0u);                                      \
+            sc = 1u;                                                                          \
+        }                                                                                     \
+    } while (0)
 #ifdef PF_PROFILE_UNITS
 #define PF_NEXT()                                                                      \
     {                                                                                  \
@@ -398,7 +410,11 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
 #ifdef PF_DIAG_NO_EXP
                     z = pf::add256(x, y);
 #else
+#ifdef PF_PROFILE_UNITS
+                    z = pf::exp256_split(x, y, exp_tbl, 64u, &prof->c[15]);
+#else
                     z = pf::exp256_split(x, y, exp_tbl, 64u);
+#endif
 #endif
                     PF_WAIT_ALL();
                 }
@@ -517,6 +533,7 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
                     }
                 }
                 BSET(d, bres);
+                if (I.x & PF_I_ASSERT) PF_DO_ASSERT(bres);
                 PF_NEXT();
             }
             case PF_U_BOOL:
@@ -533,15 +550,10 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
                         break;
                     case PF_B_SPILL: spill[(aux & (PF_MAX_SPILL - 1u)) * 8u] = BGET(a); break;
                     default:  // PF_ASSERT
-                        root &= BGET(a);
-                        if ((flags & PF_FLAG_SHORTCIRCUIT) && __ballot(root & (uint32_t)active) == 0ull) {
-                            // every lane of the wave is decided: leave the program (the
-                            // next instruction becomes END; the fetch in flight is dropped)
-                            In = make_uint4(PF_U_END << 21, 0u, 0u, 0u);
-                            sc = 1u;
-                        }
-                        break;
+                        PF_DO_ASSERT(BGET(a));
+                        PF_NEXT();
                 }
+                if (I.x & PF_I_ASSERT) PF_DO_ASSERT(BGET(d));
                 PF_NEXT();
             default:  // PF_U_ALU
                 switch (op) {
@@ -671,8 +683,9 @@ PF_INL void check_body(const pf_set_desc* __restrict__ descs, const uint32_t* __
         if (prev == 0) prev = atomicCAS((unsigned long long*)t0_slot, 0ull, (unsigned long long)now);
         // wave-uniform (both halves read from lane 0): the deadline exit stays a scalar branch
         const uint64_t t = prev ? prev : now;
-        t0 = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)t) |
-             ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(t >> 32)) << 32);
+        // (readfirstlane returns int: go through uint32_t, or the low half sign-extends)
+        t0 = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)t) |
+             ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(t >> 32)) << 32);
     }
     UnitProf prof;
 #pragma unroll

@@ -56,7 +56,7 @@ def main():
     gen_cls = collections.Counter()
     gen_multi_maxdig = collections.Counter()
     gen_multi_span = collections.Counter()
-    work_uniform = work_lane = work_nmax = work_split = 0
+    work_uniform = work_lane = work_nmax = work_split = work_nbound = work_two = work_pow = 0
     for s in range(n_dags):
         sv = po.SetView.from_batch(batch, s)
         for wv in range(waves):
@@ -105,6 +105,11 @@ def main():
                     work_uniform += sum(9 - j for j in digs)
                     for j in digs:
                         work_nmax += max(limbs(b) for (a, b) in live if ((a // b) >> (32 * j)) & 0xFFFFFFFF) + 1
+                    for j in digs:
+                        nb = 1 + max(limbs(b) for (a, b) in live if limbs(b) <= 8 - j)
+                        work_two += 2 if nb <= 2 else 9 - j
+                        work_pow += min(9 - j, 2 if nb <= 2 else (5 if nb <= 5 else 9))
+                        work_nbound += min(9 - j, 1 + max(limbs(b) for (a, b) in live if limbs(b) <= 8 - j))
                     sh = [(a, b) for (a, b) in live if b >= 2**32]
                     dg = set(j for (a, b) in sh for j in range(8) if ((a // b) >> (32 * j)) & 0xFFFFFFFF)
                     work_split += sum(9 - j for j in dg)
@@ -123,6 +128,7 @@ def main():
     print("general: multi lanes' max quotient span (digits)", sorted(gen_multi_span.items()))
     print("general: limb-steps, uniform (9-j per digit) vs widest lane only:", work_uniform, work_lane)
     print("general: limb-steps with per-digit width n_max_j + 1:", work_nmax, " short lanes split off:", work_split)
+    print("general: limb-steps with width 1 + max{n <= 8 - j} over live lanes:", work_nbound, "two widths {2, 9-j}:", work_two, "three widths {2,5,9}:", work_pow)
 
 
 if __name__ == "__main__":

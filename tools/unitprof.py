@@ -20,7 +20,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 PROF_SO = os.path.join(ROOT, "mythril_amd", "libpathfeas_prof.so")
 BUCKETS = ["ALU", "MUL", "DIV", "SHIFT", "GEN", "CMP", "BOOL", "END", "EXP", "CONST", "FETCH",
-           "DIV_zero", "DIV_short", "DIV_onedigit", "DIV_general"]
+           "DIV_zero", "DIV_short", "DIV_onedigit", "DIV_general", "EXP_window", "EXP_t", "EXP_horner"]
 
 
 def build():
@@ -52,7 +52,7 @@ def run(args):
     nb = len(BUCKETS)
     out = (ctypes.c_uint64 * (nb + 1))()
     _lib.check(L.pf_prof_read(db.handle, out), "pf_prof_read")
-    tot_ins = sum(out[:nb])
+    tot_ins = sum(out[:15])  # the EXP_* buckets are parts of EXP
     wave = out[nb]
     res = {"kernel_ms": r.kernel_ms, "wave_cycles": wave, "instr_cycles": tot_ins,
            "share": {BUCKETS[i]: round(out[i] / max(tot_ins, 1), 4) for i in range(len(BUCKETS))},
