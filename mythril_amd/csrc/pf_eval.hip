@@ -154,7 +154,9 @@ PF_INL uint4 philox(uint4 c, uint32_t k0, uint32_t k1) {
         const uint64_t p0 = mul_wide(c.x, PF_PHILOX_M0), p1 = mul_wide(c.z, PF_PHILOX_M1);
         const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
         const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
-        c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
+        // the two 3-input xors as one v_bitop3_b32 each (truth table 0x96)
+        c = make_uint4(__builtin_amdgcn_bitop3_b32(hi1, c.y, k0, (unsigned char)0x96), lo1,
+                       __builtin_amdgcn_bitop3_b32(hi0, c.w, k1, (unsigned char)0x96), lo0);
         k0 += PF_PHILOX_W0;
         k1 += PF_PHILOX_W1;
     }
