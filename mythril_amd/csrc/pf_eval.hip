@@ -75,7 +75,7 @@ PF_INL uint32_t limb_mask(uint32_t w, int i) {
 // above it are zeroed and only the top limb is and-ed — per-limb masks formed with scalar
 // selects cost ~35 SALU per narrow op.
 PF_INL void maskw(u256& x, uint32_t w) {
-    if (w < 256u) {
+    if (__builtin_expect(w < 256u, 0)) {
         const uint32_t r = w & 31u;
         const uint32_t top = r ? ((1u << r) - 1u) : 0xffffffffu;
 #define PF_MASK_CASE(K)                                                   \
@@ -386,7 +386,9 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
         const uint64_t t_ins = __builtin_amdgcn_s_memtime();
         uint32_t pbucket = op == PF_W_EXP ? 8u : (op == PF_W_CONST ? 9u : unit);
 #endif
-        if (unit == PF_U_END) break;
+        // branch hints: every taken scalar branch refetches the wave's instruction buffer, so
+        // the common path (not END, operands read) is laid out as the fall-through
+        if (__builtin_expect(unit == PF_U_END, 0)) break;
         // Issue the next fetch only after this instruction's words are decoded: scalar
         // loads return out of order, so a fetch issued before the decode would be waited
         // for together with the one being consumed (lgkmcnt(0)).
@@ -395,8 +397,8 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
         u256 x, y, z;
         // register indices are trusted: pf_batch_create checks every read and write
         // against the register file of the kernel that runs the set
-        if (tr & PF_TR_RA) RD_W(x, W, a, LPB);
-        if (tr & PF_TR_RB) RD_W(y, W, b, LPB);
+        if (__builtin_expect((tr & PF_TR_RA) != 0u, 1)) RD_W(x, W, a, LPB);
+        if (__builtin_expect((tr & PF_TR_RB) != 0u, 1)) RD_W(y, W, b, LPB);
         // Dispatch on the datapath unit (w0 bits 21..23) first.  The heavy datapaths exist
         // once each (multiplier, divider, shifter, generator) and are shared by every
         // opcode that needs them: the kernel's code must stay small enough for the
