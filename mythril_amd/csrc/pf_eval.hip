@@ -237,14 +237,17 @@ PF_INL u256 gen_var(const SetCtx& S, uint32_t v, uint32_t cand) {
         }
         // boundary arm (sel 5..8): {0, 1, 2, 3, 2^w-1, 2^w-2, 2^(w-1), 2^(w-1)-1, 2^k, 2^k-1,
         // 2^k+1, 2^160-1}[j] mod 2^w as one formula, (j >= 6 ? 2^p : 0) + delta
+        // one power of two serves both the boundary arm (2^p) and the parent-mutation arm
+        // (2^k, k = m[2] % w): a lane takes one arm, so the exponent is selected per lane
+        const uint32_t j = m.y % 12u, k = m.z % w;
+        const uint32_t p = j <= 7u ? w - 1u : (j <= 10u ? k : 160u);
+        const u256 pw = pow2(sel <= 8u ? p : k);
         u256 bnd;
         {
-            const uint32_t j = m.y % 12u, k = m.z % w;
-            const uint32_t p = j <= 7u ? w - 1u : (j <= 10u ? k : 160u);
             // delta by j, 3 bits per entry biased by 2 (a ternary chain here became a
             // divergent if-chain): j 0..11 -> 0 1 2 3 -1 -2 0 -1 0 -1 1 -1
             const int32_t delta = (int32_t)((PF_BND_DELTA >> (3u * j)) & 7ull) - 2;
-            u256 base = pow2(p);
+            u256 base = pw;
             const uint32_t usepow = j >= 6u ? 0xffffffffu : 0u;
             u256 dl;
             dl.l[0] = (uint32_t)delta;
@@ -258,10 +261,9 @@ PF_INL u256 gen_var(const SetCtx& S, uint32_t v, uint32_t cand) {
         // the lanes; without a parent, a random byte
         u256 mut = pf::zero256();
         if (has_parent) {
-            const u256 f = pow2(m.z % w);
             const uint32_t flip = (m.y & 3u) == 0u ? 0xffffffffu : 0u;
 #pragma unroll
-            for (int i = 0; i < 8; i++) mut.l[i] = par.l[i] ^ (f.l[i] & flip);
+            for (int i = 0; i < 8; i++) mut.l[i] = par.l[i] ^ (pw.l[i] & flip);
         } else {
             mut.l[0] = r0.x & 0xffu;
         }
