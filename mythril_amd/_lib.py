@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 import threading
 from typing import Optional
 
@@ -88,11 +89,15 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         # the dynamic loader bind this library to the already-loaded copies, so torch
         # (device memory, streams, RCCL) and the engine share one runtime and one device
         # context.  Loading ours first would map a second runtime and torch's device init
-        # then fails ("No HIP GPUs are available").
-        try:
-            import torch  # noqa: F401
-        except ImportError:
-            pass
+        # then fails ("No HIP GPUs are available").  A process that never uses torch — a
+        # Mythril analysis through integration.install(), which sets PF_TORCH=0 — loads the
+        # engine on /opt/rocm's runtime alone and pays neither torch's import (~1.5 s) nor
+        # its memory.
+        if os.environ.get("PF_TORCH", "1") != "0" or "torch" in sys.modules:
+            try:
+                import torch  # noqa: F401
+            except ImportError:
+                pass
         if not os.path.exists(path):
             raise PathFeasError(
                 f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")

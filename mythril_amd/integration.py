@@ -25,6 +25,7 @@ Seams:
 from __future__ import annotations
 
 import logging
+import os
 import threading
 from dataclasses import replace
 from typing import Dict, List, Optional, Tuple
@@ -207,8 +208,12 @@ def gpu_optimize_class():
 
 
 def install() -> None:
-    """Rebind the funnel's Optimize (support/model.py:13 binds it by value at import)."""
+    """Rebind the funnel's Optimize (support/model.py:13 binds it by value at import).  The
+    analysis process does not use torch, so the engine is loaded without it (PF_TORCH=0,
+    mythril_amd/_lib.py) unless the caller chose otherwise."""
     import mythril.support.model as funnel
+
+    os.environ.setdefault("PF_TORCH", "0")
 
     funnel.Optimize = gpu_optimize_class()
 

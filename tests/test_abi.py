@@ -57,3 +57,18 @@ def test_library_loads_and_exports():
 
 def test_set_desc_layout():
     assert ctypes.sizeof(_lib.pf_stats) == 40
+
+
+def test_library_loads_without_torch_when_asked():
+    """PF_TORCH=0 (set by integration.install() for a Mythril analysis process): the engine
+    library loads on /opt/rocm's HIP runtime without importing torch."""
+    import subprocess
+    import sys
+
+    code = ("import sys; from mythril_amd import _lib; _lib.load_library(); "
+            "print('torch' in sys.modules)")
+    env = dict(os.environ, PF_TORCH="0")
+    out = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True,
+                         text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.strip() == "False"
