@@ -72,3 +72,28 @@ def test_library_loads_without_torch_when_asked():
                          text=True, timeout=300)
     assert out.returncode == 0, out.stderr
     assert out.stdout.strip() == "False"
+
+
+@pytest.mark.gpu
+def test_engine_runs_without_torch_on_gpu():
+    """The analysis-process configuration on the device: PF_TORCH=0, the engine initialises
+    on /opt/rocm's runtime alone, hashes and searches, and torch is never imported."""
+    import subprocess
+    import sys
+
+    code = (
+        "import sys\n"
+        "from mythril_amd import synth\n"
+        "from mythril_amd.engine import get_engine\n"
+        "e = get_engine()\n"
+        "h = e.keccak256([b''])[0].hex()\n"
+        "assert h == 'c5d2460186f7233c927e7db2dcc703c0e500b653ca82273b7bfad8045d85a470', h\n"
+        "progs = [synth.random_dag_set(i)[0] for i in range(8)]\n"
+        "r = e.check(e.upload(progs), budget=4096, seed=0, flags=2)\n"
+        "assert (r.found == 0).all(), r.found\n"
+        "print('torch' in sys.modules)\n")
+    env = dict(os.environ, PF_TORCH="0")
+    out = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True,
+                         text=True, timeout=120)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert out.stdout.strip().splitlines()[-1] == "False"
