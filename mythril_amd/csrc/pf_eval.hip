@@ -46,6 +46,36 @@ namespace {
         _Pragma("unroll") for (int k_ = 0; k_ < 8; k_++)                                    \
             (dst).l[k_] = (W)[k_ / (LPB)][(r) * (LPB) + (k_ % (LPB))];                         \
     } while (0)
+// The 8-register kernels read and write registers through a uniform switch over the
+// register number instead: static VGPR indices, no indexing mode (config 3 +0.8 %, and 8
+// VGPRs fewer: 155).  The 16-register kernels keep s_set_gpr_idx (a 16-way switch per
+// operand is a lot of code for the 0.4 % of sets that run them).
+#define RD_CASE(dst, W, R, LPB)                                                            \
+    case R:                                                                               \
+        _Pragma("unroll") for (int k_ = 0; k_ < 8; k_++)                                  \
+            (dst).l[k_] = (W)[k_ / (LPB)][(R) * (LPB) + (k_ % (LPB))];                     \
+        break;
+#define RD_SW(dst, W, r, LPB)                                                              \
+    do {                                                                                  \
+        switch (r) {                                                                      \
+            RD_CASE(dst, W, 0, LPB) RD_CASE(dst, W, 1, LPB) RD_CASE(dst, W, 2, LPB)       \
+            RD_CASE(dst, W, 3, LPB) RD_CASE(dst, W, 4, LPB) RD_CASE(dst, W, 5, LPB)       \
+            default: RD_CASE(dst, W, 6, LPB)                                              \
+        }                                                                                 \
+    } while (0)
+#define WR_CASE(W, R, src, LPB)                                                            \
+    case R:                                                                               \
+        _Pragma("unroll") for (int k_ = 0; k_ < 8; k_++)                                  \
+            (W)[k_ / (LPB)][(R) * (LPB) + (k_ % (LPB))] = (src).l[k_];                     \
+        break;
+#define WR_SW(W, r, src, LPB)                                                              \
+    do {                                                                                  \
+        switch (r) {                                                                      \
+            WR_CASE(W, 0, src, LPB) WR_CASE(W, 1, src, LPB) WR_CASE(W, 2, src, LPB)       \
+            WR_CASE(W, 3, src, LPB) WR_CASE(W, 4, src, LPB) WR_CASE(W, 5, src, LPB)       \
+            WR_CASE(W, 6, src, LPB) default: WR_CASE(W, 7, src, LPB)                      \
+        }                                                                                 \
+    } while (0)
 #define WR_W(W, r, src, LPB)                                                                  \
     do {                                                                                      \
         _Pragma("unroll") for (int k_ = 0; k_ < 8; k_++)                                    \
@@ -399,8 +429,13 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
         u256 x, y, z;
         // register indices are trusted: pf_batch_create checks every read and write
         // against the register file of the kernel that runs the set
-        if (__builtin_expect((tr & PF_TR_RA) != 0u, 1)) RD_W(x, W, a, LPB);
-        if (__builtin_expect((tr & PF_TR_RB) != 0u, 1)) RD_W(y, W, b, LPB);
+        if (NREG == 8) {
+            if (__builtin_expect((tr & PF_TR_RA) != 0u, 1)) RD_SW(x, W, a, LPB);
+            if (__builtin_expect((tr & PF_TR_RB) != 0u, 1)) RD_SW(y, W, b, LPB);
+        } else {
+            if (__builtin_expect((tr & PF_TR_RA) != 0u, 1)) RD_W(x, W, a, LPB);
+            if (__builtin_expect((tr & PF_TR_RB) != 0u, 1)) RD_W(y, W, b, LPB);
+        }
         // Dispatch on the datapath unit (w0 bits 21..23) first.  The heavy datapaths exist
         // once each (multiplier, divider, shifter, generator) and are shared by every
         // opcode that needs them: the kernel's code must stay small enough for the
@@ -621,9 +656,13 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
             const uint32_t dd = (tr & PF_TR_WW) ? d : (uint32_t)(NREG - 1);
             // keep the 8 indexed moves one s_set_gpr_idx block: the scheduler otherwise
             // interleaves the B update into it and re-enters indexing mode per move
-            __builtin_amdgcn_sched_barrier(0);
-            WR_W(W, dd, z, LPB);
-            __builtin_amdgcn_sched_barrier(0);
+            if (NREG == 8) {
+                WR_SW(W, dd, z, LPB);
+            } else {
+                __builtin_amdgcn_sched_barrier(0);
+                WR_W(W, dd, z, LPB);
+                __builtin_amdgcn_sched_barrier(0);
+            }
         }
 #ifdef PF_PROFILE_UNITS
         prof_add(prof, pbucket, __builtin_amdgcn_s_memtime() - t_ins);

@@ -24,6 +24,7 @@ OPS = {
     "lshr": ir.W_LSHR, "ashr": ir.W_ASHR, "exp": ir.W_EXP, "hash": ir.W_HASH,
     "ult_ite": "ult_ite", "var": "var", "concat8": "concat8",
     "udiv_q1": "udiv_q1", "udiv_q8": "udiv_q8",
+    "add4": "add4", "mul4": "mul4", "add1": "add1", "mul1": "mul1",
 }
 
 
@@ -31,6 +32,22 @@ def chain_program(kind, depth, seed):
     dag = Dag()
     x = dag.var("x", 256)
     y = dag.var("y", 256)
+    if kind in ("add4", "mul4", "add1", "mul1"):
+        # hand-scheduled bytecode (the lowering's post-order would serialise the chains):
+        # "*4" = 4 interleaved independent chains (consecutive instructions independent),
+        # "*1" = the same instruction count as one dependent chain
+        op = ir.W_ADD if kind.startswith("add") else ir.W_MUL
+        p = ir.Program(vars=[ir.Var("y", 256), ir.Var("x", 256)], seed=seed)
+        p.emit(ir.W_VAR, 256, dst=0, aux0=0)
+        p.emit(ir.W_VAR, 256, dst=1, aux0=1)
+        for k in range(2, 5):
+            p.emit(ir.W_ADD, 256, dst=k, a=1, b=0)
+        for i in range(depth):
+            r = 1 + (i % 4) if kind.endswith("4") else 1
+            p.emit(op, 256, dst=r, a=r, b=0)
+        p.emit(ir.B_EQ, 256, dst=0, a=1, b=2)
+        p.emit(ir.ASSERT, 1, a=0)
+        return p.finish()
     for i in range(depth):
         if kind == "ult_ite":
             c = dag.op(ir.B_ULT, 256, x, y)
