@@ -331,7 +331,9 @@ class Lowerer {
             bool dup = false;
             for (uint32_t j = 0; j < k; ++j) dup |= (int)n.args[j] == a;
             if (dup) continue;
-            if (next_use(a, t) >= INF) {
+            // not an operand the caller pinned (a remat inside an enclosing node's operand
+            // list shares its event time: mythril_amd/lower.py)
+            if (next_use(a, t) >= INF && !(((N[a].is_bool ? pinned_b : pinned_w) >> regs[k]) & 1u)) {
                 done(a);
                 (N[a].is_bool ? pb : pw) &= ~(1u << regs[k]);
             }

@@ -508,11 +508,16 @@ def lower_py(dag: Dag, seed: int = 0, name: str = "", nw: int = ir.NW) -> Progra
             r = materialize(a, t, pw, pb)
             (pb if dag.nodes[a].is_bool else pw).add(r)
             regs.append(r)
-        # operands whose last use is this node may be reused as destination
+        # operands whose last use is this node may be reused as destination — except an
+        # operand the caller has pinned: when this node is being rematerialised as an operand
+        # of an enclosing node, that node may already hold the same value as one of its own
+        # operands (a remat's use shares the enclosing event time t), and releasing it here
+        # let this node's result overwrite it
         for a in dict.fromkeys(n.args):   # distinct operands, in argument order
-            if next_use(a, t) >= (1 << 30):
+            r = regs[n.args.index(a)]
+            if next_use(a, t) >= (1 << 30) and r not in (pinned_b if dag.nodes[a].is_bool else pinned_w):
                 done(a)
-                (pb if dag.nodes[a].is_bool else pw).discard(regs[n.args.index(a)])
+                (pb if dag.nodes[a].is_bool else pw).discard(r)
         dst = alloc(rf, i, t, pb if n.is_bool else pw)
         op = n.kind
         if op in (ir.W_ITE, ir.B_ITE):      # args: cond(B), then, else

@@ -36,13 +36,30 @@ def _synth_dag(dag_id):
     return captured["dag"], prog, wit
 
 
-@pytest.mark.parametrize("dag_id", range(12))
+# 34783, 38037: config-3 DAGs whose narrow (7-register) lowering once gave a wrong program —
+# a node rematerialised inside another node's operand list released an operand register
+# the enclosing node had pinned, and its result overwrote it (lower.py emit_node)
+@pytest.mark.parametrize("dag_id", list(range(12)) + [34783, 38037])
 def test_synth_lowering_agrees(dag_id):
     dag, prog, wit = _synth_dag(dag_id)
     assert eval_dag(dag, wit)
     sv = O.SetView.from_batch(ir.Batch([prog]), 0)
     assert sv.evaluate(wit)
     _programs_agree(dag, prog, n=16)
+
+
+def test_planted_witness_survives_lowering_scan():
+    """Every planted witness of 3,000 config-3 DAGs (ids spread over the 1M range) still
+    satisfies the lowered program, at 7 and at 15 W registers."""
+    from mythril_amd.lower import lower_py
+
+    bad = []
+    for dag_id in range(0, 1_000_000, 333):
+        dag, prog, wit = _synth_dag(dag_id)
+        for p in (prog, lower_py(dag, nw=15)):
+            if not O.SetView.from_batch(ir.Batch([p]), 0).evaluate(wit):
+                bad.append(dag_id)
+    assert not bad, bad
 
 
 def test_remat_under_pressure():
