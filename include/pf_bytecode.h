@@ -34,8 +34,10 @@
 #define PF_NW 15          /* usable wide registers (limb-sliced VGPR banks on gfx950) */
 #endif
 #define PF_W_SINK 15      /* 16th bank slot: write sink of ops without a W result     */
+#ifndef PF_NW_NARROW
 #define PF_NW_NARROW 7    /* a batch whose programs write only W registers < 7 runs the
                              8-register search kernels (3 waves/SIMD); sink = register 7 */
+#endif
 #define PF_NB 32          /* bool registers                                          */
 #define PF_LIMBS 8        /* 8 x 32-bit limbs = 256 bits, little-endian limb order   */
 #define PF_MAX_WIDTH 256

@@ -76,6 +76,50 @@ namespace {
             WR_CASE(W, 6, src, LPB) default: WR_CASE(W, 7, src, LPB)                      \
         }                                                                                 \
     } while (0)
+// Narrow kernels: the register file is PF_NW_NARROW x 8 plain scalars, every access a
+// static index under a uniform switch over the register number, so each limb is its own
+// VGPR (no 16-dword vector tuples, no write sink): 56 VGPRs for 7 registers.
+#define RDN_CASE(dst, W, R)                                                                \
+    case R:                                                                               \
+        _Pragma("unroll") for (int k_ = 0; k_ < 8; k_++)(dst).l[k_] = (W)[R][k_];          \
+        break;
+#define WRN_CASE(W, R, src)                                                                \
+    case R:                                                                               \
+        _Pragma("unroll") for (int k_ = 0; k_ < 8; k_++)(W)[R][k_] = (src).l[k_];          \
+        break;
+#if PF_NW_NARROW == 7
+#define RDN_SW(dst, W, r)                                                                  \
+    do {                                                                                  \
+        switch (r) {                                                                      \
+            RDN_CASE(dst, W, 0) RDN_CASE(dst, W, 1) RDN_CASE(dst, W, 2) RDN_CASE(dst, W, 3) \
+            RDN_CASE(dst, W, 4) RDN_CASE(dst, W, 5) default: RDN_CASE(dst, W, 6)          \
+        }                                                                                 \
+    } while (0)
+#define WRN_SW(W, r, src)                                                                  \
+    do {                                                                                  \
+        switch (r) {                                                                      \
+            WRN_CASE(W, 0, src) WRN_CASE(W, 1, src) WRN_CASE(W, 2, src) WRN_CASE(W, 3, src) \
+            WRN_CASE(W, 4, src) WRN_CASE(W, 5, src) default: WRN_CASE(W, 6, src)          \
+        }                                                                                 \
+    } while (0)
+#elif PF_NW_NARROW == 6
+#define RDN_SW(dst, W, r)                                                                  \
+    do {                                                                                  \
+        switch (r) {                                                                      \
+            RDN_CASE(dst, W, 0) RDN_CASE(dst, W, 1) RDN_CASE(dst, W, 2) RDN_CASE(dst, W, 3) \
+            RDN_CASE(dst, W, 4) default: RDN_CASE(dst, W, 5)                              \
+        }                                                                                 \
+    } while (0)
+#define WRN_SW(W, r, src)                                                                  \
+    do {                                                                                  \
+        switch (r) {                                                                      \
+            WRN_CASE(W, 0, src) WRN_CASE(W, 1, src) WRN_CASE(W, 2, src) WRN_CASE(W, 3, src) \
+            WRN_CASE(W, 4, src) default: WRN_CASE(W, 5, src)                              \
+        }                                                                                 \
+    } while (0)
+#else
+#error "PF_NW_NARROW must be 6 or 7"
+#endif
 #define WR_W(W, r, src, LPB)                                                                  \
     do {                                                                                      \
         _Pragma("unroll") for (int k_ = 0; k_ < 8; k_++)                                    \
@@ -343,7 +387,7 @@ PF_INL uint2* exp_tbl_of(uint2* lds) {
     return lds + (threadIdx.x >> 6) * (PF_EXP_TBL_ENTRIES * 4 * 64) + (threadIdx.x & 63u);
 }
 #ifndef PF_WG_PER_CU_NARROW
-#define PF_WG_PER_CU_NARROW 3
+#define PF_WG_PER_CU_NARROW 4
 #endif
 #ifndef PF_WG_PER_CU
 #define PF_WG_PER_CU 2
@@ -359,7 +403,8 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
     // No initialisation: pf_batch_create rejects programs that read a register before
     // writing it, so the banks never leak values between candidates.
     constexpr int LPB = 16 / NREG;  // limbs per vector
-    vbank W[8 / LPB];
+    vbank W[8 / LPB];               // wide kernels (NREG 16)
+    uint32_t Wn[PF_NW_NARROW][8];   // narrow kernels (NREG 8)
     // the 32 bool registers are the bits of one VGPR (bit r = B register r)
     uint32_t Bk = 0u;
     // spill slots (lowering under register pressure): dynamically indexed, so the compiler
@@ -430,8 +475,8 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
         // register indices are trusted: pf_batch_create checks every read and write
         // against the register file of the kernel that runs the set
         if (NREG == 8) {
-            if (__builtin_expect((tr & PF_TR_RA) != 0u, 1)) RD_SW(x, W, a, LPB);
-            if (__builtin_expect((tr & PF_TR_RB) != 0u, 1)) RD_SW(y, W, b, LPB);
+            if (__builtin_expect((tr & PF_TR_RA) != 0u, 1)) RDN_SW(x, Wn, a);
+            if (__builtin_expect((tr & PF_TR_RB) != 0u, 1)) RDN_SW(y, Wn, b);
         } else {
             if (__builtin_expect((tr & PF_TR_RA) != 0u, 1)) RD_W(x, W, a, LPB);
             if (__builtin_expect((tr & PF_TR_RB) != 0u, 1)) RD_W(y, W, b, LPB);
@@ -623,6 +668,7 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
                     case PF_W_SPILL:
 #pragma unroll
                         for (int i = 0; i < 8; i++) spill[(aux & (PF_MAX_SPILL - 1u)) * 8u + i] = x.l[i];
+                        if (NREG == 8) PF_NEXT();  // no W result (the wide kernels write the sink)
                         z = x;
                         break;
                     case PF_W_FILL:
@@ -657,7 +703,7 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
             // keep the 8 indexed moves one s_set_gpr_idx block: the scheduler otherwise
             // interleaves the B update into it and re-enters indexing mode per move
             if (NREG == 8) {
-                WR_SW(W, dd, z, LPB);
+                WRN_SW(Wn, d, z);  // only W results reach here (W_SPILL leaves above)
             } else {
                 __builtin_amdgcn_sched_barrier(0);
                 WR_W(W, dd, z, LPB);
