@@ -88,29 +88,41 @@ namespace {
         _Pragma("unroll") for (int k_ = 0; k_ < 8; k_++)(W)[R][k_] = (src).l[k_];          \
         break;
 #if PF_NW_NARROW == 7
-#define RDN_SW(dst, W, r)                                                                  \
+// Registers 5 and 6 live in LDS, one 32-byte slot per lane each: entry 0 of EXP's window
+// table (which keeps base^0 = 1 out of it) and one entry past it (PF_LDS_WREG6).  40 VGPRs of
+// register file is what lets the kernel run 4 waves per SIMD without spilling; the lowering
+// hands out the lowest free register, so 5 and 6 are the least used (15 % of the operand
+// traffic on config 3).
+#define RDN_SW(dst, W, r, LT)                                                              \
     do {                                                                                  \
         switch (r) {                                                                      \
             RDN_CASE(dst, W, 0) RDN_CASE(dst, W, 1) RDN_CASE(dst, W, 2) RDN_CASE(dst, W, 3) \
-            RDN_CASE(dst, W, 4) RDN_CASE(dst, W, 5) default: RDN_CASE(dst, W, 6)          \
+            RDN_CASE(dst, W, 4)                                                           \
+            case 5: (dst) = pf::tbl_get(LT, 64u, PF_LDS_WREG5); break;                      \
+            default: (dst) = pf::tbl_get(LT, 64u, PF_LDS_WREG6); break;                     \
         }                                                                                 \
     } while (0)
-#define WRN_SW(W, r, src)                                                                  \
+#define WRN_SW(W, r, src, LT)                                                              \
     do {                                                                                  \
         switch (r) {                                                                      \
             WRN_CASE(W, 0, src) WRN_CASE(W, 1, src) WRN_CASE(W, 2, src) WRN_CASE(W, 3, src) \
-            WRN_CASE(W, 4, src) WRN_CASE(W, 5, src) default: WRN_CASE(W, 6, src)          \
+            WRN_CASE(W, 4, src)                                                           \
+            case 5: pf::tbl_put(LT, 64u, PF_LDS_WREG5, src); break;                         \
+            default: pf::tbl_put(LT, 64u, PF_LDS_WREG6, src); break;                        \
         }                                                                                 \
     } while (0)
+#if PF_EXP_SPLIT > 32
+#error "the narrow kernels' LDS registers need exp256_w32 (PF_EXP_SPLIT <= 32)"
+#endif
 #elif PF_NW_NARROW == 6
-#define RDN_SW(dst, W, r)                                                                  \
+#define RDN_SW(dst, W, r, LT)                                                                  \
     do {                                                                                  \
         switch (r) {                                                                      \
             RDN_CASE(dst, W, 0) RDN_CASE(dst, W, 1) RDN_CASE(dst, W, 2) RDN_CASE(dst, W, 3) \
             RDN_CASE(dst, W, 4) default: RDN_CASE(dst, W, 5)                              \
         }                                                                                 \
     } while (0)
-#define WRN_SW(W, r, src)                                                                  \
+#define WRN_SW(W, r, src, LT)                                                              \
     do {                                                                                  \
         switch (r) {                                                                      \
             WRN_CASE(W, 0, src) WRN_CASE(W, 1, src) WRN_CASE(W, 2, src) WRN_CASE(W, 3, src) \
@@ -382,9 +394,14 @@ PF_INL void prof_add(UnitProf* P, uint32_t b, uint64_t dt) {
 // LDS for EXP's window table (pf::exp256): 2^WB entries x 4 limb pairs per lane, 64 lanes,
 // 4 waves per 256-thread workgroup (2-bit window: 32 KiB, so PF_WG_PER_CU workgroups fit
 // in the CU's 160 KiB).
-#define PF_EXP_LDS_U2 (4 * PF_EXP_TBL_ENTRIES * 4 * 64)
+// One more 32-byte entry per lane after the table: the narrow kernels' LDS registers are
+// that entry and the table's entry 0 (PF_LDS_WREG5/6).  40 KiB per 256-thread workgroup: 4 workgroups fill the CU's 160 KiB.
+#define PF_LDS_WREG5 0u
+#define PF_LDS_WREG6 PF_EXP_TBL_ENTRIES
+#define PF_LDS_ENTRIES (PF_EXP_TBL_ENTRIES + 1)
+#define PF_EXP_LDS_U2 (4 * PF_LDS_ENTRIES * 4 * 64)
 PF_INL uint2* exp_tbl_of(uint2* lds) {
-    return lds + (threadIdx.x >> 6) * (PF_EXP_TBL_ENTRIES * 4 * 64) + (threadIdx.x & 63u);
+    return lds + (threadIdx.x >> 6) * (PF_LDS_ENTRIES * 4 * 64) + (threadIdx.x & 63u);
 }
 #ifndef PF_WG_PER_CU_NARROW
 #define PF_WG_PER_CU_NARROW 4
@@ -475,8 +492,8 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
         // register indices are trusted: pf_batch_create checks every read and write
         // against the register file of the kernel that runs the set
         if (NREG == 8) {
-            if (__builtin_expect((tr & PF_TR_RA) != 0u, 1)) RDN_SW(x, Wn, a);
-            if (__builtin_expect((tr & PF_TR_RB) != 0u, 1)) RDN_SW(y, Wn, b);
+            if (__builtin_expect((tr & PF_TR_RA) != 0u, 1)) RDN_SW(x, Wn, a, exp_tbl);
+            if (__builtin_expect((tr & PF_TR_RB) != 0u, 1)) RDN_SW(y, Wn, b, exp_tbl);
         } else {
             if (__builtin_expect((tr & PF_TR_RA) != 0u, 1)) RD_W(x, W, a, LPB);
             if (__builtin_expect((tr & PF_TR_RB) != 0u, 1)) RD_W(y, W, b, LPB);
@@ -521,10 +538,11 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
                     sb = ys.l[7] >> 31;
                     ua = pf::sel256(sa, pf::neg256(xs), xs);
                     ub = pf::sel256(sb, pf::neg256(ys), ys);
-                    y = ys;
                 } else if (op == PF_B_UMUL_NOOVF) {
                     ua = pf::ones256();
                     maskw(ua, w);
+                    // a waits in LDS table entry 1 (free outside EXP) across the division
+                    pf::tbl_put(exp_tbl, 64u, 1u, x);
                 }
                 u256 q, rr;
 #ifdef PF_PROFILE_UNITS
@@ -540,8 +558,10 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
 #else
                 pf::udivrem256(ua, ub, &q, &rr);
 #endif
+                // x and y are not read past the division (their registers are free in it):
+                // UMUL_NOOVF's a comes back from LDS, SMOD's signed divisor is rebuilt from |b|
                 if (op == PF_B_UMUL_NOOVF) {
-                    BSET(d, pf::iszero256(y) | (pf::ult256(q, x) ^ 1u));
+                    BSET(d, pf::iszero256(ub) | (pf::ult256(q, pf::tbl_get(exp_tbl, 64u, 1u)) ^ 1u));
                     PF_NEXT();
                 } else if (!sgn) {
                     z = op == PF_W_UDIV ? q : rr;
@@ -550,7 +570,8 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
                 } else {
                     z = pf::sel256(sa, pf::neg256(rr), rr);
                     if (op == PF_W_SMOD)  // uniform; the fix-up itself is a per-lane select
-                        z = pf::sel256((pf::iszero256(rr) ^ 1u) & (sa ^ sb), pf::add256(z, y), z);
+                        z = pf::sel256((pf::iszero256(rr) ^ 1u) & (sa ^ sb),
+                                       pf::add256(z, pf::sel256(sb, pf::neg256(ub), ub)), z);
                 }
                 break;
             }
@@ -703,7 +724,7 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
             // keep the 8 indexed moves one s_set_gpr_idx block: the scheduler otherwise
             // interleaves the B update into it and re-enters indexing mode per move
             if (NREG == 8) {
-                WRN_SW(Wn, d, z);  // only W results reach here (W_SPILL leaves above)
+                WRN_SW(Wn, d, z, exp_tbl);  // only W results reach here (W_SPILL leaves above)
             } else {
                 __builtin_amdgcn_sched_barrier(0);
                 WR_W(W, dd, z, LPB);

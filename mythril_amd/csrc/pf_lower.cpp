@@ -234,9 +234,10 @@ class Lowerer {
 
     int alloc(RegFile& rf, int node, int t, uint32_t pinned) {
         int r;
-        if (!rf.free_.empty()) {
-            r = rf.free_.back();
-            rf.free_.pop_back();
+        if (!rf.free_.empty()) {  // the lowest free register (lower.py _RegFile.alloc)
+            auto it = std::min_element(rf.free_.begin(), rf.free_.end());
+            r = *it;
+            rf.free_.erase(it);
         } else {
             // evict the cheapest-to-restore value, farthest next use first (Belady)
             bool have = false;

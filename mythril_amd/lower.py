@@ -235,7 +235,10 @@ class _RegFile:
         """Take a free register, else evict the cheapest-to-restore value (evict_rank),
         else spill the value used farthest in the future (spill(reg, node) emits it)."""
         if self.free:
-            r = self.free.pop()
+            # the lowest free register: the narrow kernels keep their highest register out
+            # of VGPRs when pressure demands (pf_eval.hip), so it should be the rarest one
+            r = min(self.free)
+            self.free.remove(r)
         else:
             cands = [(evict_rank(nd), rg) for rg, nd in self.holder.items() if rg not in pinned]
             cands = [c for c in cands if c[0] is not None]
