@@ -38,6 +38,11 @@
 #define PF_NW_NARROW 7    /* a batch whose programs write only W registers < 7 runs the
                              8-register search kernels (3 waves/SIMD); sink = register 7 */
 #endif
+/* waves per workgroup of the search kernels (each wave owns its LDS slice, so the
+ * workgroup size only sets how finely the CU's LDS and wave slots are handed out) */
+#ifndef PF_SEARCH_WG_WAVES
+#define PF_SEARCH_WG_WAVES 1
+#endif
 #define PF_NB 32          /* bool registers                                          */
 #define PF_LIMBS 8        /* 8 x 32-bit limbs = 256 bits, little-endian limb order   */
 #define PF_MAX_WIDTH 256

@@ -213,10 +213,10 @@ int check_enqueue(Batch* B, uint64_t gseed, uint32_t budget, uint32_t flags, uin
         geometry(D->num_cus, (uint32_t)n, budget, flags, &per_wave, &slices);
         const uint64_t waves = (uint64_t)n * slices;
         if (waves > 0xffffffffull) return fail("batch too large: %llu waves", (unsigned long long)waves);
-        const uint32_t blocks = (uint32_t)((waves + 3) / 4);
+        const uint32_t blocks = (uint32_t)((waves + PF_SEARCH_WG_WAVES - 1) / PF_SEARCH_WG_WAVES);
         hipLaunchKernelGGL(part == 0 ? (early ? pf_check_early_kernel : pf_check_kernel)
                                      : (early ? pf_check_early_r16_kernel : pf_check_r16_kernel),
-                           dim3(blocks), dim3(256), 0, st, B->d_descs, B->d_order + first,
+                           dim3(blocks), dim3(64 * PF_SEARCH_WG_WAVES), 0, st, B->d_descs, B->d_order + first,
                            (uint32_t)n, B->d_code, B->d_consts, B->d_schema, B->d_parents,
                            gseed, budget, per_wave, slices, flags, deadline, d_t0, d_found, d_counters);
         HIPCHK(hipGetLastError());

@@ -400,6 +400,9 @@ PF_INL void prof_add(UnitProf* P, uint32_t b, uint64_t dt) {
 #define PF_LDS_WREG6 PF_EXP_TBL_ENTRIES
 #define PF_LDS_ENTRIES (PF_EXP_TBL_ENTRIES + 1)
 #define PF_EXP_LDS_U2 (4 * PF_LDS_ENTRIES * 4 * 64)
+// search kernels: PF_SEARCH_WG_WAVES waves per workgroup (pathfeas.hip launches with the
+// same constant from include/pathfeas.h)
+#define PF_SEARCH_LDS_U2 (PF_SEARCH_WG_WAVES * PF_LDS_ENTRIES * 4 * 64)
 PF_INL uint2* exp_tbl_of(uint2* lds) {
     return lds + (threadIdx.x >> 6) * (PF_LDS_ENTRIES * 4 * 64) + (threadIdx.x & 63u);
 }
@@ -783,7 +786,7 @@ PF_INL void check_body(const pf_set_desc* __restrict__ descs, const uint32_t* __
     const uint32_t set = __builtin_amdgcn_readfirstlane(order[wave / slices]);
     const uint32_t slice = __builtin_amdgcn_readfirstlane(wave % slices);
     const SetCtx S = make_ctx(descs, set, code, consts, schema, parents, gseed);
-    __shared__ uint2 pf_exp_lds[PF_EXP_LDS_U2];
+    __shared__ uint2 pf_exp_lds[PF_SEARCH_LDS_U2];
     uint2* exp_tbl = exp_tbl_of(pf_exp_lds);
 
     uint64_t t0 = 0;
@@ -870,16 +873,16 @@ PF_INL void check_body(const pf_set_desc* __restrict__ descs, const uint32_t* __
 // at 2 waves.  Occupancy is the lever: config 3 runs +22 % faster on the 8-register build
 // (DESIGN.md §3), the interpreter's scalar dispatch and memory latency being what a third
 // wave hides.
-extern "C" __global__ void __launch_bounds__(256, PF_WG_PER_CU_NARROW) pf_check_kernel(PF_CHECK_PARAMS) {
+extern "C" __global__ void __launch_bounds__(64 * PF_SEARCH_WG_WAVES, PF_WG_PER_CU_NARROW) pf_check_kernel(PF_CHECK_PARAMS) {
     check_body<false, PF_NW_NARROW + 1>(PF_CHECK_ARGS);
 }
-extern "C" __global__ void __launch_bounds__(256, PF_WG_PER_CU_NARROW) pf_check_early_kernel(PF_CHECK_PARAMS) {
+extern "C" __global__ void __launch_bounds__(64 * PF_SEARCH_WG_WAVES, PF_WG_PER_CU_NARROW) pf_check_early_kernel(PF_CHECK_PARAMS) {
     check_body<true, PF_NW_NARROW + 1>(PF_CHECK_ARGS);
 }
-extern "C" __global__ void __launch_bounds__(256, PF_WG_PER_CU) pf_check_r16_kernel(PF_CHECK_PARAMS) {
+extern "C" __global__ void __launch_bounds__(64 * PF_SEARCH_WG_WAVES, PF_WG_PER_CU) pf_check_r16_kernel(PF_CHECK_PARAMS) {
     check_body<false, 16>(PF_CHECK_ARGS);
 }
-extern "C" __global__ void __launch_bounds__(256, PF_WG_PER_CU) pf_check_early_r16_kernel(PF_CHECK_PARAMS) {
+extern "C" __global__ void __launch_bounds__(64 * PF_SEARCH_WG_WAVES, PF_WG_PER_CU) pf_check_early_r16_kernel(PF_CHECK_PARAMS) {
     check_body<true, 16>(PF_CHECK_ARGS);
 }
 
