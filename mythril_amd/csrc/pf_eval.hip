@@ -34,6 +34,14 @@ using pf::u256;
 // tree (56 VALU per operand read) but indexes a 16-dword vector with s_set_gpr_idx (one
 // v_mov per limb).
 typedef uint32_t vbank __attribute__((ext_vector_type(16)));
+// the instruction stream in the constant address space (scalar loads), as a clang vector
+// (HIP's uint4 struct cannot be copied out of a non-generic address space)
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(4))) u32x4 pf_code_t;
+PF_INL uint4 fetch_ins(const pf_code_t* p) {
+    const u32x4 v = *p;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
 typedef uint32_t v32u __attribute__((ext_vector_type(32)));
 
 namespace {
@@ -460,8 +468,12 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
     // instruction i executes.  The loop ends at PF_END (pf_batch_create checks that every
     // program ends with it), which is decoded before the next fetch, so no load reads past
     // the program and the loop needs no instruction counter.
-    const uint4* ip = S.code;
-    uint4 In = *ip;
+    // The stream is read through the constant address space: the kernel's LDS and scratch
+    // stores made hipcc treat the code as possibly clobbered, and it then fetched every
+    // instruction with a vector load waited on at once (plus 4 readfirstlanes) instead of
+    // the pipelined scalar load
+    const pf_code_t* ip = (const pf_code_t*)S.code;
+    uint4 In = fetch_ins(ip);
     for (;;) {
 #ifdef PF_PROFILE_UNITS
         {
@@ -490,7 +502,7 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
         // loads return out of order, so a fetch issued before the decode would be waited
         // for together with the one being consumed (lgkmcnt(0)).
         __builtin_amdgcn_sched_barrier(0);
-        In = *(++ip);
+        In = fetch_ins(++ip);
         u256 x, y, z;
         // register indices are trusted: pf_batch_create checks every read and write
         // against the register file of the kernel that runs the set
