@@ -5,6 +5,7 @@ import os
 import random
 import subprocess
 import sys
+import tempfile
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 M = (1 << 256) - 1
@@ -26,7 +27,7 @@ def vals(rng):
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 20000
-    exe = "/tmp/u256_host_check"
+    exe = os.path.join(tempfile.gettempdir(), f"u256_host_check_{os.getpid()}")
     extra = os.environ.get("U256_FLAGS", "").split()
     subprocess.check_call([CLANG, "-O2", "-std=c++17", *extra, "-o", exe, os.path.join(HERE, "u256_host_check.cpp")])
     rng = random.Random(1234)
