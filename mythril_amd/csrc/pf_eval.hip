@@ -242,9 +242,11 @@ PF_INL uint64_t mul_wide(uint32_t a, uint32_t m) {
     return r;
 }
 
-PF_INL uint4 philox(uint4 c, uint32_t k0, uint32_t k1) {
+// rounds FIRST..9 of Philox4x32-10 (k0, k1 already advanced FIRST times)
+template <int FIRST>
+PF_INL uint4 philox_tail(uint4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
-    for (int i = 0; i < 10; i++) {
+    for (int i = FIRST; i < 10; i++) {
         const uint64_t p0 = mul_wide(c.x, PF_PHILOX_M0), p1 = mul_wide(c.z, PF_PHILOX_M1);
         const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
         const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
@@ -255,6 +257,28 @@ PF_INL uint4 philox(uint4 c, uint32_t k0, uint32_t k1) {
         k1 += PF_PHILOX_W1;
     }
     return c;
+}
+
+PF_INL uint4 philox(uint4 c, uint32_t k0, uint32_t k1) { return philox_tail<0>(c, k0, k1); }
+
+// philox(make_uint4(cand, v, z, 0), k0, k1), bit for bit, for the generator's counters:
+// only cand varies per lane, so round 1's second product (z * M1) is a constant, its first
+// (cand * M0, passed in as p0) is shared by the three blocks of a variable, and round 2's
+// first product has a wave-uniform operand and runs on the scalar unit — 17 per-lane
+// v_mad_u64_u32 per block instead of 20
+PF_INL uint4 philox_gen(uint64_t p0, uint32_t v, uint32_t z, uint32_t k0, uint32_t k1) {
+    const uint64_t p1 = (uint64_t)z * PF_PHILOX_M1;
+    const uint32_t x1 = (uint32_t)(p1 >> 32) ^ v ^ k0;  // uniform
+    const uint32_t y1 = (uint32_t)p1;                   // constant
+    const uint32_t z1 = (uint32_t)(p0 >> 32) ^ k1;      // per lane (counter word 3 is 0)
+    const uint32_t w1 = (uint32_t)p0;                   // per lane
+    k0 += PF_PHILOX_W0;
+    k1 += PF_PHILOX_W1;
+    const uint64_t q0 = (uint64_t)x1 * PF_PHILOX_M0;    // uniform: scalar multiply
+    const uint64_t q1 = mul_wide(z1, PF_PHILOX_M1);
+    const uint4 c = make_uint4((uint32_t)(q1 >> 32) ^ (y1 ^ k0), (uint32_t)q1,
+                               ((uint32_t)(q0 >> 32) ^ k1) ^ w1, (uint32_t)q0);
+    return philox_tail<2>(c, k0 + PF_PHILOX_W0, k1 + PF_PHILOX_W1);
 }
 
 struct SetCtx {
@@ -274,7 +298,8 @@ struct SetCtx {
 // walking a lane-divergent if-chain; the per-variable kind stays a (uniform) branch.
 PF_INL u256 gen_var(const SetCtx& S, uint32_t v, uint32_t cand) {
     const uint4 sc = S.schema[v];  // uniform -> scalar load
-    const uint4 m = philox(make_uint4(cand, v, 2u, 0u), S.k0, S.k1);
+    const uint64_t p0 = mul_wide(cand, PF_PHILOX_M0);  // round 1 of all three blocks
+    const uint4 m = philox_gen(p0, v, 2u, S.k0, S.k1);
     const uint32_t kind = sc.x & 0xffu, w = (sc.x >> 8) & 0x3ffu;
     const uint32_t hint0 = sc.y, hint1 = sc.z, pslot = sc.w;
     // The one per-lane gather (a constant of the set for the +-1 arm, or the actor table
@@ -287,10 +312,14 @@ PF_INL u256 gen_var(const SetCtx& S, uint32_t v, uint32_t cand) {
     const uint32_t ci = S.n_const ? (m.y % S.n_const) : 0u;
     const uint32_t* gp = S.consts + (size_t)(act ? hint0 + ai : ci) * 8u;
     u256 g;
+#ifdef PF_DIAG_NO_GATHER  // timing probe only: the per-lane gather's cost
+    g = pf::zero256(); g.l[0] = (uint32_t)(size_t)gp;
+#else
 #pragma unroll
     for (int i = 0; i < 8; i++) g.l[i] = gp[i];
-    const uint4 r0 = philox(make_uint4(cand, v, 0u, 0u), S.k0, S.k1);
-    const uint4 r1 = philox(make_uint4(cand, v, 1u, 0u), S.k0, S.k1);
+#endif
+    const uint4 r0 = philox_gen(p0, v, 0u, S.k0, S.k1);
+    const uint4 r1 = philox_gen(p0, v, 1u, S.k0, S.k1);
     const bool has_parent = pslot != PF_NO_PARENT;
     u256 par = pf::zero256();
     if (has_parent) {
