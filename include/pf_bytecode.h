@@ -43,6 +43,11 @@
 #ifndef PF_SEARCH_WG_WAVES
 #define PF_SEARCH_WG_WAVES 1
 #endif
+/* early-exit search work queue: heads per launch part, PF_EARLY_QUEUE_STRIDE u32 (128 B,
+ * one L2 line) apart, in the batch scratch from byte PF_EARLY_QUEUE_OFF on */
+#define PF_EARLY_QUEUES 16
+#define PF_EARLY_QUEUE_STRIDE 32
+#define PF_EARLY_QUEUE_OFF 512
 #define PF_NB 32          /* bool registers                                          */
 #define PF_LIMBS 8        /* 8 x 32-bit limbs = 256 bits, little-endian limb order   */
 #define PF_MAX_WIDTH 256

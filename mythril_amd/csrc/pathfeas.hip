@@ -44,10 +44,13 @@ int g_default = -1;       // index in g_devs of the default device (lowest id)
 // search-kernel waves launched per CU (PF_WAVES_PER_CU overrides both).  Measured on config 3
 // (1024 sets x 65,536 candidates, profiles/r01_wavesweep.md): with the longest-first set order
 // the full sweep peaks at 512 (finer slices even out the sets' unequal costs in the last round
-// of waves; 64 was 17 % slower); with early exit every concurrently running slice of a set
-// evaluates past its first witness, so fewer slices: 96.
+// of waves; 64 was 17 % slower).  The early-exit search is a work queue of (set, chunk) items
+// taken by a chip-filling grid: 16 waves per CU (4 per SIMD, the narrow kernels' occupancy;
+// PF_WAVES_PER_CU_EARLY), chunks of g_early_chunk_groups 64-candidate groups
+// (PF_EARLY_CHUNK_GROUPS).
 uint32_t g_waves_per_cu_full = 512;
-uint32_t g_waves_per_cu_early = 96;
+uint32_t g_waves_per_cu_early = 16;
+uint32_t g_early_chunk_groups = 8;
 
 int fail(const char* fmt, ...) {
     char buf[512];
@@ -178,6 +181,11 @@ hipStream_t pick_stream(Dev* D, void* s) { return s ? reinterpret_cast<hipStream
 // each wave walking >= 64 candidates of one set.
 void geometry(int num_cus, uint32_t n_sets, uint32_t budget, uint32_t flags, uint32_t* per_wave,
               uint32_t* slices) {
+    if (flags & PF_FLAG_EARLY_EXIT) {  // work-queue items: chunks of g_early_chunk_groups groups
+        *per_wave = g_early_chunk_groups * 64u;
+        *slices = std::max<uint32_t>(1u, (budget + *per_wave - 1) / *per_wave);
+        return;
+    }
     const uint64_t target_waves =
         (uint64_t)num_cus * ((flags & PF_FLAG_EARLY_EXIT) ? g_waves_per_cu_early : g_waves_per_cu_full);
     uint64_t groups = (budget + 63u) / 64u;  // 64-candidate groups per set
@@ -201,6 +209,9 @@ int check_enqueue(Batch* B, uint64_t gseed, uint32_t budget, uint32_t flags, uin
     HIPCHK(hipMemsetAsync(B->d_scratch, 0, 64, st));
 #endif
     HIPCHK(hipMemsetAsync(d_found, 0xff, std::max<size_t>(B->n_sets, 1) * sizeof(uint32_t), st));
+    if (flags & PF_FLAG_EARLY_EXIT)  // the work-queue heads of both launch parts
+        HIPCHK(hipMemsetAsync(B->d_scratch + PF_EARLY_QUEUE_OFF / 4, 0,
+                              2 * PF_EARLY_QUEUES * PF_EARLY_QUEUE_STRIDE * 4, st));
     HIPCHK(hipEventRecord(B->ev0, st));
     const uint64_t deadline = timeout_ms ? (uint64_t)timeout_ms * 100000ull : 0ull;  // 100 MHz
     const bool early = flags & PF_FLAG_EARLY_EXIT;
@@ -211,14 +222,21 @@ int check_enqueue(Batch* B, uint64_t gseed, uint32_t budget, uint32_t flags, uin
         if (n == 0 || budget == 0) continue;
         uint32_t per_wave, slices;
         geometry(D->num_cus, (uint32_t)n, budget, flags, &per_wave, &slices);
-        const uint64_t waves = (uint64_t)n * slices;
-        if (waves > 0xffffffffull) return fail("batch too large: %llu waves", (unsigned long long)waves);
+        const uint64_t items = (uint64_t)n * slices;
+        if (items > 0xffffffffull) return fail("batch too large: %llu waves", (unsigned long long)items);
+        // early exit: a chip-filling grid of persistent waves takes the items from the queue
+        // heads (zeroed above); full sweep: one wave per item
+        const uint64_t waves =
+            early ? std::min<uint64_t>(items, (uint64_t)D->num_cus * g_waves_per_cu_early) : items;
+        uint32_t* d_queue =
+            B->d_scratch + PF_EARLY_QUEUE_OFF / 4 + part * PF_EARLY_QUEUES * PF_EARLY_QUEUE_STRIDE;
         const uint32_t blocks = (uint32_t)((waves + PF_SEARCH_WG_WAVES - 1) / PF_SEARCH_WG_WAVES);
         hipLaunchKernelGGL(part == 0 ? (early ? pf_check_early_kernel : pf_check_kernel)
                                      : (early ? pf_check_early_r16_kernel : pf_check_r16_kernel),
                            dim3(blocks), dim3(64 * PF_SEARCH_WG_WAVES), 0, st, B->d_descs, B->d_order + first,
                            (uint32_t)n, B->d_code, B->d_consts, B->d_schema, B->d_parents,
-                           gseed, budget, per_wave, slices, flags, deadline, d_t0, d_found, d_counters);
+                           gseed, budget, per_wave, slices, flags, deadline, d_t0, d_found, d_counters,
+                           d_queue);
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(B->ev1, st));
@@ -284,6 +302,14 @@ int pf_init(uint64_t device_mask) {
     if (const char* e = getenv("PF_WAVES_PER_CU")) {
         long v = strtol(e, nullptr, 10);
         if (v >= 8 && v <= 4096) g_waves_per_cu_full = g_waves_per_cu_early = (uint32_t)v;
+    }
+    if (const char* e = getenv("PF_WAVES_PER_CU_EARLY")) {  // the early-exit search alone
+        long v = strtol(e, nullptr, 10);
+        if (v >= 1 && v <= 4096) g_waves_per_cu_early = (uint32_t)v;
+    }
+    if (const char* e = getenv("PF_EARLY_CHUNK_GROUPS")) {
+        long v = strtol(e, nullptr, 10);
+        if (v >= 1 && v <= 1024) g_early_chunk_groups = (uint32_t)v;
     }
     for (int id = 0; id < n && id < 64; ++id) {
         if (!((device_mask >> id) & 1ull) || find_dev(id)) continue;
@@ -462,7 +488,8 @@ int pf_batch_create_on(int device, const uint32_t* code, size_t n_ins, const uin
     const size_t o_code = 0, o_const = o_code + al(n_ins * 16), o_schema = o_const + al(n_const * 32 + 32),
                  o_par = o_schema + al(n_vars * 16), o_desc = o_par + al(n_parents * 32),
                  o_order = o_desc + al(n_sets * sizeof(pf_set_desc)), o_found = o_order + al(n_sets * 4),
-                 o_scr = o_found + al(std::max<size_t>(n_sets, 1) * 4), total = o_scr + 512;
+                 o_scr = o_found + al(std::max<size_t>(n_sets, 1) * 4),
+                 total = o_scr + PF_EARLY_QUEUE_OFF + 2 * PF_EARLY_QUEUES * PF_EARLY_QUEUE_STRIDE * 4;
     std::vector<uint8_t> stage(o_found, 0);  // found / scratch are cleared by every search
     auto put = [&](size_t off, const void* src, size_t bytes) {
         if (bytes && src) memcpy(stage.data() + off, src, bytes);

@@ -808,6 +808,47 @@ PF_INL SetCtx make_ctx(const pf_set_desc* __restrict__ descs, uint32_t set,
 
 }  // namespace
 
+// candidates [begin, end) of one set: 64-candidate groups, ballot, smallest witness by
+// atomicMin; with EARLY the walk stops at the first witness or once a witness below the
+// next group exists
+template <bool EARLY, int NREG>
+PF_INL void search_item(const SetCtx& S, uint32_t set, uint32_t begin, uint32_t end, uint32_t flags,
+                        uint64_t deadline_ticks, uint64_t t0, uint32_t* __restrict__ found,
+                        uint2* exp_tbl, uint64_t& evals_full, uint64_t& decided, uint64_t& ops,
+                        uint32_t& cut, UnitProf& prof) {
+    const uint32_t lane = threadIdx.x & 63u;
+    for (uint32_t base = begin; base < end; base += 64u) {
+        if (EARLY) {
+            uint32_t f = __hip_atomic_load(found + set, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (__builtin_amdgcn_readfirstlane(f) <= base) break;
+        }
+        if (deadline_ticks) {
+            uint64_t now = __builtin_amdgcn_s_memrealtime();
+            if (now - t0 > deadline_ticks) {
+                cut = 1u;  // this item is not fully searched: no complete verdict
+                break;
+            }
+        }
+        const uint32_t cand = base + lane;
+        const bool active = cand < end;
+        uint32_t complete = 0;
+        uint64_t lane_ops = 0;
+        uint32_t sat = run_program<MODE_GEN, NREG>(S, cand, active, flags, nullptr, 0u, exp_tbl, &complete,
+                                             &lane_ops, &prof);
+        const uint64_t m_act = __ballot(active);
+        const uint64_t m_sat = __ballot((uint32_t)active & sat);
+        const uint64_t m_full = __ballot((uint32_t)active & complete);
+        decided += __popcll(m_act);
+        evals_full += __popcll(m_full);
+        ops += lane_ops * (uint64_t)__popcll(m_act);
+        if (m_sat) {
+            uint32_t first = base + (uint32_t)__builtin_ctzll(m_sat);
+            if (lane == 0) atomicMin(found + set, first);
+            if (EARLY) break;
+        }
+    }
+}
+
 // ---- search kernel: generate + evaluate + ballot early exit ---------------------------
 // grid: one wave per (set, slice); a slice is `per_wave` consecutive candidates.
 // Two entry points over one body: the full sweep (pf_check_kernel) and the production
@@ -820,13 +861,12 @@ PF_INL void check_body(const pf_set_desc* __restrict__ descs, const uint32_t* __
                        const uint4* __restrict__ schema, const uint32_t* __restrict__ parents,
                        uint64_t gseed, uint32_t budget, uint32_t per_wave, uint32_t slices,
                        uint32_t flags, uint64_t deadline_ticks, uint64_t* __restrict__ t0_slot,
-                       uint32_t* __restrict__ found, unsigned long long* __restrict__ counters) {
+                       uint32_t* __restrict__ found, unsigned long long* __restrict__ counters,
+                       uint32_t* __restrict__ queue) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
-    if (wave >= n_sets * slices) return;
-    const uint32_t set = __builtin_amdgcn_readfirstlane(order[wave / slices]);
-    const uint32_t slice = __builtin_amdgcn_readfirstlane(wave % slices);
-    const SetCtx S = make_ctx(descs, set, code, consts, schema, parents, gseed);
+    const uint32_t n_items = n_sets * slices;
+    if (!EARLY && wave >= n_items) return;
     __shared__ uint2 pf_exp_lds[PF_SEARCH_LDS_U2];
     uint2* exp_tbl = exp_tbl_of(pf_exp_lds);
 
@@ -849,38 +889,45 @@ PF_INL void check_body(const pf_set_desc* __restrict__ descs, const uint32_t* __
 #ifdef PF_PROFILE_UNITS
     const uint64_t t_wave = __builtin_amdgcn_s_memtime();
 #endif
-    const uint32_t begin = slice * per_wave;
-    const uint32_t end = min(budget, begin + per_wave);
     uint64_t evals_full = 0, decided = 0, ops = 0;
     uint32_t cut = 0u;
-    for (uint32_t base = begin; base < end; base += 64u) {
-        if (EARLY) {
-            uint32_t f = __hip_atomic_load(found + set, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (__builtin_amdgcn_readfirstlane(f) <= base) break;
-        }
-        if (deadline_ticks) {
-            uint64_t now = __builtin_amdgcn_s_memrealtime();
-            if (now - t0 > deadline_ticks) {
-                cut = 1u;  // this wave's slice is not fully searched: no complete verdict
-                break;
+    // Full sweep: one wave per (set, slice), set-major (a set's slices side by side, sets
+    // longest first).  Early exit: a work queue of (set, chunk) items in chunk-major order —
+    // chunk 0 of every set first, then chunk 1, ... — taken one at a time by a chip-filling
+    // grid of waves.  A witness found in a low chunk makes the set's later chunks cost one
+    // found[] read each, instead of every concurrently launched slice of the set evaluating
+    // at least one group, and no wave idles while items remain (dynamic balance).  The
+    // smallest-witness result does not depend on the order: a chunk stops only once a witness
+    // below its own range exists.  Every wave leaves the loop: the queue head only grows.
+    if (!EARLY) {
+        const uint32_t set = __builtin_amdgcn_readfirstlane(order[wave / slices]);
+        const uint32_t slice = wave % slices;
+        search_item<EARLY, NREG>(make_ctx(descs, set, code, consts, schema, parents, gseed), set,
+                                 slice * per_wave, min(budget, slice * per_wave + per_wave), flags,
+                                 deadline_ticks, t0, found, exp_tbl, evals_full, decided, ops, cut, prof);
+    } else {
+        // PF_EARLY_QUEUES heads, 128 B apart: queue q hands out items q, q + Q, q + 2Q, ...
+        // (so the claims stay close to chunk-major order overall); a wave starts at queue
+        // wave % Q and moves on to the next queue when one runs dry.  One head serialised the
+        // claims at ~14 ns each in L2 — the whole cost of a planted batch, whose items after
+        // the first chunk are all skips.  Each inner loop ends because its head only grows.
+        for (uint32_t qi = 0; qi < PF_EARLY_QUEUES; ++qi) {
+            const uint32_t q = (wave + qi) % PF_EARLY_QUEUES;
+            const uint32_t nq = n_items > q ? (n_items - q + PF_EARLY_QUEUES - 1u) / PF_EARLY_QUEUES : 0u;
+            for (;;) {
+                uint32_t v = 0u;
+                if (lane == 0u) v = atomicAdd(queue + q * PF_EARLY_QUEUE_STRIDE, 1u);
+                const uint32_t k = __builtin_amdgcn_readfirstlane(v);
+                if (k >= nq) break;
+                const uint32_t item = k * PF_EARLY_QUEUES + q;
+                const uint32_t set = __builtin_amdgcn_readfirstlane(order[item % n_sets]);
+                const uint32_t slice = item / n_sets;
+                search_item<EARLY, NREG>(make_ctx(descs, set, code, consts, schema, parents, gseed), set,
+                                         slice * per_wave, min(budget, slice * per_wave + per_wave), flags,
+                                         deadline_ticks, t0, found, exp_tbl, evals_full, decided, ops, cut, prof);
+                if (cut) break;
             }
-        }
-        const uint32_t cand = base + lane;
-        const bool active = cand < end;
-        uint32_t complete = 0;
-        uint64_t lane_ops = 0;
-        uint32_t sat = run_program<MODE_GEN, NREG>(S, cand, active, flags, nullptr, 0u, exp_tbl, &complete,
-                                             &lane_ops, &prof);
-        const uint64_t m_act = __ballot(active);
-        const uint64_t m_sat = __ballot((uint32_t)active & sat);
-        const uint64_t m_full = __ballot((uint32_t)active & complete);
-        decided += __popcll(m_act);
-        evals_full += __popcll(m_full);
-        ops += lane_ops * (uint64_t)__popcll(m_act);
-        if (m_sat) {
-            uint32_t first = base + (uint32_t)__builtin_ctzll(m_sat);
-            if (lane == 0) atomicMin(found + set, first);
-            if (EARLY) break;
+            if (cut) break;
         }
     }
     if (lane == 0) {
@@ -904,10 +951,10 @@ PF_INL void check_body(const pf_set_desc* __restrict__ descs, const uint32_t* __
         const uint4 *__restrict__ schema, const uint32_t *__restrict__ parents, uint64_t gseed, \
         uint32_t budget, uint32_t per_wave, uint32_t slices, uint32_t flags,                   \
         uint64_t deadline_ticks, uint64_t *__restrict__ t0_slot, uint32_t *__restrict__ found, \
-        unsigned long long *__restrict__ counters
+        unsigned long long *__restrict__ counters, uint32_t *__restrict__ queue
 #define PF_CHECK_ARGS                                                                         \
     descs, order, n_sets, code, consts, schema, parents, gseed, budget, per_wave, slices, flags, \
-        deadline_ticks, t0_slot, found, counters
+        deadline_ticks, t0_slot, found, counters, queue
 
 // The search kernels exist twice: over 8 registers at 3 waves per SIMD (programs whose
 // lowering fits PF_NW_NARROW registers — the host picks per batch, pathfeas.hip) and over 16
