@@ -181,8 +181,16 @@ hipStream_t pick_stream(Dev* D, void* s) { return s ? reinterpret_cast<hipStream
 // each wave walking >= 64 candidates of one set.
 void geometry(int num_cus, uint32_t n_sets, uint32_t budget, uint32_t flags, uint32_t* per_wave,
               uint32_t* slices) {
-    if (flags & PF_FLAG_EARLY_EXIT) {  // work-queue items: chunks of g_early_chunk_groups groups
-        *per_wave = g_early_chunk_groups * 64u;
+    if (flags & PF_FLAG_EARLY_EXIT) {
+        // work-queue items: chunks of g_early_chunk_groups groups, larger when the batch
+        // would make more than 64 items per wave — every item costs a claim (an L2 atomic,
+        // ~14 ns per head) even when its set is already decided, which dominated planted
+        // batches of 65,536 sets (tools/full_pass.py: 136 ms per 1M sets at 8 groups)
+        const uint64_t groups = (budget + 63u) / 64u;
+        const uint64_t max_items = (uint64_t)num_cus * g_waves_per_cu_early * 64u;
+        uint64_t cg = std::max<uint64_t>(g_early_chunk_groups, (n_sets * groups + max_items - 1) / max_items);
+        cg = std::max<uint64_t>(1, std::min<uint64_t>(cg, groups));
+        *per_wave = (uint32_t)(cg * 64u);
         *slices = std::max<uint32_t>(1u, (budget + *per_wave - 1) / *per_wave);
         return;
     }
