@@ -67,3 +67,20 @@ def test_laser_shaped_sets_match_oracle(engine):
     progs = [synth.mythril_like_set(i) for i in range(96)]
     _compare(engine, progs, ir.FLAG_EARLY_EXIT | ir.FLAG_SHORTCIRCUIT,
              _oracle_first(progs, BUDGET, SEED))
+
+
+def test_early_exit_large_batch_matches_full_sweep(engine, config3):
+    """A batch big enough that the early-exit work queue grows its chunks (pathfeas.hip
+    geometry(): at most 64 items per wave; 4,608 sets x 1,024 groups -> 16-group chunks):
+    the smallest witness of every set equals the full sweep's, and the oracle's below 4,096."""
+    _, progs, want = config3
+    big = progs * 6
+    b = engine.upload(big)
+    full = [int(f) for f in engine.check(b, budget=65536, seed=SEED, flags=0).found]
+    early = [int(f) for f in engine.check(b, budget=65536, seed=SEED,
+                                          flags=ir.FLAG_EARLY_EXIT | ir.FLAG_SHORTCIRCUIT).found]
+    bad = [(i, f, e) for i, (f, e) in enumerate(zip(full, early)) if f != e]
+    assert not bad, bad[:10]
+    for i, f in enumerate(early):
+        w = want[i % len(progs)]
+        assert f == w if w is not None else (f == 0xFFFFFFFF or f >= BUDGET), (i, f, w)
