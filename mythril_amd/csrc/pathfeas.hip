@@ -217,7 +217,10 @@ int check_enqueue(Batch* B, uint64_t gseed, uint32_t budget, uint32_t flags, uin
     HIPCHK(hipMemsetAsync(B->d_scratch, 0, 64, st));
 #endif
     HIPCHK(hipMemsetAsync(d_found, 0xff, std::max<size_t>(B->n_sets, 1) * sizeof(uint32_t), st));
-    if (flags & PF_FLAG_EARLY_EXIT)  // the work-queue heads of both launch parts
+#ifndef PF_FULL_QUEUE
+#define PF_FULL_QUEUE 1
+#endif
+    if ((flags & PF_FLAG_EARLY_EXIT) || PF_FULL_QUEUE)  // the work-queue heads of both launch parts
         HIPCHK(hipMemsetAsync(B->d_scratch + PF_EARLY_QUEUE_OFF / 4, 0,
                               2 * PF_EARLY_QUEUES * PF_EARLY_QUEUE_STRIDE * 4, st));
     HIPCHK(hipEventRecord(B->ev0, st));
@@ -234,8 +237,9 @@ int check_enqueue(Batch* B, uint64_t gseed, uint32_t budget, uint32_t flags, uin
         if (items > 0xffffffffull) return fail("batch too large: %llu waves", (unsigned long long)items);
         // early exit: a chip-filling grid of persistent waves takes the items from the queue
         // heads (zeroed above); full sweep: one wave per item
-        const uint64_t waves =
-            early ? std::min<uint64_t>(items, (uint64_t)D->num_cus * g_waves_per_cu_early) : items;
+        const uint64_t waves = early ? std::min<uint64_t>(items, (uint64_t)D->num_cus * g_waves_per_cu_early)
+                             : PF_FULL_QUEUE ? std::min<uint64_t>(items, (uint64_t)D->num_cus * 16u)
+                                             : items;
         uint32_t* d_queue =
             B->d_scratch + PF_EARLY_QUEUE_OFF / 4 + part * PF_EARLY_QUEUES * PF_EARLY_QUEUE_STRIDE;
         const uint32_t blocks = (uint32_t)((waves + PF_SEARCH_WG_WAVES - 1) / PF_SEARCH_WG_WAVES);

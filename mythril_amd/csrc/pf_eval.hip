@@ -849,6 +849,12 @@ PF_INL void search_item(const SetCtx& S, uint32_t set, uint32_t begin, uint32_t 
     }
 }
 
+// PF_FULL_QUEUE (default 1): the full sweep also runs as the persistent work queue (items
+// set-major, sets longest first; +2 % on config 3 against one wave per item, which
+// PF_FULL_QUEUE=0 restores)
+#ifndef PF_FULL_QUEUE
+#define PF_FULL_QUEUE 1
+#endif
 // ---- search kernel: generate + evaluate + ballot early exit ---------------------------
 // grid: one wave per (set, slice); a slice is `per_wave` consecutive candidates.
 // Two entry points over one body: the full sweep (pf_check_kernel) and the production
@@ -866,7 +872,7 @@ PF_INL void check_body(const pf_set_desc* __restrict__ descs, const uint32_t* __
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
     const uint32_t n_items = n_sets * slices;
-    if (!EARLY && wave >= n_items) return;
+    if (!EARLY && !PF_FULL_QUEUE && wave >= n_items) return;
     __shared__ uint2 pf_exp_lds[PF_SEARCH_LDS_U2];
     uint2* exp_tbl = exp_tbl_of(pf_exp_lds);
 
@@ -899,7 +905,7 @@ PF_INL void check_body(const pf_set_desc* __restrict__ descs, const uint32_t* __
     // at least one group, and no wave idles while items remain (dynamic balance).  The
     // smallest-witness result does not depend on the order: a chunk stops only once a witness
     // below its own range exists.  Every wave leaves the loop: the queue head only grows.
-    if (!EARLY) {
+    if (!EARLY && !PF_FULL_QUEUE) {
         const uint32_t set = __builtin_amdgcn_readfirstlane(order[wave / slices]);
         const uint32_t slice = wave % slices;
         search_item<EARLY, NREG>(make_ctx(descs, set, code, consts, schema, parents, gseed), set,
@@ -920,8 +926,9 @@ PF_INL void check_body(const pf_set_desc* __restrict__ descs, const uint32_t* __
                 const uint32_t k = __builtin_amdgcn_readfirstlane(v);
                 if (k >= nq) break;
                 const uint32_t item = k * PF_EARLY_QUEUES + q;
-                const uint32_t set = __builtin_amdgcn_readfirstlane(order[item % n_sets]);
-                const uint32_t slice = item / n_sets;
+                // early exit: chunk-major; full sweep: set-major, sets longest first
+                const uint32_t set = __builtin_amdgcn_readfirstlane(order[EARLY ? item % n_sets : item / slices]);
+                const uint32_t slice = EARLY ? item / n_sets : item % slices;
                 search_item<EARLY, NREG>(make_ctx(descs, set, code, consts, schema, parents, gseed), set,
                                          slice * per_wave, min(budget, slice * per_wave + per_wave), flags,
                                          deadline_ticks, t0, found, exp_tbl, evals_full, decided, ops, cut, prof);
