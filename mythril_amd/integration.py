@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import logging
 import os
+import sys
 import threading
 from dataclasses import replace
 from typing import Dict, List, Optional, Tuple
@@ -78,17 +79,29 @@ class Z3WitnessView:
     Immutable by design: the funnel stores the model in ``ModelCache`` (support/model.py:120)
     and every later quick-sat check deep-copies it (support_utils.py:62-68), so a copy is
     the object itself.  No module or reader object is held (z3 is imported where needed).
-    ``eval`` converts the expression with the process-wide AST converter and evaluates it
-    under the witness; symbols the witness does not assign evaluate to z3's
-    ``model_completion`` defaults (0 / false / arrays 0 everywhere), and UF applications
-    outside the query take the engine's interpretation of that UF.  With
-    ``model_completion=False`` the completed value is returned as well (z3 would hand back
-    the symbol itself for an unassigned one).
+
+    ``eval`` follows z3's ``ModelRef.eval`` contract, including that it never raises on a
+    well-formed expression: ``check_quick_sat`` (support_utils.py:63-67) evaluates every
+    later query against every cached model with no ``try``, so an exception here would
+    abort ``get_model`` (support/model.py:96) and the analysis with it.
+    * The expression is converted with the process-wide AST converter and evaluated under
+      the witness — the kernel's interpretation, bit for bit.  With ``model_completion=True``
+      symbols the witness does not assign take z3's completion defaults (0 / false / arrays
+      0 everywhere) and UF applications outside the query the engine's UF interpretation.
+    * With ``model_completion=False`` an expression over a symbol the witness does not
+      interpret is returned partially evaluated, as z3 does: the assigned symbols are
+      substituted and the result simplified, so a bare unassigned symbol comes back as
+      itself (model.py:45-59).
+    * An expression the converter cannot take (an operator outside the lowering's
+      vocabulary) is evaluated the same way, by substitution + ``z3.simplify``.  If that does
+      not reduce a Bool to a literal, the answer is ``False``: ``is_true`` fails, quick-sat
+      moves on to the next model and the query reaches z3 — never an unsound ``True``.
     """
 
     def __init__(self, internal):
         self.internal = internal   # mythril_amd.smt.model.WitnessModel
         self._decls = None
+        self._names = None
 
     def __deepcopy__(self, memo):
         return self
@@ -119,16 +132,69 @@ class Z3WitnessView:
             return z3.BoolVal(w.bools[name])
         return None
 
+    def _interpreted(self) -> set:
+        """Names the witness interprets: the symbols, arrays and UFs of its query."""
+        if self._names is None:
+            self._names = {d.name() for d in self.internal.decls()}
+        return self._names
+
     def eval(self, expression, model_completion: bool = False):
         import z3
 
-        from .z3_terms import converter
+        try:
+            from .smt.model import _symbols
+            from .z3_terms import converter
 
-        term = converter(z3).term(expression)
-        v = self.internal.w.ev(term)
-        if term.is_bool:
-            return z3.BoolVal(bool(v))
-        return z3.BitVecVal(int(v), term.width)
+            term = converter(z3).term(expression)
+            names = self._interpreted()
+            if model_completion or all(
+                    (s.val[0] if s.op == "apply" else s.val) in names for s in _symbols([term])):
+                v = self.internal.w.ev(term)
+                if term.is_bool:
+                    return z3.BoolVal(bool(v))
+                return z3.BitVecVal(int(v), term.width)
+        except Exception as e:  # noqa: BLE001 - z3's eval does not raise; see the docstring
+            log.debug("witness eval by substitution: %s", e)
+        try:
+            return self._eval_substituted(z3, expression, model_completion)
+        except Exception as e:  # noqa: BLE001
+            log.debug("witness eval failed: %s", e)
+            return z3.BoolVal(False) if z3.is_bool(expression) else expression
+
+    def _eval_substituted(self, z3, expression, model_completion: bool):
+        """Substitute the witness's symbol values (completion defaults for the others when
+        ``model_completion``) and let z3 simplify; a Bool that does not reduce is False under
+        completion."""
+        w = self.internal.w
+        pairs, seen, stack = [], set(), [expression]
+        while stack:
+            e = stack.pop()
+            if e.get_id() in seen:
+                continue
+            seen.add(e.get_id())
+            d = e.decl()
+            if e.num_args() == 0 and d.kind() == z3.Z3_OP_UNINTERPRETED:
+                name, srt = d.name(), e.sort()
+                if z3.is_bool(e):
+                    if name in w.bools or model_completion:
+                        pairs.append((e, z3.BoolVal(bool(w.bools.get(name, False)))))
+                elif z3.is_bv(e):
+                    if name in w.vars or model_completion:
+                        pairs.append((e, z3.BitVecVal(w.vars.get(name, 0), srt.size())))
+                elif z3.is_array(e):
+                    tab = w.tables().get(name)
+                    if tab is not None or model_completion:
+                        dom, rng = srt.domain(), srt.range()
+                        a = z3.K(dom, z3.BitVecVal(0, rng.size()))
+                        for i, v in sorted((tab or {}).items()):
+                            a = z3.Store(a, z3.BitVecVal(i, dom.size()), z3.BitVecVal(v, rng.size()))
+                        pairs.append((e, a))
+                continue
+            stack.extend(e.arg(i) for i in range(e.num_args()))
+        r = z3.simplify(z3.substitute(expression, *pairs) if pairs else expression)
+        if model_completion and z3.is_bool(r) and not (z3.is_true(r) or z3.is_false(r)):
+            return z3.BoolVal(False)
+        return r
 
 
 def _query_key(terms: List[T.Term]) -> Tuple[T.Term, ...]:
@@ -147,12 +213,29 @@ def _lookup_batch(terms: List[T.Term]):
     return None
 
 
+_GPU_OPTIMIZE = None
+
+
 def gpu_optimize_class():
-    """Build the drop-in subclass of ``mythril.laser.smt.Optimize`` (needs Mythril + z3)."""
+    """The drop-in subclass of ``mythril.laser.smt.Optimize`` (needs Mythril + z3); built
+    once per process.
+
+    Query accounting: ``check`` carries Mythril's own ``@stat_smt_query``
+    (solver_statistics.py:7-25), exactly as ``BaseSolver.check`` does (solver.py:72), so
+    every query — GPU-answered or sent to z3 — bumps ``SolverStatistics().query_count`` and
+    ``solver_time`` once; the z3 fallback runs ``BaseSolver.check``'s body (``_z3_check``)
+    rather than the decorated ``super().check()``, which would count the query twice.
+    ``gpu_sat`` / ``gpu_attempts`` are kept beside them (mythril_amd.smt.solver), so
+    "% discharged" = ``gpu_sat / query_count`` (:func:`discharge_ratio`)."""
+    global _GPU_OPTIMIZE
+    from mythril.laser.smt import Optimize as MythrilOptimize
+
+    if _GPU_OPTIMIZE is not None and _GPU_OPTIMIZE.__bases__[0] is MythrilOptimize:
+        return _GPU_OPTIMIZE
     import z3
     from mythril.laser.ethereum.function_managers import keccak_function_manager
-    from mythril.laser.smt import Optimize as MythrilOptimize
     from mythril.laser.smt.model import Model
+    from mythril.laser.smt.solver.solver_statistics import stat_smt_query
 
     from .smt import gpu_check
     from .smt.solver import SolverStatistics
@@ -177,6 +260,7 @@ def gpu_optimize_class():
             self._objectives = True
             super().maximize(element)
 
+        @stat_smt_query
         def check(self, *args):
             self._gpu_model = None
             if not self._objectives and not args and gpu_check.CONFIG.enabled:
@@ -190,6 +274,8 @@ def gpu_optimize_class():
                         cfg = gpu_check.CONFIG
                         if self._timeout_ms:
                             cfg = replace(cfg, timeout_ms=int(self._timeout_ms))
+                        # parent models: buckets new to this query start from the newest
+                        # witness / z3 model values of their symbols (gpu_check._RECENT)
                         internal = gpu_check.check_sets([terms], config=cfg)[0]
                     if internal is not None:
                         stats.gpu_sat += 1
@@ -197,23 +283,83 @@ def gpu_optimize_class():
                         return z3.sat
                 except Exception as e:  # the GPU never decides a query it cannot answer
                     log.info("GPU path skipped: %s", e)
-            return super().check(*args)
+            result = self._z3_check(*args)
+            if result == z3.sat and gpu_check.CONFIG.enabled:
+                _note_z3_model(z3, self.raw)
+            return result
+
+        def _z3_check(self, *args):
+            """``BaseSolver.check``'s body without its decorator (solver.py:72-88): stdout
+            silenced around libz3, a ``Z3Exception`` becomes ``unknown``."""
+            old_stdout = sys.stdout
+            with open(os.devnull, "w") as dev_null_fd:
+                sys.stdout = dev_null_fd
+                try:
+                    evaluate = self.raw.check(args)
+                except z3.z3types.Z3Exception as e:
+                    evaluate = z3.unknown
+                    log.info("Encountered Z3 exception when checking the constraints: %s", e)
+                finally:
+                    sys.stdout = old_stdout
+            return evaluate
 
         def model(self):
             if self._gpu_model is not None:
                 return self._gpu_model
             return super().model()
 
+    _GPU_OPTIMIZE = GpuOptimize
     return GpuOptimize
+
+
+def _note_z3_model(z3, raw) -> None:
+    """A z3-answered query's model becomes the parent model of the buckets its children add
+    (a child state = the parent's constraints + one JUMPI condition, instructions.py:1638,
+    1662; the reference keeps the same model in ``model_cache``, support/model.py:120)."""
+    from .smt import gpu_check
+
+    try:
+        m = raw.model()
+        vals = {}
+        for d in m.decls():
+            if d.arity() != 0:
+                continue
+            v = m[d]
+            if z3.is_bv_value(v):
+                vals[d.name()] = v.as_long()
+            elif z3.is_true(v) or z3.is_false(v):
+                vals[d.name()] = int(z3.is_true(v))
+        gpu_check.note_values(vals)
+    except Exception as e:  # noqa: BLE001 - parents are only a search seed
+        log.debug("z3 model not noted: %s", e)
+
+
+def discharge_ratio() -> Optional[float]:
+    """SURVEY §8(d) "% discharged": GPU-answered objective-free queries over Mythril's
+    ``SolverStatistics().query_count`` (solver_statistics.py:14-21; counted only while
+    Mythril's statistics are enabled, mythril_analyzer.py:147).  None before any query."""
+    from mythril.laser.smt.solver.solver_statistics import SolverStatistics as MythrilStats
+
+    from .smt.solver import SolverStatistics
+
+    n = MythrilStats().query_count
+    return SolverStatistics().gpu_sat / n if n else None
 
 
 def install() -> None:
     """Rebind the funnel's Optimize (support/model.py:13 binds it by value at import).  The
     analysis process does not use torch, so the engine is loaded without it (PF_TORCH=0,
-    mythril_amd/_lib.py) unless the caller chose otherwise."""
+    mythril_amd/_lib.py) unless the caller chose otherwise.
+
+    Devices: Mythril analyses in ONE process (``myth analyze``), so unless the caller chose
+    (``PF_DEVICES``) or the process is one rank of a launcher (``LOCAL_RANK``), the engine
+    drives every visible gfx950 device (``PF_DEVICES=all``, engine.get_engine): a tx-boundary
+    batch is split into cost-balanced shards searched concurrently."""
     import mythril.support.model as funnel
 
     os.environ.setdefault("PF_TORCH", "0")
+    if "LOCAL_RANK" not in os.environ:
+        os.environ.setdefault("PF_DEVICES", "all")
 
     funnel.Optimize = gpu_optimize_class()
 
@@ -240,17 +386,32 @@ def batch_open_states(open_states, kfm=None, registry: UFRegistry = DEFAULT_REGI
     constraint set (svm.py:85,380: ``open_states`` holds WorldStates); each witness is
     parked under the state's query so the ``is_possible()`` pass that follows is answered
     without z3.  The previous batch's witnesses are dropped first.  Returns the number of
-    states with a witness."""
+    states with a witness.
+
+    The batch is an optimisation only: a state whose constraints do not convert (an operator
+    or sort outside the lowering) is left out — its ``is_possible()`` goes to z3 as before —
+    and an engine error drops the batch, never the analysis (svm.py:306-307 runs the hook
+    with no guard)."""
     from .smt.gpu_check import check_sets
 
     if kfm is None:  # pragma: no cover - needs Mythril
         from mythril.laser.ethereum.function_managers import keccak_function_manager as kfm
-    sync_keccak_registry(kfm, registry)
-    sets = [state_terms(st) for st in open_states]
-    models = check_sets(sets, registry=registry) if sets else []
-    n = 0
     with _BATCH_LOCK:
         _BATCH_CACHE.clear()
+    sync_keccak_registry(kfm, registry)
+    sets = []
+    for st in open_states:
+        try:
+            sets.append(state_terms(st))
+        except Exception as e:  # noqa: BLE001 - z3 answers this state later
+            log.info("tx-boundary batch: state left to z3 (%s)", e)
+    try:
+        models = check_sets(sets, registry=registry) if sets else []
+    except Exception as e:  # noqa: BLE001
+        log.warning("tx-boundary batch skipped: %s", e)
+        return 0
+    n = 0
+    with _BATCH_LOCK:
         for terms, m in zip(sets, models):
             if m is not None:
                 _BATCH_CACHE[_query_key(terms)] = m
@@ -258,10 +419,25 @@ def batch_open_states(open_states, kfm=None, registry: UFRegistry = DEFAULT_REGI
     return n
 
 
+_PLUGIN_CLASSES = None
+
+
 def _plugin_classes():
+    """(MythrilAmdLaserPlugin, MythrilAmdPluginBuilder), built once per Mythril binding.
+
+    The builder is constructed the way Mythril constructs installed plugins —
+    ``plugin(**plugin_args)`` (plugin/discovery.py:57) — and then read as a LASER
+    ``PluginBuilder`` (``.enabled``, laser/plugin/loader.py:62-64).  ``MythrilLaserPlugin``
+    resolves ``__init__`` to ``MythrilPlugin.__init__(**kwargs)``, which does not set
+    ``enabled`` (plugin/interface.py:23-24 shadows laser/plugin/builder.py:14-15), so the
+    builder's own ``__init__`` runs both."""
+    global _PLUGIN_CLASSES
     from mythril.laser.plugin.builder import PluginBuilder
     from mythril.laser.plugin.interface import LaserPlugin
     from mythril.plugin.interface import MythrilLaserPlugin
+
+    if _PLUGIN_CLASSES is not None and _PLUGIN_CLASSES[1].__bases__[0] is MythrilLaserPlugin:
+        return _PLUGIN_CLASSES
 
     class MythrilAmdLaserPlugin(LaserPlugin):
         def initialize(self, symbolic_vm) -> None:
@@ -269,19 +445,29 @@ def _plugin_classes():
 
             @symbolic_vm.laser_hook("stop_sym_trans")
             def _batch():
-                n = batch_open_states(symbolic_vm.open_states)
-                log.info("GPU batch: %d/%d open states have a witness", n, len(symbolic_vm.open_states))
+                try:
+                    n = batch_open_states(symbolic_vm.open_states)
+                    log.info("GPU batch: %d/%d open states have a witness", n,
+                             len(symbolic_vm.open_states))
+                except Exception as e:  # noqa: BLE001 - the batch is only an optimisation
+                    log.warning("GPU batch failed: %s", e)
 
-    class MythrilAmdPluginBuilder(MythrilLaserPlugin, PluginBuilder):
+    class MythrilAmdPluginBuilder(MythrilLaserPlugin):
         name = "mythril-amd-path-feasibility"
         plugin_default_enabled = True
         author = "mythril_amd"
+        plugin_version = "0.3.0"
         plugin_description = "MI355X batched path-feasibility engine (GPU witnesses skip z3)"
+
+        def __init__(self, **kwargs):
+            MythrilLaserPlugin.__init__(self, **kwargs)   # MythrilPlugin.__init__
+            PluginBuilder.__init__(self)                  # enabled = True
 
         def __call__(self, *args, **kwargs):
             return MythrilAmdLaserPlugin()
 
-    return MythrilAmdLaserPlugin, MythrilAmdPluginBuilder
+    _PLUGIN_CLASSES = (MythrilAmdLaserPlugin, MythrilAmdPluginBuilder)
+    return _PLUGIN_CLASSES
 
 
 def __getattr__(name):  # lazy: importing mythril_amd never imports mythril

@@ -366,14 +366,20 @@ def lower(dag: Dag, seed: int = 0, name: str = "", nw: Optional[int] = None) -> 
     forced_a = limbs(dag.forced)
     roots = np.array(dag.roots or [0], dtype=np.uint32)
     cap_i = 16 * nn + 64 + 4 * len(dag.roots)
-    code = np.zeros((cap_i, 4), dtype=np.uint32)
     cap_c = len(pool) + len(dag.forced) + 1
-    consts = np.zeros((cap_c, 8), dtype=np.uint32)
     ni, nc = ctypes.c_size_t(), ctypes.c_size_t()
     p = lambda x: x.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))  # noqa: E731
-    rc = L.pfl_lower(p(arr), nn, p(pool_a), len(pool), p(roots), len(dag.roots), p(forced_a),
-                     len(dag.forced), nw, p(code), cap_i, ctypes.byref(ni), p(consts), cap_c,
-                     ctypes.byref(nc))
+    for _ in range(4):
+        code = np.zeros((cap_i, 4), dtype=np.uint32)
+        consts = np.zeros((cap_c, 8), dtype=np.uint32)
+        rc = L.pfl_lower(p(arr), nn, p(pool_a), len(pool), p(roots), len(dag.roots), p(forced_a),
+                         len(dag.forced), nw, p(code), cap_i, ctypes.byref(ni), p(consts), cap_c,
+                         ctypes.byref(nc))
+        if rc != -3:
+            break
+        # output capacity: rematerialisation and spill code under register pressure can
+        # exceed the estimate; the library checks before writing, so retry larger
+        cap_i, cap_c = 4 * cap_i, 4 * cap_c
     if rc != 0:
         msg = L.pfl_last_error().decode(errors="replace")
         if rc == -2:

@@ -43,6 +43,13 @@ class GpuConfig:
     enabled: bool = True
     split: bool = True           # independence buckets
     hints: bool = True           # constraint-directed parent (hint) models
+    # parent models for buckets new to a query: the newest witness / z3-model value of each
+    # of the bucket's symbols and array reads (note_values / _note_witness) — a child state
+    # is its parent's constraints plus one JUMPI condition (instructions.py:1638,1662), so
+    # the parent's model is the natural candidate 0 (mutated by the generator's
+    # neighbourhood candidates, include/pf_bytecode.h) for the one bucket the condition changes
+    parents: bool = True
+    recent_size: int = 1 << 14   # symbol values kept for parent models
     cache_size: int = 1 << 16    # bucket witnesses kept
     # re-evaluate every constraint of a multi-bucket set under the union of its bucket
     # witnesses.  Off by default: each bucket witness is re-checked on exactly its bucket's
@@ -84,14 +91,81 @@ _CACHE: "OrderedDict[tuple, Tuple[Lowered, List[int]]]" = OrderedDict()
 _NEG: "OrderedDict[tuple, None]" = OrderedDict()
 
 
+# newest values of symbols (name -> value) and of base-array reads (array name ->
+# {select term -> value}) over the accepted witnesses and noted z3 models: the parent models
+_RECENT_VARS: "OrderedDict[str, int]" = OrderedDict()
+_RECENT_READS: "OrderedDict[str, OrderedDict]" = OrderedDict()
+
+
 def reset_cache() -> None:
     with _lock:
         _CACHE.clear()
         _NEG.clear()
+        _RECENT_VARS.clear()
+        _RECENT_READS.clear()
 
 
 def _neg_key(key: tuple, cfg: GpuConfig) -> tuple:
+    # parents only seed candidate 0 of a bucket's first search; a bucket whose complete
+    # search found nothing stays negative (as the reference's lru_cache'd check_quick_sat
+    # keeps its negative answers, support_utils.py:59)
     return (key, cfg.budget, cfg.seed, cfg.flags, cfg.hints)
+
+
+def note_values(vals: Dict[str, int], cfg: Optional[GpuConfig] = None) -> None:
+    """Record symbol values (a z3 model's, integration._note_z3_model) for parent models."""
+    cfg = cfg or CONFIG
+    with _lock:
+        for k, v in vals.items():
+            _RECENT_VARS[k] = v
+            _RECENT_VARS.move_to_end(k)
+        while len(_RECENT_VARS) > cfg.recent_size:
+            _RECENT_VARS.popitem(last=False)
+
+
+def _note_witness(lo: Lowered, values: List[int], cfg: GpuConfig) -> None:
+    """Record an accepted bucket witness's variable values (caller holds _lock)."""
+    for term, val in zip(lo.var_terms, values):
+        if term.op in ("var", "bvar"):
+            _RECENT_VARS[term.val] = val
+            _RECENT_VARS.move_to_end(term.val)
+        elif term.op == "select" and term.args[0].op == "array":
+            name = term.args[0].val
+            tab = _RECENT_READS.get(name)
+            if tab is None:
+                tab = _RECENT_READS[name] = OrderedDict()
+            _RECENT_READS.move_to_end(name)
+            tab[term] = val
+            tab.move_to_end(term)
+            while len(tab) > 256:
+                tab.popitem(last=False)
+    while len(_RECENT_VARS) > cfg.recent_size:
+        _RECENT_VARS.popitem(last=False)
+    while len(_RECENT_READS) > 1024:
+        _RECENT_READS.popitem(last=False)
+
+
+def _recent_parent(bucket: List[T.Term]) -> Optional[dict]:
+    """Parent model of a bucket from the recent values of its symbols and array reads
+    (keys: symbol names, and select terms — hash-consed, so the same read in a child
+    query is the same key)."""
+    from .independence import dependence_keys
+
+    keys = set()
+    for c in bucket:
+        keys |= dependence_keys(c)
+    out: dict = {}
+    with _lock:
+        for k in keys:
+            if k.startswith("v:"):
+                v = _RECENT_VARS.get(k[2:])
+                if v is not None:
+                    out[k[2:]] = v
+            elif k.startswith("a:"):
+                tab = _RECENT_READS.get(k[2:])
+                if tab:
+                    out.update(tab)
+    return out or None
 
 
 def _set_seed(constraints: Sequence[T.Term]) -> int:
@@ -109,6 +183,17 @@ def _lower_bucket(bucket: List[T.Term], reg: UFRegistry, parent: Optional[dict],
     return lo, lower(lo.dag, seed=_set_seed(bucket))
 
 
+def _origin(idx: int, prog, hinted: bool, parented: bool) -> str:
+    """Provenance of a bucket witness: "search" = a later GPU candidate; candidate 0 is the
+    host hint model ("hint"), the parent model ("parent") or the generator's first
+    candidate ("first")."""
+    if idx > 0:
+        return "search"
+    if prog.has_parent:
+        return "hint" if hinted else ("parent" if parented else "first")
+    return "first"
+
+
 def _lower_chunk(job):
     """Worker: lower a chunk of buckets; the DAG stays behind (witnesses need only the
     variable / UF / array-read terms)."""
@@ -118,8 +203,10 @@ def _lower_chunk(job):
         try:
             lo, prog = _lower_bucket(bucket, reg, parent, hints)
             out.append((Lowered(None, lo.var_terms, lo.uf_apps, lo.array_reads), prog, None))
-        except LoweringError as e:
-            out.append((None, None, str(e)))
+        except (LoweringError, ValueError, OverflowError) as e:
+            # one bucket the lowering cannot take (or whose native emission fails) is that
+            # bucket's failure only: the rest of the batch is still searched
+            out.append((None, None, f"{type(e).__name__}: {e}" if not isinstance(e, LoweringError) else str(e)))
     return out
 
 
@@ -218,7 +305,8 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
         bks = buckets(cs) if cfg.split else [cs]
         ks = []
         for b in bks:
-            key = (tuple(b), tuple(sorted(parent.items())) if parent else None, reg_sig)
+            # a witness answers its bucket whatever parent model seeded the search
+            key = (tuple(b), reg_sig)
             ks.append(key)
             if key in found or key in pending:
                 continue
@@ -226,17 +314,23 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
             if cached is not None:
                 found[key] = cached
                 hits += 1
+                if cfg.parents:
+                    with _lock:
+                        _note_witness(cached[0], cached[1], cfg)
                 continue
             if _neg_key(key, cfg) in _NEG:  # a complete search found nothing: same answer
                 found[key] = None
                 hits += 1
                 continue
             pending.add(key)
-            jobs.append((b, parent))
+            bp = parent if parent is not None else (_recent_parent(b) if cfg.parents else None)
+            jobs.append((b, bp))
             job_keys.append(key)
         set_buckets.append(ks)
     lap("bucket")
     failed = set()
+    parented: List[bool] = []
+    job_parent = {k: bool(j[1]) for k, j in zip(job_keys, jobs)}
     lowered_all = _lower_all(jobs, reg, cfg)
     lap("lower")
     for key, (lo, prog, err) in zip(job_keys, lowered_all):
@@ -251,6 +345,7 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
         progs.append(prog)
         lows.append(lo)
         keys.append(key)
+        parented.append(job_parent[key])
     for ks in set_buckets:
         if ks is not None and not any(k in failed or (k in found and found[k] is None) for k in ks):
             n_lowered += 1
@@ -296,7 +391,7 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
             # provenance of the witness: candidate 0 of a hinted program is the host's
             # constraint-directed hint model itself; any other index was found by the search
             idx = int(res.found[k])
-            origin[key] = "search" if idx > 0 else ("hint" if progs[k].has_parent else "first")
+            origin[key] = _origin(idx, progs[k], cfg.hints, parented[k])
             w = Witness(lows[k], v, reg)
             # re-check on the host under the same interpretation before trusting it
             if all(w.ev(c) for c in key[0]):
@@ -305,6 +400,7 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
                     _CACHE[key] = (lows[k], v)
                     while len(_CACHE) > cfg.cache_size:
                         _CACHE.popitem(last=False)
+                    _note_witness(lows[k], v, cfg)
         lap("recheck")
 
     n_sat = 0
@@ -323,13 +419,11 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
             ok = all(w.ev(c) for c in cs)
         if ok:
             out[i] = WitnessModel(w, list(sets[i]))
-            # per bucket: "hint" = candidate 0 of a hinted program (the host hint model),
-            # "first" = candidate 0 of an unhinted one (the generator's first candidate),
-            # "search" = a later candidate; the set takes the strongest of its buckets
-            # the set: "search" if some bucket needed a later candidate, else "hint" if a
-            # host hint model answered some bucket, else "first" / "cache"
+            # per bucket: _origin(); the set takes the strongest of its buckets: "search" if
+            # some bucket needed a later candidate, else "hint" / "parent" / "first" if such a
+            # candidate 0 answered some bucket, else "cache"
             kinds = {origin.get(k, "cache") for k in ks}
-            out[i].origin = next((c for c in ("search", "hint", "first") if c in kinds), "cache")
+            out[i].origin = next((c for c in ("search", "hint", "parent", "first") if c in kinds), "cache")
             n_sat += 1
     lap("models")
     with _lock:

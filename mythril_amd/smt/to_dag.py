@@ -126,8 +126,13 @@ class TermLowering:
         elif kind == ir.VK_SMALL:
             hint0 = 4 + 32 * 8
         before = len(self.dag.vars)
-        node = self.dag.var(name, w, kind, hint0, hint1,
-                            parent if parent is not None else self.parent.get(name))
+        if parent is None and self.parent:
+            # parent models are keyed by symbol name, or by the read's own (hash-consed)
+            # select term for array reads (gpu_check._recent_parent)
+            parent = self.parent.get(name)
+            if parent is None:
+                parent = self.parent.get(term)
+        node = self.dag.var(name, w, kind, hint0, hint1, parent)
         if len(self.dag.vars) > before:
             self.var_terms.append(term)
         return node

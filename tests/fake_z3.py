@@ -520,6 +520,26 @@ def is_const(e):
     return isinstance(e, ExprRef) and e.num_args() == 0
 
 
+def substitute(t, *m):
+    """z3.substitute(t, (from, to), ...) — also accepts one list of pairs, as z3py does."""
+    if len(m) == 1 and isinstance(m[0], list):
+        m = tuple(m[0])
+    table = {a.get_id(): b for a, b in m}
+    memo = {}
+
+    def go(x):
+        r = memo.get(x.get_id())
+        if r is None:
+            r = table.get(x.get_id())
+            if r is None:
+                kids = [go(a) for a in x.children()]
+                r = x if all(k is a for k, a in zip(kids, x.children())) else _mk(x.decl(), kids, x._val)
+            memo[x.get_id()] = r
+        return r
+
+    return go(t)
+
+
 # ---- simplify: the rewrites z3's bit-vector simplifier is known to apply ------------------
 def _val(e):
     return e._val if isinstance(e, BitVecNumRef) else None
@@ -572,6 +592,18 @@ def _simp(e, args):
         return _op(Z3_OP_SLEQ, BoolSort(), [args[1], args[0]])
     if k == Z3_OP_SLT:
         return Not(_op(Z3_OP_SLEQ, BoolSort(), [args[1], args[0]]))
+    if k == Z3_OP_SELECT and vals[1] is not None:  # read over store / const-array chains
+        arr = args[0]
+        while True:
+            ak = arr.decl().kind()
+            if ak == Z3_OP_CONST_ARRAY:
+                return arr.arg(0)
+            if ak == Z3_OP_STORE and _val(arr.arg(1)) is not None:
+                if _val(arr.arg(1)) == vals[1]:
+                    return arr.arg(2)
+                arr = arr.arg(0)
+                continue
+            break
     if all(v is not None for v in vals) and args:
         w = e.sort().size() if e.sort().kind() == Z3_BV_SORT else None
         folded = _fold(k, vals, [a.size() for a in args], w, e.decl().params())

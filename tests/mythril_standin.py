@@ -1,50 +1,76 @@
 """Stand-ins for the Mythril modules the engine's seams touch (Mythril is not importable in
 this image: z3, eth_abi and eth_hash are missing — SURVEY.md §8c).
 
-Each piece restates the behaviour of the reference module it stands for, so the drop-in
-``Optimize``, the witness model and the tx-boundary hook run inside the same control flow a
-real analysis would give them:
+Each piece restates the reference module it stands for LINE FOR LINE where the engine's code
+meets it (class bases, ``__init__`` signatures, decorators, the loader's construction
+sequence), so the drop-in ``Optimize``, the witness model and the plugin run inside exactly
+the control flow a real analysis gives them.  A stand-in that simplifies the reference at a
+seam hides the very bugs these tests exist to find (round-2 review: a ``check`` without
+``@stat_smt_query``, a ``MythrilPlugin`` without ``__init__(**kwargs)``).
 
-* ``mythril.laser.smt`` — ``BaseSolver``/``Optimize`` over ``z3.Optimize`` (raw assertions,
-  ``set_timeout`` -> ``raw.set(timeout=)``, ``model()`` -> ``Model([raw.model()])`` or an
-  empty ``Model()`` on a z3 exception; mythril/laser/smt/solver/solver.py:20-143), ``Bool``,
-  ``And``, ``simplify``;
-* ``mythril.laser.smt.model.Model`` — the relevance rule of ``eval``: the first internal
-  model whose ``decls()`` contains ``expression.decl()``, else the last one
-  (mythril/laser/smt/model.py:45-59);
-* ``mythril.support.support_utils.ModelCache`` — ``check_quick_sat`` deep-copies every
-  cached model and evaluates the query with ``model_completion=True``
-  (support_utils.py:57-71);
-* ``mythril.support.model.get_model`` — the funnel: bools, quick-sat, ``solver_worker`` on a
-  ``ThreadPool(1)``, sat -> ``model_cache.put(s.model(), 1)``, unknown ->
-  ``SolverTimeOutException``, unsat -> ``UnsatError`` (support/model.py:23-125);
+* ``mythril.support.support_utils`` — ``Singleton`` (support_utils.py:15-34), ``LRUCache``,
+  ``ModelCache.check_quick_sat`` (:35-71: deep copy + ``eval(..., model_completion=True)``);
+* ``mythril.laser.smt.solver.solver_statistics`` — ``stat_smt_query`` / ``SolverStatistics``
+  (solver_statistics.py:7-42);
+* ``mythril.laser.smt`` — ``BaseSolver``/``Solver``/``Optimize`` over ``z3.Optimize`` with the
+  decorated ``check`` that silences stdout and maps a ``Z3Exception`` to ``unknown``
+  (solver/solver.py:20-143), ``Model`` (model.py:6-59), ``Bool``, ``And``, ``simplify``;
+* ``mythril.support.model`` — ``solver_worker`` / ``get_model`` (support/model.py:23-125),
+  including the ``except Exception`` -> ``unknown`` around the worker's result;
 * ``Constraints.is_possible`` (constraints.py:31-46), ``WorldState.constraints``
-  (world_state.py:39), the keccak manager singleton, the plugin interfaces.
+  (world_state.py:39), the keccak manager singleton;
+* the plugin stack: ``LaserPlugin`` (laser/plugin/interface.py), ``PluginBuilder``
+  (laser/plugin/builder.py:6-21), ``MythrilPlugin`` / ``MythrilLaserPlugin``
+  (plugin/interface.py:6-46), ``LaserPluginLoader`` (laser/plugin/loader.py:12-75),
+  ``PluginDiscovery`` (plugin/discovery.py:11-73; the installed entry points are injected,
+  since nothing is pip-installed here) and ``MythrilPluginLoader`` (plugin/loader.py:19-79).
 
 Test infrastructure only.
 """
 
 from __future__ import annotations
 
+import os
 import sys
 import types
+from abc import ABC, abstractmethod
 from collections import OrderedDict
 from copy import deepcopy
 from functools import lru_cache
 from multiprocessing import TimeoutError
 from multiprocessing.pool import ThreadPool
+from time import time
+from typing import Dict
+
+MODULES = (
+    "mythril", "mythril.exceptions", "mythril.laser", "mythril.laser.smt",
+    "mythril.laser.smt.model", "mythril.laser.smt.solver", "mythril.laser.smt.solver.solver",
+    "mythril.laser.smt.solver.solver_statistics", "mythril.support", "mythril.support.model",
+    "mythril.support.support_utils", "mythril.laser.ethereum",
+    "mythril.laser.ethereum.function_managers", "mythril.laser.ethereum.state",
+    "mythril.laser.ethereum.state.constraints", "mythril.laser.plugin",
+    "mythril.laser.plugin.builder", "mythril.laser.plugin.interface",
+    "mythril.laser.plugin.loader", "mythril.plugin", "mythril.plugin.interface",
+    "mythril.plugin.discovery", "mythril.plugin.loader")
 
 
-def build(z3):
-    """Module objects keyed by their Mythril names, bound to the given z3 module."""
-    mods = {n: types.ModuleType(n) for n in (
-        "mythril", "mythril.exceptions", "mythril.laser", "mythril.laser.smt",
-        "mythril.laser.smt.model", "mythril.support", "mythril.support.model",
-        "mythril.support.support_utils", "mythril.laser.ethereum",
-        "mythril.laser.ethereum.function_managers", "mythril.laser.ethereum.state",
-        "mythril.laser.ethereum.state.constraints", "mythril.laser.plugin",
-        "mythril.laser.plugin.builder", "mythril.laser.plugin.interface", "mythril.plugin",
-        "mythril.plugin.interface")}
+def build(z3, installed_plugins=None):
+    """Module objects keyed by their Mythril names, bound to the given z3 module.
+    ``installed_plugins`` = {entry-point name: "module:attr"}, the ``"mythril.plugins"``
+    entry points ``PluginDiscovery`` loads (discovery.py:22-36) — nothing is pip-installed
+    here, so the test passes the value the package metadata declares (pyproject.toml)."""
+    mods = {n: types.ModuleType(n) for n in MODULES}
+
+    # ---- support_utils.py:15-34 -----------------------------------------------------------
+    class Singleton(type):
+        _instances: Dict = {}
+
+        def __call__(cls, *args, **kwargs):
+            if cls not in cls._instances:
+                cls._instances[cls] = super(Singleton, cls).__call__(*args, **kwargs)
+            return cls._instances[cls]
+
+    mods["mythril.support.support_utils"].Singleton = Singleton
 
     # ---- exceptions (mythril/exceptions.py:16-28) -------------------------------------
     class UnsatError(Exception):
@@ -55,6 +81,38 @@ def build(z3):
 
     mods["mythril.exceptions"].UnsatError = UnsatError
     mods["mythril.exceptions"].SolverTimeOutException = SolverTimeOutException
+
+    # ---- solver_statistics.py:7-42 --------------------------------------------------------
+    def stat_smt_query(func):
+        stat_store = SolverStatistics()
+
+        def function_wrapper(*args, **kwargs):
+            if not stat_store.enabled:
+                return func(*args, **kwargs)
+
+            stat_store.query_count += 1
+            begin = time()
+
+            result = func(*args, **kwargs)
+
+            end = time()
+            stat_store.solver_time += end - begin
+
+            return result
+
+        return function_wrapper
+
+    class SolverStatistics(object, metaclass=Singleton):
+        def __init__(self):
+            self.enabled = False
+            self.query_count = 0
+            self.solver_time = 0
+
+        def __repr__(self):
+            return "Query count: {} \nSolver time: {}".format(self.query_count, self.solver_time)
+
+    stats_mod = mods["mythril.laser.smt.solver.solver_statistics"]
+    stats_mod.stat_smt_query, stats_mod.SolverStatistics = stat_smt_query, SolverStatistics
 
     # ---- facade ------------------------------------------------------------------------
     class Bool:
@@ -74,35 +132,39 @@ def build(z3):
         expression.simplify()
         return expression
 
+    # ---- model.py:6-59 -----------------------------------------------------------------------
     class Model:
         def __init__(self, models=None):
             self.raw = models or []
 
         def decls(self):
-            out = []
-            for m in self.raw:
-                out.extend(m.decls())
-            return out
+            result = []
+            for internal_model in self.raw:
+                result.extend(internal_model.decls())
+            return result
 
         def __getitem__(self, item):
-            for i, m in enumerate(self.raw):
+            for internal_model in self.raw:
+                is_last_model = self.raw.index(internal_model) == len(self.raw) - 1
                 try:
-                    r = m[item]
-                    if r is not None:
-                        return r
+                    result = internal_model[item]
+                    if result is not None:
+                        return result
                 except IndexError:
-                    if i == len(self.raw) - 1:
+                    if is_last_model:
                         raise
+                    continue
             return None
 
         def eval(self, expression, model_completion=False):
-            for i, m in enumerate(self.raw):
-                is_last = i == len(self.raw) - 1
-                relevant = expression.decl() in list(m.decls())
-                if relevant or is_last:
-                    return m.eval(expression, model_completion)
+            for internal_model in self.raw:
+                is_last_model = self.raw.index(internal_model) == len(self.raw) - 1
+                is_relevant_model = expression.decl() in list(internal_model.decls())
+                if is_relevant_model or is_last_model:
+                    return internal_model.eval(expression, model_completion)
             return None
 
+    # ---- solver/solver.py:20-143 ------------------------------------------------------------
     class BaseSolver:
         def __init__(self, raw):
             self.raw = raw
@@ -110,17 +172,30 @@ def build(z3):
         def set_timeout(self, timeout):
             self.raw.set(timeout=timeout)
 
+        def set_unsat_core(self):
+            self.raw.set(unsat_core=True)
+
         def add(self, *constraints):
-            self.raw.add([c.raw for c in constraints])
+            z3_constraints = [c.raw for c in constraints]
+            self.raw.add(z3_constraints)
+
+        def assert_and_track(self, constraints, name):
+            self.raw.assert_and_track(constraints.raw, name)
 
         def append(self, *constraints):
             self.add(*constraints)
 
+        @stat_smt_query
         def check(self, *args):
-            try:
-                return self.raw.check(args)
-            except z3.z3types.Z3Exception:
-                return z3.unknown
+            old_stdout = sys.stdout
+            with open(os.devnull, "w") as dev_null_fd:
+                sys.stdout = dev_null_fd
+                try:
+                    evaluate = self.raw.check(args)
+                except z3.z3types.Z3Exception:
+                    evaluate = z3.unknown
+            sys.stdout = old_stdout
+            return evaluate
 
         def model(self):
             try:
@@ -130,6 +205,16 @@ def build(z3):
 
         def sexpr(self):
             return self.raw.sexpr()
+
+    class Solver(BaseSolver):
+        def __init__(self):
+            super().__init__(z3.Solver())
+
+        def reset(self):
+            self.raw.reset()
+
+        def pop(self, num):
+            self.raw.pop(num)
 
     class Optimize(BaseSolver):
         def __init__(self):
@@ -142,9 +227,12 @@ def build(z3):
             self.raw.maximize(element.raw)
 
     smt = mods["mythril.laser.smt"]
-    smt.Bool, smt.And, smt.simplify, smt.Optimize, smt.BaseSolver = Bool, And, simplify, Optimize, BaseSolver
-    smt.Model = Model
+    smt.Bool, smt.And, smt.simplify, smt.Optimize, smt.Solver = Bool, And, simplify, Optimize, Solver
+    smt.BaseSolver, smt.Model, smt.SolverStatistics = BaseSolver, Model, SolverStatistics
     mods["mythril.laser.smt.model"].Model = Model
+    for name in ("mythril.laser.smt.solver", "mythril.laser.smt.solver.solver"):
+        mods[name].BaseSolver, mods[name].Solver, mods[name].Optimize = BaseSolver, Solver, Optimize
+    mods["mythril.laser.smt.solver"].SolverStatistics = SolverStatistics
 
     # ---- keccak manager singleton -----------------------------------------------------
     kfm = types.SimpleNamespace(interval_hook_for_size={}, concrete_hashes={},
@@ -189,6 +277,7 @@ def build(z3):
         def put(self, key, value):
             self.model_cache.put(key, value)
 
+    mods["mythril.support.support_utils"].LRUCache = LRUCache
     mods["mythril.support.support_utils"].ModelCache = ModelCache
 
     # ---- the funnel (support/model.py:23-125) ------------------------------------------
@@ -200,42 +289,46 @@ def build(z3):
     def solver_worker(constraints, minimize=(), maximize=(), solver_timeout=None):
         s = funnel.Optimize()  # resolved at call time: the name install() rebinds
         s.set_timeout(solver_timeout)
-        for c in constraints:
-            s.add(c)
+        for constraint in constraints:
+            s.add(constraint)
         for e in minimize:
             s.minimize(e)
         for e in maximize:
             s.maximize(e)
-        return s.check(), s
+        result = s.check()
+        return result, s
 
     @lru_cache(maxsize=2 ** 23)
     def get_model(constraints, minimize=(), maximize=(), solver_timeout=None):
         solver_timeout = solver_timeout or funnel.solver_timeout_default
         if solver_timeout <= 0:
             raise SolverTimeOutException
-        for c in constraints:
-            if isinstance(c, bool) and not c:
+        for constraint in constraints:
+            if isinstance(constraint, bool) and not constraint:
                 raise UnsatError
         if isinstance(constraints, tuple) is False:
             constraints = constraints.get_all_constraints()
         constraints = [c for c in constraints if isinstance(c, bool) is False]
         if len(maximize) + len(minimize) == 0:
-            ret = funnel.model_cache.check_quick_sat(simplify(And(*constraints)).raw)
-            if ret:
-                return ret
+            ret_model = funnel.model_cache.check_quick_sat(simplify(And(*constraints)).raw)
+            if ret_model:
+                return ret_model
         pool = ThreadPool(1)
         try:
-            res = pool.apply_async(solver_worker, args=(constraints, minimize, maximize, solver_timeout))
+            thread_result = pool.apply_async(
+                solver_worker, args=(constraints, minimize, maximize, solver_timeout))
             try:
-                result, s = res.get(solver_timeout)
+                result, s = thread_result.get(solver_timeout)
             except TimeoutError:
+                result = z3.unknown
+            except Exception:
                 result = z3.unknown
         finally:
             pool.terminate()
         if result == z3.sat:
             funnel.model_cache.model_cache.put(s.model(), 1)
             return s.model()
-        if result == z3.unknown:
+        elif result == z3.unknown:
             raise SolverTimeOutException
         raise UnsatError
 
@@ -265,39 +358,181 @@ def build(z3):
     mods["mythril.laser.ethereum.state.constraints"].Constraints = Constraints
     mods["mythril.laser.ethereum.state"].WorldState = WorldState
 
-    # ---- plugin interfaces (laser/plugin/interface.py, builder.py; plugin/interface.py) --
+    # ---- laser/plugin/interface.py ---------------------------------------------------------
     class LaserPlugin:
         def initialize(self, symbolic_vm):
             raise NotImplementedError
 
-    class PluginBuilder:
-        name = "default"
+    # ---- laser/plugin/builder.py:6-21 -------------------------------------------------------
+    class PluginBuilder(ABC):
+        name = "Default Plugin Name"
 
         def __init__(self):
             self.enabled = True
 
+        @abstractmethod
+        def __call__(self, *args, **kwargs):
+            pass
+
+    # ---- plugin/interface.py:6-46 -----------------------------------------------------------
     class MythrilPlugin:
         author = "Default Author"
         name = "Plugin Name"
+        plugin_license = "All rights reserved."
+        plugin_type = "Mythril Plugin"
+        plugin_version = "0.0.1 "
         plugin_description = "This is an example plugin description"
 
-    class MythrilLaserPlugin(MythrilPlugin):
-        def __call__(self, *args, **kwargs):
-            raise NotImplementedError
+        def __init__(self, **kwargs):
+            pass
+
+        def __repr__(self):
+            plugin_name = type(self).__name__
+            return f"{plugin_name} - {self.plugin_version} - {self.author}"
+
+    class MythrilCLIPlugin(MythrilPlugin):
+        pass
+
+    class MythrilLaserPlugin(MythrilPlugin, PluginBuilder, ABC):
+        pass
+
+    # ---- laser/plugin/loader.py:12-75 -------------------------------------------------------
+    class LaserPluginLoader(object, metaclass=Singleton):
+        def __init__(self):
+            self.laser_plugin_builders = {}
+            self.plugin_args = {}
+            self.plugin_list = {}
+
+        def add_args(self, plugin_name, **kwargs):
+            self.plugin_args[plugin_name] = kwargs
+
+        def load(self, plugin_builder):
+            if plugin_builder.name in self.laser_plugin_builders:
+                return
+            self.laser_plugin_builders[plugin_builder.name] = plugin_builder
+
+        def is_enabled(self, plugin_name):
+            if plugin_name not in self.laser_plugin_builders:
+                return False
+            else:
+                return self.laser_plugin_builders[plugin_name].enabled
+
+        def enable(self, plugin_name):
+            if plugin_name not in self.laser_plugin_builders:
+                return ValueError(f"Plugin with name: {plugin_name} was not loaded")
+            self.laser_plugin_builders[plugin_name].enabled = True
+
+        def instrument_virtual_machine(self, symbolic_vm, with_plugins):
+            for plugin_name, plugin_builder in self.laser_plugin_builders.items():
+                enabled = (plugin_builder.enabled if not with_plugins
+                           else plugin_name in with_plugins)
+
+                if not enabled:
+                    continue
+
+                plugin = plugin_builder(**self.plugin_args.get(plugin_name, {}))
+                plugin.initialize(symbolic_vm)
+                self.plugin_list[plugin_name] = plugin
+
+    # ---- plugin/discovery.py:11-73 (entry points injected) ---------------------------------
+    class PluginDiscovery(object, metaclass=Singleton):
+        _installed_plugins = None
+
+        def init_installed_plugins(self):
+            from importlib.metadata import EntryPoint
+
+            self._installed_plugins = {
+                name: EntryPoint(name, value, "mythril.plugins").load()
+                for name, value in (installed_plugins or {}).items()}
+
+        @property
+        def installed_plugins(self):
+            if self._installed_plugins is None:
+                self.init_installed_plugins()
+            return self._installed_plugins
+
+        def is_installed(self, plugin_name):
+            return plugin_name in self.installed_plugins.keys()
+
+        def build_plugin(self, plugin_name, plugin_args):
+            if not self.is_installed(plugin_name):
+                raise ValueError(f"Plugin with name: `{plugin_name}` is not installed")
+
+            plugin = self.installed_plugins.get(plugin_name)
+            if plugin is None or not issubclass(plugin, MythrilPlugin):
+                raise ValueError(f"No valid plugin was found for {plugin_name}")
+
+            return plugin(**plugin_args)
+
+        def get_plugins(self, default_enabled=None):
+            if default_enabled is None:
+                return list(self.installed_plugins.keys())
+
+            return [plugin_name
+                    for plugin_name, plugin_class in self.installed_plugins.items()
+                    if plugin_class.plugin_default_enabled == default_enabled]
+
+    # ---- plugin/loader.py:19-79 -------------------------------------------------------------
+    class UnsupportedPluginType(Exception):
+        pass
+
+    class MythrilPluginLoader(object, metaclass=Singleton):
+        def __init__(self):
+            self.loaded_plugins = []
+            self.plugin_args = dict()
+            self._load_default_enabled()
+
+        def set_args(self, plugin_name, **kwargs):
+            self.plugin_args[plugin_name] = kwargs
+
+        def load(self, plugin):
+            if not isinstance(plugin, MythrilPlugin):
+                raise ValueError("Passed plugin is not of type MythrilPlugin")
+            if isinstance(plugin, MythrilLaserPlugin):
+                self._load_laser_plugin(plugin)
+            else:
+                raise UnsupportedPluginType("Passed plugin type is not yet supported")
+
+            self.loaded_plugins.append(plugin)
+
+        @staticmethod
+        def _load_laser_plugin(plugin):
+            LaserPluginLoader().load(plugin)
+
+        def _load_default_enabled(self):
+            for plugin_name in PluginDiscovery().get_plugins(default_enabled=True):
+                plugin = PluginDiscovery().build_plugin(
+                    plugin_name, self.plugin_args.get(plugin_name, {}))
+                self.load(plugin)
 
     mods["mythril.laser.plugin.builder"].PluginBuilder = PluginBuilder
     mods["mythril.laser.plugin.interface"].LaserPlugin = LaserPlugin
-    mods["mythril.plugin.interface"].MythrilLaserPlugin = MythrilLaserPlugin
+    mods["mythril.laser.plugin.loader"].LaserPluginLoader = LaserPluginLoader
+    pi = mods["mythril.plugin.interface"]
+    pi.MythrilPlugin, pi.MythrilCLIPlugin, pi.MythrilLaserPlugin = MythrilPlugin, MythrilCLIPlugin, MythrilLaserPlugin
+    mods["mythril.plugin.discovery"].PluginDiscovery = PluginDiscovery
+    mods["mythril.plugin.loader"].MythrilPluginLoader = MythrilPluginLoader
+    mods["mythril.plugin.loader"].UnsupportedPluginType = UnsupportedPluginType
     return mods, types.SimpleNamespace(
-        Bool=Bool, Model=Model, Optimize=Optimize, Constraints=Constraints, WorldState=WorldState,
-        ModelCache=ModelCache, UnsatError=UnsatError, SolverTimeOutException=SolverTimeOutException,
-        LaserPlugin=LaserPlugin, PluginBuilder=PluginBuilder, MythrilLaserPlugin=MythrilLaserPlugin,
-        funnel=funnel, kfm=kfm)
+        Bool=Bool, Model=Model, Optimize=Optimize, Solver=Solver, Constraints=Constraints,
+        WorldState=WorldState, ModelCache=ModelCache, UnsatError=UnsatError,
+        SolverTimeOutException=SolverTimeOutException, SolverStatistics=SolverStatistics,
+        LaserPlugin=LaserPlugin, PluginBuilder=PluginBuilder, MythrilPlugin=MythrilPlugin,
+        MythrilLaserPlugin=MythrilLaserPlugin, LaserPluginLoader=LaserPluginLoader,
+        PluginDiscovery=PluginDiscovery, MythrilPluginLoader=MythrilPluginLoader,
+        Singleton=Singleton, funnel=funnel, kfm=kfm)
 
 
-def install(monkeypatch, z3):
+def install(monkeypatch, z3, installed_plugins=None):
     """Register the stand-ins (and z3) in sys.modules for one test."""
-    mods, ns = build(z3)
+    mods, ns = build(z3, installed_plugins)
+    # integration.install() sets process defaults (PF_TORCH, PF_DEVICES): undo them with the test
+    for var in ("PF_TORCH", "PF_DEVICES", "LOCAL_RANK"):
+        if var in os.environ:
+            monkeypatch.setenv(var, os.environ[var])
+        else:
+            monkeypatch.setenv(var, "")
+            monkeypatch.delenv(var)
     monkeypatch.setitem(sys.modules, "z3", z3)
     for k, v in mods.items():
         monkeypatch.setitem(sys.modules, k, v)

@@ -2,15 +2,14 @@
 (mythril_amd/integration.py).
 
 Mythril itself is not importable here (z3, eth_abi, eth_hash missing — SURVEY §8c), so the
-plugin classes are exercised against minimal stand-ins of the three Mythril interfaces they
-subclass (mythril/laser/plugin/interface.py, mythril/laser/plugin/builder.py,
-mythril/plugin/interface.py:40-46) and a stand-in symbolic VM exposing ``laser_hook`` and
-``open_states`` (svm.py:133-145, 726-741).  The batch itself runs on the GPU over states
+plugin classes are exercised against the Mythril plugin stack restated line for line
+(tests/mythril_standin.py: the interfaces they subclass, discovery and both loaders) and a
+stand-in symbolic VM exposing ``laser_hook`` and ``open_states`` (svm.py:133-145, 726-741).  The batch itself runs on the GPU over states
 whose constraints are mythril_amd.smt terms (the drop-in facade); with z3 present the same
 function reads z3 ASTs through SMT-LIB2.
 """
 
-import sys
+import os
 import types
 
 import pytest
@@ -19,49 +18,33 @@ from mythril_amd import integration
 from mythril_amd.smt import ULT, symbol_factory
 from mythril_amd.smt.to_dag import UFRegistry
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _entry_points():
+    """The ``"mythril.plugins"`` entry points the package metadata declares (setup.cfg
+    ``[options.entry_points]``; test_wheel_declares_the_entry_point builds the wheel)."""
+    import configparser
+
+    cfg = configparser.ConfigParser()
+    cfg.read(os.path.join(ROOT, "setup.cfg"))
+    out = {}
+    for line in cfg["options.entry_points"]["mythril.plugins"].strip().splitlines():
+        name, value = (x.strip() for x in line.split("=", 1))
+        out[name] = value
+    return out
+
 
 @pytest.fixture
 def stub_mythril(monkeypatch):
-    """Register stand-ins for the Mythril plugin interfaces in sys.modules."""
+    """The Mythril plugin stack restated line for line (tests/mythril_standin.py:
+    plugin/interface.py:6-46, laser/plugin/builder.py:6-21, laser/plugin/loader.py:12-75,
+    plugin/discovery.py, plugin/loader.py), with the package's declared entry points as the
+    installed plugins."""
+    import fake_z3
+    import mythril_standin
 
-    class LaserPlugin:  # mythril/laser/plugin/interface.py
-        def initialize(self, symbolic_vm):
-            raise NotImplementedError
-
-    class PluginBuilder:  # mythril/laser/plugin/builder.py
-        name = "default"
-
-        def __init__(self):
-            self.enabled = True
-
-    class MythrilPlugin:  # mythril/plugin/interface.py
-        author = "Default Author"
-        name = "Plugin Name"
-        plugin_license = "All rights reserved."
-        plugin_type = "Mythril Plugin"
-        plugin_version = "0.0.1 "
-        plugin_description = "This is an example plugin description"
-
-    class MythrilLaserPlugin(MythrilPlugin):  # mythril/plugin/interface.py:40-46
-        def __call__(self, *args, **kwargs):
-            raise NotImplementedError
-
-    mods = {
-        "mythril": types.ModuleType("mythril"),
-        "mythril.laser": types.ModuleType("mythril.laser"),
-        "mythril.laser.plugin": types.ModuleType("mythril.laser.plugin"),
-        "mythril.laser.plugin.builder": types.ModuleType("mythril.laser.plugin.builder"),
-        "mythril.laser.plugin.interface": types.ModuleType("mythril.laser.plugin.interface"),
-        "mythril.plugin": types.ModuleType("mythril.plugin"),
-        "mythril.plugin.interface": types.ModuleType("mythril.plugin.interface"),
-    }
-    mods["mythril.laser.plugin.builder"].PluginBuilder = PluginBuilder
-    mods["mythril.laser.plugin.interface"].LaserPlugin = LaserPlugin
-    mods["mythril.plugin.interface"].MythrilLaserPlugin = MythrilLaserPlugin
-    for k, v in mods.items():
-        monkeypatch.setitem(sys.modules, k, v)
-    return types.SimpleNamespace(LaserPlugin=LaserPlugin, PluginBuilder=PluginBuilder,
-                                 MythrilLaserPlugin=MythrilLaserPlugin)
+    return mythril_standin.install(monkeypatch, fake_z3, installed_plugins=_entry_points())
 
 
 class FakeSVM:
@@ -79,32 +62,97 @@ class FakeSVM:
 
 
 def test_plugin_builder_contract(stub_mythril):
-    """discovery.py:71 reads plugin_default_enabled; SymExecWrapper calls the builder and
-    initialize(symbolic_vm) (analysis/symbolic.py:169, laser/plugin/loader.py:55-75)."""
+    """discovery.py:71 reads plugin_default_enabled; the builder is a MythrilLaserPlugin
+    (so also a LASER PluginBuilder, plugin/interface.py:40) built with keyword arguments
+    (discovery.py:57) that still carries ``enabled`` (laser/plugin/builder.py:14-15)."""
     laser_cls, builder_cls = integration._plugin_classes()
     assert issubclass(builder_cls, stub_mythril.MythrilLaserPlugin)
     assert issubclass(builder_cls, stub_mythril.PluginBuilder)
+    assert issubclass(builder_cls, stub_mythril.MythrilPlugin)
     assert builder_cls.plugin_default_enabled is True
     assert builder_cls.name == "mythril-amd-path-feasibility"
-    plugin = builder_cls()()
+    b = builder_cls(**{})
+    assert b.enabled is True
+    plugin = b()
     assert isinstance(plugin, stub_mythril.LaserPlugin)
+    assert integration._plugin_classes() is integration._plugin_classes()   # built once
 
 
-def test_plugin_initialize_registers_tx_boundary_hook(stub_mythril, monkeypatch):
-    """initialize() rebinds the funnel's Optimize once and registers a stop_sym_trans hook
-    that batches every open state (svm.py:307-308 runs it right before the next
-    iteration's is_possible() pass, svm.py:279-283)."""
-    calls = {"install": 0, "batch": []}
-    monkeypatch.setattr(integration, "install", lambda: calls.__setitem__("install", calls["install"] + 1))
+def test_reference_loader_sequence_reaches_the_hook(stub_mythril, monkeypatch):
+    """The construction sequence of a real ``myth analyze`` with the package installed:
+    ``MythrilPluginLoader()`` (cli.py:32) loads every default-enabled entry point —
+    ``PluginDiscovery.build_plugin`` -> ``plugin(**{})`` (discovery.py:50-57) ->
+    ``LaserPluginLoader().load`` (plugin/loader.py:65-68) — and ``SymExecWrapper`` then calls
+    ``instrument_virtual_machine(laser, None)`` (analysis/symbolic.py:169), which reads
+    ``.enabled``, builds the LASER plugin and initialises it (laser/plugin/loader.py:55-75);
+    LASER fires ``stop_sym_trans`` after each transaction (svm.py:306-307)."""
+    calls = {"batch": []}
     monkeypatch.setattr(integration, "batch_open_states",
-                        lambda states: calls["batch"].append(list(states)) or len(states))
-    _, builder_cls = integration._plugin_classes()
-    svm = FakeSVM(open_states=["s0", "s1", "s2"])
-    builder_cls()().initialize(svm)
-    assert calls["install"] == 1
-    assert list(svm.hooks) == ["stop_sym_trans"]
+                        lambda states: calls["batch"].append(list(states)) or 0)
+    ml = stub_mythril.MythrilPluginLoader()
+    assert [type(p).__name__ for p in ml.loaded_plugins] == ["MythrilAmdPluginBuilder"]
+    laser_loader = stub_mythril.LaserPluginLoader()
+    assert laser_loader.is_enabled("mythril-amd-path-feasibility")
+    svm = FakeSVM(open_states=["s0", "s1"])
+    laser_loader.instrument_virtual_machine(svm, None)
+    assert "mythril-amd-path-feasibility" in laser_loader.plugin_list
+    import sys
+    assert sys.modules["mythril.support.model"].Optimize.__name__ == "GpuOptimize"
+    assert os.environ.get("PF_DEVICES") == "all"     # one Mythril process drives every GPU
+    for hook in svm.hooks["stop_sym_trans"]:
+        hook()
+    assert calls["batch"] == [["s0", "s1"]]
+
+
+def test_install_keeps_an_explicit_device_choice(stub_mythril, monkeypatch):
+    """PF_DEVICES (or a launcher's LOCAL_RANK) wins over the all-devices default."""
+    monkeypatch.setenv("PF_DEVICES", "1")
+    integration.install()
+    assert os.environ["PF_DEVICES"] == "1"
+    monkeypatch.delenv("PF_DEVICES")
+    monkeypatch.setenv("LOCAL_RANK", "3")
+    integration.install()
+    assert "PF_DEVICES" not in os.environ
+
+
+def test_plugin_hook_never_raises(stub_mythril, monkeypatch):
+    """svm.py:306-307 runs the hook with no guard: an engine failure inside the batch must
+    not end the analysis."""
+    def boom(states):
+        raise RuntimeError("device lost")
+
+    monkeypatch.setattr(integration, "batch_open_states", boom)
+    monkeypatch.setattr(integration, "install", lambda: None)
+    svm = FakeSVM(open_states=["s0"])
+    integration._plugin_classes()[1](**{})().initialize(svm)
     svm.hooks["stop_sym_trans"][0]()
-    assert calls["batch"] == [["s0", "s1", "s2"]]
+
+
+def test_wheel_declares_the_entry_point(tmp_path):
+    """The package builds offline into a wheel whose entry_points.txt registers the builder
+    under ``mythril.plugins`` (what PluginDiscovery iterates, discovery.py:22-36)."""
+    import shutil
+    import subprocess
+    import sys
+    import zipfile
+
+    src = tmp_path / "src"
+    src.mkdir()
+    for f in ("pyproject.toml", "setup.cfg"):
+        shutil.copy(os.path.join(ROOT, f), src / f)
+    shutil.copytree(os.path.join(ROOT, "mythril_amd"), src / "mythril_amd",
+                    ignore=shutil.ignore_patterns("*.so", "__pycache__"))
+    r = subprocess.run([sys.executable, "-m", "pip", "wheel", "--no-deps", "--no-build-isolation",
+                        "--no-index", "-q", str(src), "-w", str(tmp_path / "dist")],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    whl, = (tmp_path / "dist").glob("mythril_amd-*.whl")
+    z = zipfile.ZipFile(whl)
+    ep = [n for n in z.namelist() if n.endswith("entry_points.txt")]
+    text = z.read(ep[0]).decode()
+    assert "[mythril.plugins]" in text
+    assert "mythril_amd = mythril_amd.integration:MythrilAmdPluginBuilder" in text
+    assert any(n.startswith("mythril_amd/integration.py") for n in z.namelist())
 
 
 class _BV:

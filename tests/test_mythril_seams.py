@@ -306,3 +306,170 @@ def test_gpu_funnel_and_deepcopy(monkeypatch, engine):
               ns.WorldState([B(z3.ULT(x, z3.BitVecVal(5, 256))), B(z3.ULT(z3.BitVecVal(9, 256), x))])]
     assert integration.batch_open_states(states, kfm=ns.kfm, registry=UFRegistry()) == 1
     assert [s.constraints.is_possible() for s in states] == [True, False]
+
+
+# ---- query accounting ---------------------------------------------------------
+def _mythril_stats():
+    import sys
+
+    return sys.modules["mythril.laser.smt.solver.solver_statistics"].SolverStatistics()
+
+
+def test_query_accounting_counts_each_query_once(standin):
+    """GpuOptimize.check carries Mythril's own @stat_smt_query (solver_statistics.py:7-25)
+    like BaseSolver.check (solver.py:72): a GPU-discharged query and a z3 fallback each
+    bump query_count by exactly one (not two), and "% discharged" is gpu_sat / query_count."""
+    integration.install()
+    st = _mythril_stats()
+    st.enabled = True                      # mythril_analyzer.py:147
+    B = standin.Bool
+    x = z3.BitVec("call_value1", 256)
+    opt = standin.funnel.Optimize()
+    opt.add(B(z3.ULT(x, z3.BitVecVal(50, 256))), B(x != z3.BitVecVal(0, 256)))
+    assert opt.check() == z3.sat
+    assert st.query_count == 1 and st.solver_time > 0
+    opt2 = standin.funnel.Optimize()     # contradiction: no witness -> z3 (the stand-in: unknown)
+    opt2.add(B(z3.ULT(x, z3.BitVecVal(5, 256))), B(z3.ULT(z3.BitVecVal(9, 256), x)))
+    assert opt2.check() == z3.unknown
+    assert st.query_count == 2
+    opt3 = standin.funnel.Optimize()     # objectives: z3 only, still counted once
+    opt3.add(B(z3.ULT(x, z3.BitVecVal(5, 256))))
+    opt3.minimize(B(x))
+    opt3.check()
+    assert st.query_count == 3
+    assert SolverStatistics().gpu_sat == 1
+    assert integration.discharge_ratio() == pytest.approx(1 / 3)
+    st.enabled = False
+    opt.check()
+    assert st.query_count == 3           # disabled statistics count nothing (:11-12)
+
+
+def test_funnel_query_count_through_is_possible(standin):
+    """Through the funnel (support/model.py:63-125): quick-sat hits never reach a solver, so
+    only the GPU query is counted — what Mythril's printed statistics show
+    (mythril_analyzer.py:187)."""
+    integration.install()
+    st = _mythril_stats()
+    st.enabled = True
+    B = standin.Bool
+    x = z3.BitVec("call_value1", 256)
+    assert standin.Constraints([B(z3.ULT(x, z3.BitVecVal(50, 256))), B(x != z3.BitVecVal(0, 256))]).is_possible()
+    assert standin.Constraints([B(z3.ULT(x, z3.BitVecVal(60, 256))), B(x != z3.BitVecVal(0, 256))]).is_possible()
+    assert st.query_count == 1
+    assert integration.discharge_ratio() == 1.0
+
+
+# ---- the witness eval never raises (support_utils.py:63-67 has no try) -------------------------
+def _unsupported_pred(a, b):
+    """A Bool operator outside the lowering's vocabulary (a signed-overflow predicate kind
+    the converter has no entry for)."""
+    d = z3.FuncDeclRef("bvsmul_noovfl", 0x7FFF, [a.sort(), b.sort()], z3.BoolSort())
+    return z3._mk(d, [a, b])
+
+
+def test_quick_sat_with_unsupported_op_moves_on_to_z3(standin):
+    """A GPU model sits in model_cache; a later query with an operator the converter rejects
+    is evaluated by check_quick_sat without raising (False: this model is skipped) and the
+    funnel then asks the solver — z3's own ModelRef.eval would not raise either."""
+    integration.install()
+    B = standin.Bool
+    x = z3.BitVec("call_value1", 256)
+    assert standin.Constraints([B(z3.ULT(x, z3.BitVecVal(50, 256))), B(x != z3.BitVecVal(0, 256))]).is_possible()
+    model = list(standin.funnel.model_cache.model_cache.lru_cache.keys())[0]
+    odd = _unsupported_pred(x, z3.BitVecVal(3, 256))
+    assert z3.is_false(model.eval(odd, model_completion=True))
+    assert standin.funnel.model_cache.check_quick_sat(z3.And(odd, x != z3.BitVecVal(0, 256))) is False
+    c = standin.Constraints([B(odd), B(x != z3.BitVecVal(0, 256))])
+    assert c.is_possible(solver_timeout=100) is True   # reached the (stand-in) solver: unknown
+
+
+def test_witness_eval_unsupported_op_by_substitution(standin):
+    """Substitution + simplify decides what it can: an unsupported op over concrete values
+    folds only if z3 folds it; a supported subterm still evaluates exactly."""
+    x = z3.BitVec("call_value1", 256)
+    internal = _witness_model([z3.ULT(x, z3.BitVecVal(1000, 256)), x != z3.BitVecVal(0, 256)])
+    view = integration.Z3WitnessView(internal)
+    xv = view.eval(x, model_completion=True).as_long()
+    # a BitVec expression with an unsupported Bool inside: returned partially evaluated
+    d = z3.FuncDeclRef("bvfoo", 0x7FFE, [x.sort()], x.sort())
+    e = z3._mk(d, [x + 1])
+    r = view.eval(e, model_completion=True)
+    assert r.decl().name() == "bvfoo" and z3.is_bv_value(r.arg(0)) and r.arg(0).as_long() == xv + 1
+
+
+def test_witness_eval_without_completion_returns_unassigned_symbols(standin):
+    """model_completion=False (model.py:45-59 contract): a symbol the witness does not
+    interpret comes back as itself, an expression over it partially evaluated; assigned
+    symbols evaluate to their values."""
+    x = z3.BitVec("call_value1", 256)
+    internal = _witness_model([z3.ULT(x, z3.BitVecVal(1000, 256)), x != z3.BitVecVal(0, 256)])
+    view = integration.Z3WitnessView(internal)
+    other = z3.BitVec("sender_7", 256)
+    assert view.eval(other, model_completion=False) is other
+    assert view.eval(other, model_completion=True).as_long() == 0
+    xv = view.eval(x, model_completion=False)
+    assert z3.is_bv_value(xv) and 0 < xv.as_long() < 1000
+    part = view.eval(other + x, model_completion=False)
+    assert not z3.is_bv_value(part)
+    assert any(z3.is_bv_value(a) and a.as_long() == xv.as_long() for a in part.children())
+
+
+def test_batch_skips_states_that_do_not_convert(standin):
+    """An open state with an unconvertible constraint is left to z3; the others are still
+    batched (the hook must not abort the symbolic run, svm.py:306-307)."""
+    B = standin.Bool
+    x = z3.BitVec("x", 256)
+    good = standin.WorldState([B(z3.ULT(x, z3.BitVecVal(10, 256)))])
+    bad = standin.WorldState([B(_unsupported_pred(x, z3.BitVecVal(2, 256)))])
+    assert integration.batch_open_states([bad, good], kfm=standin.kfm, registry=UFRegistry()) == 1
+    assert integration._lookup_batch(integration.state_terms(good)) is not None
+
+
+def test_batch_survives_an_engine_error(standin, monkeypatch):
+    def boom(*a, **k):
+        raise RuntimeError("device lost")
+
+    monkeypatch.setattr(gpu_check, "check_sets", boom)
+    B = standin.Bool
+    s = standin.WorldState([B(z3.ULT(z3.BitVec("x", 256), z3.BitVecVal(10, 256)))])
+    assert integration.batch_open_states([s], kfm=standin.kfm, registry=UFRegistry()) == 0
+
+
+# ---- parent models in the live path (SURVEY §7 step 4; instructions.py:1638,1662) ------------------
+def test_child_query_starts_from_the_parent_witness(standin, monkeypatch):
+    """A child = the parent's constraints + one JUMPI condition.  With the host hints off,
+    the bucket the condition changes starts its search from the parent's witness values
+    (candidate 0 = the parent model), recorded from the parent query's witness."""
+    from dataclasses import replace
+
+    cfg = replace(gpu_check.CONFIG, hints=False, budget=4096)
+    x = z3.BitVec("call_value1", 256)
+    k1, k2 = 0xDEADBEEF_0000_1234_5678, 0x0BAD_F00D_9999_0000_0000_1111
+    v = k1 ^ k2
+    pc = (x ^ z3.BitVecVal(k1, 256)) == z3.BitVecVal(k2, 256)
+    parent = converter(z3).terms([pc])
+    # the generator does not find it from scratch at this budget (not a harvested constant) ...
+    assert gpu_check.check_sets([parent], config=replace(cfg, parents=False))[0] is None
+    # ... a z3 model of the parent (the funnel notes it, integration._note_z3_model)
+    gpu_check.note_values({"call_value1": v})
+    child = converter(z3).terms([pc, z3.ULT(z3.BitVecVal(5, 256), x)])
+    m = gpu_check.check_sets([child], config=cfg)[0]
+    assert m is not None and m.origin == "parent"
+    assert m.w.vars["call_value1"] == v
+    # a sibling whose new condition the parent value misses: mutations of it search on
+    y = z3.BitVec("call_value2", 256)
+    gpu_check.note_values({"call_value2": v})
+    sib = converter(z3).terms([z3.Extract(255, 8, y) == z3.BitVecVal(v >> 8, 248),
+                               z3.Extract(7, 0, y) != z3.BitVecVal(v & 0xFF, 8)])
+    m2 = gpu_check.check_sets([sib], config=cfg)[0]
+    assert m2 is not None and m2.origin == "search"
+    assert (m2.w.vars["call_value2"] >> 8) == (v >> 8)
+
+
+def test_gpu_witness_feeds_later_parents(standin):
+    """Accepted witnesses are recorded per symbol: a later query over the same symbol gets
+    them as its parent model."""
+    x = z3.BitVec("call_value1", 256)
+    m = _witness_model([z3.ULT(x, z3.BitVecVal(1000, 256)), x != z3.BitVecVal(0, 256)])
+    got = gpu_check._recent_parent(converter(z3).terms([z3.ULT(x, z3.BitVecVal(7, 256))]))
+    assert got == {"call_value1": m.w.vars["call_value1"]}
