@@ -170,8 +170,15 @@ enum pf_var_kind {
     PF_VK_GENERIC = 0, /* plain BitVec symbol                                          */
     PF_VK_ACTOR = 1,   /* sender_*: const[hint0 .. hint0+hint1) are the actor addresses */
     PF_VK_KECCAK = 2,  /* keccak UF output slot: const[hint0] + 64*k, k < 2^117         */
-    PF_VK_SMALL = 3,   /* sizes: uniform in [0, hint0]                                  */
-    PF_VK_BOOL = 4     /* free Bool symbol                                              */
+    PF_VK_SMALL = 3,   /* sizes: uniform in [0, hint0], or ABI-aligned (4 + 32 k)       */
+    PF_VK_BOOL = 4,    /* free Bool symbol                                              */
+    PF_VK_CDBYTE = 5,  /* calldata byte at a constant offset: hint0 = its bit position in
+                          its big-endian ABI word (selector or 32-byte argument, bits
+                          0..7) | K << 8 | start << 20 (the set's word constants are
+                          const[start .. start+K), 12 bits each; K = 0: the whole pool),
+                          hint1 = the word's id (bytes of one word share it)            */
+    PF_VK_VALUE = 6    /* call values (call_value<tx>): 0 in half the candidates (every
+                          non-payable function requires it), else PF_VK_GENERIC        */
 };
 #define PF_NO_PARENT 0xffffffffu
 
@@ -205,8 +212,23 @@ typedef struct pf_set_desc {
  * of the candidates are few-variable mutations of the parent (hint) model.
  * PF_VK_ACTOR: m[1] % 4 < hint1 -> const[hint0 + m[1] % 4], else generic.
  * PF_VK_KECCAK: const[hint0] + ((r[0..3] & (2^117 - 1)) << 6).
- * PF_VK_SMALL: r[0] % (hint0 + 1).   PF_VK_BOOL: r[0] & 1.
+ * PF_VK_SMALL: if (m[0] & 16) and 4 <= hint0 < 2^32 - 1, the ABI-aligned size
+ *   4 + 32 (r[1] % ((hint0 - 4) / 32 + 1)) (selector + whole argument words, what the ABI
+ *   size checks compare against), else r[0] % (hint0 + 1).   PF_VK_BOOL: r[0] & 1.
+ * PF_VK_VALUE: 0 if (m[0] & 16), else the PF_VK_GENERIC rules.
+ * PF_VK_CDBYTE (LASER's calldata bytes, state/calldata.py:233-246): one hash per
+ *   (candidate, ABI word) u = mix32(cand ^ key0 ^ hint1 * 0x9E3779B9) — so every byte of
+ *   one word takes the same decision; with s = hint0 & 0xff, K = (hint0 >> 8) & 0xfff and
+ *   start = hint0 >> 20 (K = 0: start = 0, K = n_const), if (u & 1) and K > 0 the byte is
+ *   ((const[start + (u >> 1) % K] + {0, +1, -1, 0}[u >> 30]) mod 2^256 >> s) & 0xff: a
+ *   whole selector or argument word spelled from one harvested constant or its neighbour
+ *   (a dispatcher's `selector == 0xa9059cbb` needs all four bytes at once, an argument
+ *   bound `x < c` the word c - 1); else the PF_VK_GENERIC rules at width 8.
+ *   mix32(x): x ^= x >> 16; x *= 0x7feb352d; x ^= x >> 15; x *= 0x846ca68b; x ^= x >> 16.
  * All results are masked to the variable's width.                                  */
+#define PF_MIX_M1 0x7feb352du
+#define PF_MIX_M2 0x846ca68bu
+#define PF_CDWORD_MUL 0x9E3779B9u
 /* PF_W_HASH with salt s of value x (limbs x0..x7):
  *   h = Philox(ctr=(x0,x1,x2,x3), key=(s, 0x5BD1E995)),
  *   g = Philox(ctr=(x4^h0, x5^h1, x6^h2, x7^h3), key=(s, 0x27D4EB2F)),

@@ -51,6 +51,103 @@ int pfl_hints(const uint32_t* nodes, size_t n_nodes, const uint32_t* const_pool,
               const uint32_t* soft, uint32_t* hints_out, int* n_sat_out);
 int pfl_version(void);
 
+/* ---- term store: constraint terms -> DAG -> program, natively (csrc/pf_terms.cpp) -------
+ * The native form of mythril_amd/smt/to_dag.py:TermLowering + lower.py:Dag, node for node,
+ * followed by pfl_hints and pfl_lower (tests/test_native_terms.py).  Reference interface it
+ * serves: the objective-free query path of mythril/support/model.py:63-125 (one bucket per
+ * call; the fork-prune call site svm.py:351-358 poses two queries per fork).
+ *
+ * Terms (mythril_amd/smt/terms.py) enter the store once, children first; pflt_add returns
+ * the term's id (or -1).  op = PFLT_* below; sortk 0 Bool / 1 bit-vector (w1 = width) /
+ * 2 array (w1 = domain, w2 = range); i0/i1 = extract hi/lo or zero_extend's count; limbs =
+ * a constant's value (little-endian u32); name = symbol, array or function name (for an
+ * operator the store does not lower: its SMT-LIB name, quoted in the error). */
+#define PFLT_BV 1
+#define PFLT_TRUE 2
+#define PFLT_FALSE 3
+#define PFLT_VAR 4
+#define PFLT_BVAR 5
+#define PFLT_ARRAY 6
+#define PFLT_K 7
+#define PFLT_SELECT 8
+#define PFLT_STORE 9
+#define PFLT_APPLY 10
+#define PFLT_EXTRACT 11
+#define PFLT_CONCAT 12
+#define PFLT_ZERO_EXTEND 13
+#define PFLT_ITE 14
+#define PFLT_EQ 15
+#define PFLT_IFF 16
+#define PFLT_AND 17
+#define PFLT_OR 18
+#define PFLT_NOT 19
+#define PFLT_XOR 20
+#define PFLT_BVNOT 21
+#define PFLT_BVNEG 22
+#define PFLT_BVADD 30
+#define PFLT_BVSUB 31
+#define PFLT_BVMUL 32
+#define PFLT_BVUDIV 33
+#define PFLT_BVUREM 34
+#define PFLT_BVSDIV 35
+#define PFLT_BVSREM 36
+#define PFLT_BVSMOD 37
+#define PFLT_BVAND 38
+#define PFLT_BVOR 39
+#define PFLT_BVXOR 40
+#define PFLT_BVSHL 41
+#define PFLT_BVLSHR 42
+#define PFLT_BVASHR 43
+#define PFLT_BVEXP 44
+#define PFLT_BVULT 50
+#define PFLT_BVULE 51
+#define PFLT_BVSLT 52
+#define PFLT_BVSLE 53
+#define PFLT_BVUADD_NOOVF 54
+#define PFLT_BVUMUL_NOOVF 55
+#define PFLT_OTHER 99
+/* var_terms descriptor types: the variable's term / select(array a, index b) /
+ * extract(hi c, lo b) of term a */
+#define PFLT_VT_TERM 0
+#define PFLT_VT_SELECT 1
+#define PFLT_VT_EXTRACT 2
+/* pflt_lower flags */
+#define PFLT_HINTS 1u    /* derive the hint model (seed.apply_hints) */
+#define PFLT_PROGRAM 2u  /* allocate registers and emit (lower.lower) */
+/* pflt_result_get selectors */
+#define PFLT_GET_VARS 0
+#define PFLT_GET_VAR_TERMS 1
+#define PFLT_GET_UF_APPS 2
+#define PFLT_GET_READS 3
+#define PFLT_GET_CODE 4
+#define PFLT_GET_CONSTS 5
+#define PFLT_GET_NODES 6
+#define PFLT_GET_POOL 7
+#define PFLT_GET_ROOTS 8
+#define PFLT_GET_FORCED 9
+
+void* pflt_store_new(void);
+void pflt_store_free(void* store);
+size_t pflt_store_size(void* store);
+int64_t pflt_add(void* store, uint32_t op, uint32_t sortk, uint32_t w1, uint32_t w2, const uint32_t* args,
+                 uint32_t nargs, int64_t i0, int64_t i1, const uint32_t* limbs, uint32_t nlimbs,
+                 const char* name);
+/* Lower one bucket (roots = its conjuncts' term ids).  registry = n_actors, actors x 8 u32,
+ * n_specs, then per keccak width: n, has_lo, base x 8, n_concrete, per concrete hash: the
+ * input value (ceil(n / 32) u32) and the digest (8 u32).  Parent models: symbol names
+ * ('\0'-separated) with values (per name: its limb count, then the limbs — any width), and
+ * array reads (array id, index id) with values (8 u32 each).  Returns a result handle (0 and *rc_out = -2 when the set leaves the lowering's
+ * vocabulary or register file: LoweringError -> z3; -1 on malformed input); the message is
+ * in pflt_last_error().  flags: PFLT_HINTS | PFLT_PROGRAM. */
+void* pflt_lower(void* store, const uint32_t* roots, size_t n_roots, const uint32_t* registry,
+                 size_t n_registry, const char* par_names, const uint32_t* par_name_vals, size_t n_par_names,
+                 const uint32_t* par_reads, const uint32_t* par_read_vals, size_t n_par_reads,
+                 uint32_t flags, uint32_t seed, int* rc_out);
+const char* pflt_last_error(void);
+void pflt_result_free(void* result);
+void pflt_result_info(void* result, uint64_t* info);  /* 14 sizes, see pf_terms.cpp */
+void pflt_result_get(void* result, uint32_t which, uint32_t* out, char* names_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -85,6 +85,7 @@ class _PlantedEval(Witness):
         self.uf_apps = []
         self._memo = {}
         self._tables = planted.arrays
+        self._pos = None
         self._keccak_tables = {}
 
 
@@ -456,6 +457,25 @@ def _calldata(rng, fn: Fn, actors_used: List[int], k: Contract) -> bytes:
         out += v.to_bytes(32, "big")
     if fn.name == "batchTransfer":
         out += int(rng.integers(1, 25)).to_bytes(32, "big")   # receivers.length
+    return out
+
+
+def live_order_groups(queries: Sequence[Query]) -> List[List[Query]]:
+    """The queries as a live analysis poses them, in issue order: both successors of a fork
+    together (svm.py:351-358 checks a fork's pair back to back) and each tx-boundary query
+    on its own (svm.py:279-283)."""
+    out: List[List[Query]] = []
+    cur: List[Query] = []
+    key = None
+    for q in queries:
+        k = q.origin.rsplit(":", 1)[0] if q.origin.endswith((":T", ":F")) else q.origin
+        if k != key and cur:
+            out.append(cur)
+            cur = []
+        key = k
+        cur.append(q)
+    if cur:
+        out.append(cur)
     return out
 
 

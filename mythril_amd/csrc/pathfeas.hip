@@ -396,6 +396,9 @@ int pf_batch_create_on(int device, const uint32_t* code, size_t n_ins, const uin
             if (kind == PF_VK_KECCAK && sc[1] >= d.n_const) return fail("set %zu var %u: keccak base", s, v);
             if (kind == PF_VK_ACTOR && (sc[2] > 4 || sc[1] + sc[2] > d.n_const))
                 return fail("set %zu var %u: actor table", s, v);
+            if (kind == PF_VK_CDBYTE && ((sc[1] & 0xffu) > 248u || (sc[1] & 7u) ||
+                                         (sc[1] >> 20) + ((sc[1] >> 8) & 0xfffu) > d.n_const))
+                return fail("set %zu var %u: calldata word constants", s, v);
         }
         max_vars = std::max(max_vars, d.n_vars);
     }

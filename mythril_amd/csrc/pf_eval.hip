@@ -344,6 +344,12 @@ PF_INL u256 gen_var(const SetCtx& S, uint32_t v, uint32_t cand) {
         out = pf::add256(base, k);
     } else if (kind == PF_VK_SMALL) {
         out.l[0] = (hint0 == 0xffffffffu) ? r0.x : (r0.x % (hint0 + 1u));
+#ifndef PF_DIAG_NO_LASER_ARMS
+        if (hint0 >= 4u && hint0 != 0xffffffffu) {  // uniform: ABI-aligned sizes in half the lanes
+            const uint32_t al = 4u + 32u * (r0.y % ((hint0 - 4u) / 32u + 1u));
+            out.l[0] = (m.x & 16u) ? al : out.l[0];
+        }
+#endif
     } else if (kind == PF_VK_BOOL) {
         out.l[0] = r0.x & 1u;
     } else {
@@ -401,6 +407,39 @@ PF_INL u256 gen_var(const SetCtx& S, uint32_t v, uint32_t cand) {
             // the actor set (transaction/symbolic.py:215) in most lanes
             out.l[i] = act ? g.l[i] : out.l[i];
         }
+#ifndef PF_DIAG_NO_LASER_ARMS  // timing probe only: the LASER-aware arms compiled out
+        if (kind == PF_VK_VALUE) {  // uniform: call values are 0 in half the lanes
+#pragma unroll
+            for (int i = 0; i < 8; i++) out.l[i] = (m.x & 16u) ? 0u : out.l[i];
+        }
+        if (kind == PF_VK_CDBYTE) {
+            // calldata bytes (uniform branch, after the generic arms so nothing of it lives
+            // across the Philox blocks): one hash per (candidate, ABI word) decides whether
+            // the word is spelled from one of the set's word constants const[ws .. ws + wk)
+            // (+-1), which every byte of the word then agrees on
+            uint32_t wk = (hint0 >> 8) & 0xfffu, ws = hint0 >> 20;
+            if (wk == 0u) { wk = S.n_const; ws = 0u; }
+            if (wk) {
+                uint32_t u = cand ^ S.k0 ^ (hint1 * PF_CDWORD_MUL);
+                u ^= u >> 16; u *= PF_MIX_M1; u ^= u >> 15; u *= PF_MIX_M2; u ^= u >> 16;
+                const uint32_t cdd = u >> 30;  // the word's neighbour: +0, +1, -1, +0
+                const uint32_t* wp = S.consts + (size_t)(ws + (u >> 1) % wk) * 8u;
+                u256 cw, dl;
+#pragma unroll
+                for (int i = 0; i < 8; i++) cw.l[i] = wp[i];
+                dl.l[0] = cdd == 1u ? 1u : (cdd == 2u ? 0xffffffffu : 0u);
+#pragma unroll
+                for (int i = 1; i < 8; i++) dl.l[i] = cdd == 2u ? 0xffffffffu : 0u;
+                cw = pf::add256(cw, dl);
+                const uint32_t li = (hint0 >> 5) & 7u;
+                uint32_t word = cw.l[0];
+#pragma unroll
+                for (int i = 1; i < 8; i++) word = li == (uint32_t)i ? cw.l[i] : word;
+                const uint32_t byte = (word >> (hint0 & 24u)) & 0xffu;
+                out.l[0] = (u & 1u) ? byte : out.l[0];
+            }
+        }
+#endif
     }
     // the parent model itself (candidate 0) and its neighbourhood (odd candidates keep the
     // parent value of most variables)
@@ -817,6 +856,11 @@ PF_INL void search_item(const SetCtx& S, uint32_t set, uint32_t begin, uint32_t 
                         uint2* exp_tbl, uint64_t& evals_full, uint64_t& decided, uint64_t& ops,
                         uint32_t& cut, UnitProf& prof) {
     const uint32_t lane = threadIdx.x & 63u;
+    // the item's groups run in increasing candidate order, so its first witness is its
+    // smallest: one found[] atomic per item.  (Device-scope atomics are performed beyond the
+    // per-XCD L2s, so each is an HBM-side write request: one per witnessed group made the
+    // round-2 full sweep's 30 MB of WRITE_SIZE per launch.)
+    bool posted = false;
     for (uint32_t base = begin; base < end; base += 64u) {
         if (EARLY) {
             uint32_t f = __hip_atomic_load(found + set, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -841,9 +885,13 @@ PF_INL void search_item(const SetCtx& S, uint32_t set, uint32_t begin, uint32_t 
         decided += __popcll(m_act);
         evals_full += __popcll(m_full);
         ops += lane_ops * (uint64_t)__popcll(m_act);
-        if (m_sat) {
+#ifdef PF_DIAG_ALL_ATOMICS  // timing probe only: one found[] atomic per witnessed group
+        posted = false;
+#endif
+        if (m_sat && !posted) {
             uint32_t first = base + (uint32_t)__builtin_ctzll(m_sat);
             if (lane == 0) atomicMin(found + set, first);
+            posted = true;
             if (EARLY) break;
         }
     }

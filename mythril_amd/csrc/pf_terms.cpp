@@ -1,0 +1,1454 @@
+// pf_terms.cpp — libpflower.so: constraint terms -> bytecode DAG -> program, natively
+// (include/pf_lower.h, "term store" section).
+//
+// The native form of mythril_amd/smt/to_dag.py:TermLowering and mythril_amd/lower.py:Dag —
+// node for node: the same hash-consed node table (same order, same word-slicing rewrites),
+// the same variables (names, kinds, schema hints, parents), the same by-construction
+// interpretation of arrays, keccak256_<n> / inverse and Power, the same chunked wide values —
+// and then the hint derivation (pfl_hints) and register allocation (pfl_lower) of the same
+// library, so a bucket goes from terms to a program without a Python DAG in between.
+// tests/test_native_terms.py checks the node tables, variables, witness metadata and
+// programs against the Python lowering.  Host code, no HIP.
+//
+// Terms live in a store the host fills once per term (hash-consed Python terms are immortal,
+// so a term's store id never changes): children before parents.  A lowering call names the
+// bucket's roots, the keccak registry, the parent models and the program seed.
+#include <algorithm>
+#include <array>
+#include <cctype>
+#include <cstdlib>
+#include <tuple>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <unordered_map>
+#include <utility>
+#include <vector>
+
+#include "../../include/pf_bytecode.h"
+#include "../../include/pf_lower.h"
+
+namespace {
+
+thread_local std::string t_err;
+
+struct TermError {
+    int rc;
+};
+
+[[noreturn]] void lerr(const char* fmt, ...) {
+    char buf[256];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    t_err = buf;
+    throw TermError{-2};
+}
+
+// ---- big unsigned integers (term constants: any width) ---------------------------------
+typedef std::vector<uint32_t> Big;  // little-endian limbs, no trailing-zero normalisation
+
+uint32_t limb(const Big& v, size_t i) { return i < v.size() ? v[i] : 0u; }
+
+Big mask_big(const Big& v, uint32_t w) {
+    const size_t nl = (w + 31) / 32;
+    Big r(nl, 0u);
+    for (size_t i = 0; i < nl; i++) r[i] = limb(v, i);
+    if (w % 32 && nl) r[nl - 1] &= (1u << (w % 32)) - 1u;
+    return r;
+}
+
+Big shr_big(const Big& v, uint32_t s) {
+    const size_t q = s / 32, b = s % 32;
+    Big r;
+    for (size_t i = q; i < v.size(); i++) {
+        uint32_t x = v[i] >> b;
+        if (b && i + 1 < v.size()) x |= v[i + 1] << (32 - b);
+        r.push_back(x);
+    }
+    return r;
+}
+
+bool big_eq(const Big& a, const Big& b) {
+    const size_t n = std::max(a.size(), b.size());
+    for (size_t i = 0; i < n; i++)
+        if (limb(a, i) != limb(b, i)) return false;
+    return true;
+}
+
+bool big_zero(const Big& a) {
+    for (uint32_t x : a)
+        if (x) return false;
+    return true;
+}
+
+uint32_t bitlen(const Big& a) {
+    for (size_t i = a.size(); i-- > 0;)
+        if (a[i]) return (uint32_t)(32 * i + 32 - __builtin_clz(a[i]));
+    return 0;
+}
+
+// ---- 256-bit constants (DAG constant nodes) ------------------------------------------------
+struct C8 {
+    uint32_t l[8];
+    bool operator==(const C8& o) const { return memcmp(l, o.l, sizeof(l)) == 0; }
+};
+
+C8 c8_of(const Big& v, uint32_t w) {  // v masked to w <= 256 bits
+    C8 c;
+    const Big m = mask_big(v, w);
+    for (int i = 0; i < 8; i++) c.l[i] = limb(m, i);
+    return c;
+}
+
+C8 c8_small(uint64_t x, uint32_t w) {
+    Big b = {(uint32_t)x, (uint32_t)(x >> 32)};
+    return c8_of(b, w);
+}
+
+Big big_of(const C8& c) { return Big(c.l, c.l + 8); }
+
+// a * b mod 2^256 and b^e mod 2^256 (Power's concrete facts, pow(c1, c2, 1 << 256))
+C8 mul8(const C8& a, const C8& b) {
+    uint32_t r[8] = {0};
+    for (int i = 0; i < 8; i++) {
+        uint64_t c = 0;
+        for (int j = 0; i + j < 8; j++) {
+            c += (uint64_t)a.l[i] * b.l[j] + r[i + j];
+            r[i + j] = (uint32_t)c;
+            c >>= 32;
+        }
+    }
+    C8 o;
+    memcpy(o.l, r, sizeof(r));
+    return o;
+}
+
+C8 pow8(const C8& b, const C8& e) {
+    C8 r = c8_small(1, 256), x = b;
+    for (int i = 0; i < 256; i++) {
+        if ((e.l[i / 32] >> (i % 32)) & 1u) r = mul8(r, x);
+        x = mul8(x, x);
+    }
+    return r;
+}
+
+uint32_t crc32_of(const std::string& s) {  // zlib.crc32 (to_dag.salt_of)
+    uint32_t c = 0xffffffffu;
+    for (unsigned char ch : s) {
+        c ^= ch;
+        for (int k = 0; k < 8; k++) c = (c >> 1) ^ (0xEDB88320u & (0u - (c & 1u)));
+    }
+    return c ^ 0xffffffffu;
+}
+
+// ---- the term store -------------------------------------------------------------------
+struct TermRec {
+    uint32_t op, sortk, w1, w2;
+    std::vector<uint32_t> args;
+    int64_t i0, i1;
+    Big val;
+    std::string name;
+};
+
+struct Store {
+    std::vector<TermRec> t;
+};
+
+// ---- the DAG (mythril_amd/lower.py Dag) ---------------------------------------------------
+constexpr uint32_t K_VAR = PFL_K_VAR, K_CONST = PFL_K_CONST, K_BCONST = PFL_K_BCONST,
+                   K_BVAR = PFL_K_BVAR;
+
+struct DNode {
+    uint32_t kind, width, nargs;
+    int32_t args[3];
+    uint32_t aux;
+    C8 cv;  // K_CONST value
+    bool is_bool;
+};
+
+struct DVar {
+    std::string name;
+    uint32_t width, kind, hint0, hint1;
+    bool has_parent;
+    C8 parent;
+};
+
+struct Dag {
+    std::vector<DNode> nodes;
+    std::vector<int32_t> roots;
+    std::vector<DVar> vars;
+    std::vector<C8> forced;
+    std::unordered_map<std::string, int32_t> memo;
+    std::unordered_map<std::string, int32_t> var_index;
+
+    static std::string key_of(const DNode& n) {
+        std::string k;
+        k.append((const char*)&n.kind, 4);
+        k.append((const char*)&n.width, 4);
+        k.append((const char*)&n.nargs, 4);
+        k.append((const char*)n.args, 4 * n.nargs);
+        k.append((const char*)&n.aux, 4);
+        if (n.kind == K_CONST) k.append((const char*)n.cv.l, 32);
+        k.push_back(n.is_bool ? 1 : 0);
+        return k;
+    }
+
+    int32_t add(uint32_t kind, uint32_t width, std::initializer_list<int32_t> args, uint32_t aux,
+                bool is_bool, const C8* cv = nullptr) {
+        DNode n;
+        memset(&n, 0, sizeof(n));
+        n.kind = kind;
+        n.width = width;
+        n.nargs = (uint32_t)args.size();
+        int i = 0;
+        for (int32_t a : args) n.args[i++] = a;
+        n.aux = aux;
+        if (cv) n.cv = *cv;
+        n.is_bool = is_bool;
+        const std::string k = key_of(n);
+        auto it = memo.find(k);
+        if (it != memo.end()) return it->second;
+        const int32_t id = (int32_t)nodes.size();
+        nodes.push_back(n);
+        memo.emplace(k, id);
+        return id;
+    }
+
+    uint32_t force_consts(const std::vector<C8>& vals) {
+        const uint32_t start = (uint32_t)forced.size();
+        forced.insert(forced.end(), vals.begin(), vals.end());
+        return start;
+    }
+
+    int32_t var(const std::string& name, uint32_t width, uint32_t kind, uint32_t h0, uint32_t h1,
+                bool has_parent, const C8& parent, bool* created) {
+        auto it = var_index.find(name);
+        uint32_t idx;
+        *created = false;
+        if (it == var_index.end()) {
+            idx = (uint32_t)vars.size();
+            DVar v{name, width, kind, h0, h1, has_parent, parent};
+            vars.push_back(v);
+            var_index.emplace(name, (int32_t)idx);
+            *created = true;
+        } else {
+            idx = (uint32_t)it->second;
+        }
+        if (kind == PF_VK_BOOL) return add(K_BVAR, 1, {}, idx, true);
+        return add(K_VAR, width, {}, idx, false);
+    }
+
+    int32_t cnst(const C8& v, uint32_t width) {
+        C8 m = c8_of(big_of(v), width);
+        return add(K_CONST, width, {}, 0, false, &m);
+    }
+    int32_t cnst(uint64_t v, uint32_t width) { return cnst(c8_small(v, width), width); }
+    int32_t bconst(bool v) { return add(K_BCONST, 1, {}, v ? 1u : 0u, true); }
+
+    const C8* cval(int32_t i) const { return nodes[i].kind == K_CONST ? &nodes[i].cv : nullptr; }
+
+    int32_t op(uint32_t opc, uint32_t w, std::initializer_list<int32_t> args, uint32_t aux = 0) {
+        std::vector<int32_t> a(args);
+        const int32_t r = simplify(opc, w, a, aux);
+        if (r >= 0) return r;
+        const bool is_bool = opc >= PF_B_CONST;
+        switch (a.size()) {
+            case 1: return add(opc, w, {a[0]}, aux, is_bool);
+            case 2: return add(opc, w, {a[0], a[1]}, aux, is_bool);
+            case 3: return add(opc, w, {a[0], a[1], a[2]}, aux, is_bool);
+            default: return add(opc, w, {}, aux, is_bool);
+        }
+    }
+
+    // Dag._simplify: the word-slicing rewrites (lower.py)
+    int32_t simplify(uint32_t opc, uint32_t w, const std::vector<int32_t>& args, uint32_t aux) {
+        if (opc == PF_W_UDIV) {
+            const C8* c = cval(args[1]);
+            if (c) {
+                const Big cb = big_of(*c);
+                const uint32_t bl = bitlen(cb);
+                if (bl && bitlen(mask_big(shr_big(cb, 0), bl - 1)) == 0) {  // power of two
+                    const uint32_t k = bl - 1;
+                    return k == 0 ? args[0] : op(PF_W_LSHR, w, {args[0], cnst(k, w)});
+                }
+            }
+        } else if (opc == PF_W_LSHR) {
+            const C8* c = cval(args[1]);
+            const DNode x = nodes[args[0]];
+            if (c && bitlen(big_of(*c)) <= 32 && c->l[0] < w) {
+                const uint32_t k = c->l[0];
+                if (k == 0) return args[0];
+                if (x.kind == PF_W_MOV) {
+                    const int32_t inner = x.args[0];
+                    const uint32_t wi = nodes[inner].width;
+                    if (k >= wi) return cnst(0, w);
+                    return op(PF_W_MOV, w, {op(PF_W_EXTRACT, wi - k, {inner}, k)});
+                }
+                if (x.kind == PF_W_CONCAT) return op(PF_W_MOV, w, {op(PF_W_EXTRACT, w - k, {args[0]}, k)});
+            }
+        } else if (opc == PF_W_AND) {
+            for (int xi = 0; xi < 2; xi++) {
+                const int ci = 1 - xi;
+                const C8* c = cval(args[ci]);
+                if (!c) continue;
+                const Big cb = big_of(*c);
+                const uint32_t bl = bitlen(cb);
+                if (bl == 0) continue;
+                // c == 2^bl - 1
+                bool ones = true;
+                for (uint32_t i = 0; i < bl; i++)
+                    if (!((cb[i / 32] >> (i % 32)) & 1u)) { ones = false; break; }
+                if (ones && bl < w) return op(PF_W_MOV, w, {op(PF_W_EXTRACT, bl, {args[xi]}, 0)});
+            }
+        } else if (opc == PF_W_EXTRACT) {
+            const DNode x = nodes[args[0]];
+            if (aux == 0 && w == x.width) return args[0];
+            if (x.kind == PF_W_CONCAT) {
+                const int32_t hi = x.args[0], lo = x.args[1];
+                const uint32_t wl = x.aux;
+                if (aux >= wl) return op(PF_W_EXTRACT, w, {hi}, aux - wl);
+                if (aux + w <= wl) return op(PF_W_EXTRACT, w, {lo}, aux);
+                const int32_t top = op(PF_W_EXTRACT, aux + w - wl, {hi}, 0);
+                const int32_t bot = op(PF_W_EXTRACT, wl - aux, {lo}, aux);
+                return op(PF_W_CONCAT, w, {top, bot}, wl - aux);
+            }
+            if (x.kind == PF_W_MOV) {
+                const int32_t inner = x.args[0];
+                const uint32_t wi = nodes[inner].width;
+                if (aux + w <= wi) return op(PF_W_EXTRACT, w, {inner}, aux);
+                if (aux >= wi) return cnst(0, w);
+            }
+            if (x.kind == K_CONST) return cnst(c8_of(shr_big(big_of(x.cv), aux), w), w);
+        } else if (opc == PF_W_MOV) {
+            const DNode x = nodes[args[0]];
+            if (x.width == w) return args[0];
+            if (x.kind == PF_W_MOV) return op(PF_W_MOV, w, {x.args[0]});
+            if (x.kind == K_CONST) return cnst(x.cv, w);
+        } else if (opc == PF_B_EQ) {
+            for (int xi = 0; xi < 2; xi++) {
+                const int ci = 1 - xi;
+                const C8* c = cval(args[ci]);
+                const DNode x = nodes[args[xi]];
+                if (c && x.kind == PF_W_MOV) {
+                    const uint32_t wy = nodes[x.args[0]].width;
+                    if (!big_zero(shr_big(big_of(*c), wy))) return bconst(false);
+                    return op(PF_B_EQ, wy, {x.args[0], cnst(*c, wy)});
+                }
+            }
+        }
+        return -1;
+    }
+
+    // the calldata-byte arm's word constants (Dag.word_constants / finalize_word_hints)
+    void finalize_word_hints() {
+        bool any = false;
+        for (const DVar& v : vars) any |= v.kind == PF_VK_CDBYTE;
+        if (!any) return;
+        std::vector<C8> words;
+        for (const DNode& nd : nodes) {
+            if (!(nd.kind == PF_B_EQ || nd.kind == PF_B_ULT || nd.kind == PF_B_ULE ||
+                  nd.kind == PF_B_SLT || nd.kind == PF_B_SLE))
+                continue;
+            const DNode& a = nodes[nd.args[0]];
+            const DNode& b = nodes[nd.args[1]];
+            const DNode* pairs[2][2] = {{&a, &b}, {&b, &a}};
+            for (auto& pr : pairs) {
+                const DNode* c = pr[0];
+                const DNode* other = pr[1];
+                if (c->kind != K_CONST) continue;
+                if (other->kind == K_VAR && vars[other->aux].kind == PF_VK_SMALL) continue;
+                bool seen = false;
+                for (const C8& x : words) seen |= x == c->cv;
+                if (!seen) words.push_back(c->cv);
+            }
+        }
+        if (words.size() > 0xFFF) words.resize(0xFFF);
+        if (words.empty() || forced.size() >= 0xFFF) return;
+        const uint32_t start = force_consts(words);
+        for (DVar& v : vars)
+            if (v.kind == PF_VK_CDBYTE) v.hint0 = (v.hint0 & 0xFFu) | ((uint32_t)words.size() << 8) | (start << 20);
+    }
+};
+
+// ---- term lowering (to_dag.TermLowering) ---------------------------------------------------
+enum TOp : uint32_t {
+    T_BV = PFLT_BV, T_TRUE = PFLT_TRUE, T_FALSE = PFLT_FALSE, T_VAR = PFLT_VAR, T_BVAR = PFLT_BVAR,
+    T_ARRAY = PFLT_ARRAY, T_K = PFLT_K, T_SELECT = PFLT_SELECT, T_STORE = PFLT_STORE,
+    T_APPLY = PFLT_APPLY, T_EXTRACT = PFLT_EXTRACT, T_CONCAT = PFLT_CONCAT,
+    T_ZEXT = PFLT_ZERO_EXTEND, T_ITE = PFLT_ITE, T_EQ = PFLT_EQ, T_IFF = PFLT_IFF,
+    T_AND = PFLT_AND, T_OR = PFLT_OR, T_NOT = PFLT_NOT, T_XOR = PFLT_XOR, T_BVNOT = PFLT_BVNOT,
+    T_BVNEG = PFLT_BVNEG,
+};
+
+uint32_t wbin_op(uint32_t op) {
+    switch (op) {
+        case PFLT_BVADD: return PF_W_ADD;
+        case PFLT_BVSUB: return PF_W_SUB;
+        case PFLT_BVMUL: return PF_W_MUL;
+        case PFLT_BVUDIV: return PF_W_UDIV;
+        case PFLT_BVUREM: return PF_W_UREM;
+        case PFLT_BVSDIV: return PF_W_SDIV;
+        case PFLT_BVSREM: return PF_W_SREM;
+        case PFLT_BVSMOD: return PF_W_SMOD;
+        case PFLT_BVAND: return PF_W_AND;
+        case PFLT_BVOR: return PF_W_OR;
+        case PFLT_BVXOR: return PF_W_XOR;
+        case PFLT_BVSHL: return PF_W_SHL;
+        case PFLT_BVLSHR: return PF_W_LSHR;
+        case PFLT_BVASHR: return PF_W_ASHR;
+        case PFLT_BVEXP: return PF_W_EXP;
+        default: return 0;
+    }
+}
+
+uint32_t bcmp_op(uint32_t op) {
+    switch (op) {
+        case PFLT_BVULT: return PF_B_ULT;
+        case PFLT_BVULE: return PF_B_ULE;
+        case PFLT_BVSLT: return PF_B_SLT;
+        case PFLT_BVSLE: return PF_B_SLE;
+        case PFLT_BVUADD_NOOVF: return PF_B_UADD_NOOVF;
+        case PFLT_BVUMUL_NOOVF: return PF_B_UMUL_NOOVF;
+        default: return 0;
+    }
+}
+
+typedef std::vector<std::pair<int32_t, uint32_t>> Chunks;  // (node, width), LSB first
+
+struct Val {  // TermLowering.w(): a node, or chunks for values wider than 256 bits
+    bool wide;
+    int32_t node;
+    Chunks ch;
+};
+
+struct KSpec {
+    bool has_lo;
+    C8 base;
+    std::vector<std::pair<Big, C8>> concrete;  // insertion order (dict order)
+};
+
+// var_terms descriptors handed back to the host (Lowered.var_terms)
+struct VarTerm {
+    uint32_t type;  // PFLT_VT_TERM / PFLT_VT_SELECT / PFLT_VT_EXTRACT
+    uint32_t a, b;  // term id | (array id, index id) | (term id, lo)
+    uint32_t c;     // extract hi
+};
+
+struct Lowering {
+    const Store& S;
+    Dag d;
+    std::unordered_map<uint32_t, Val> memo;
+    std::vector<VarTerm> var_terms;
+    // base array name -> [(idx id, arr id, idx node, value node)]; names in insertion order
+    std::vector<std::string> array_order;
+    std::unordered_map<std::string, std::vector<std::array<int32_t, 4>>> arrays;
+    std::map<uint32_t, std::vector<std::pair<uint32_t, int32_t>>> keccak_apps;  // n -> (arg id, f node)
+    std::map<uint32_t, std::vector<std::pair<int32_t, int32_t>>> inv_apps;      // n -> (key node, value node)
+    std::vector<uint32_t> uf_apps;   // app term ids, registration order
+    std::vector<int32_t> side;
+    bool actors_forced = false;
+    uint32_t actor_start = 0;
+    std::vector<C8> actors;
+    std::map<uint32_t, KSpec> kspecs;
+    // Power: (b id, e id, value node, symbolic); concrete facts in discovery order
+    std::vector<std::tuple<uint32_t, uint32_t, int32_t, bool>> power_apps;
+    std::vector<std::pair<std::pair<C8, C8>, C8>> power_facts;
+    // parents: by symbol name, by (array id, index id)
+    std::unordered_map<std::string, Big> par_name;
+    std::map<std::pair<uint32_t, uint32_t>, C8> par_read;
+
+    explicit Lowering(const Store& s) : S(s) {}
+
+    const TermRec& T(uint32_t id) const { return S.t[id]; }
+    uint32_t width(uint32_t id) const { return T(id).sortk == 1 ? T(id).w1 : 0; }
+
+    // ---- leaves --------------------------------------------------------------------
+    static bool cdbyte_name(const std::string& name, uint32_t* off) {
+        // ^\d+_calldata\[(\d+)\]$
+        size_t i = 0;
+        while (i < name.size() && isdigit((unsigned char)name[i])) i++;
+        if (i == 0) return false;
+        static const char mid[] = "_calldata[";
+        if (name.compare(i, sizeof(mid) - 1, mid) != 0) return false;
+        i += sizeof(mid) - 1;
+        size_t j = i;
+        while (j < name.size() && isdigit((unsigned char)name[j])) j++;
+        if (j == i || j + 1 != name.size() || name[j] != ']') return false;
+        *off = (uint32_t)strtoul(name.c_str() + i, nullptr, 10);
+        return true;
+    }
+
+    static uint32_t var_kind(const std::string& name, uint32_t w) {
+        if (name.rfind("sender_", 0) == 0 && w == 256) return PF_VK_ACTOR;
+        const std::string suf = "_calldatasize";
+        if (name.size() >= suf.size() && name.compare(name.size() - suf.size(), suf.size(), suf) == 0)
+            return PF_VK_SMALL;
+        uint32_t off;
+        if (w == 8 && cdbyte_name(name, &off)) return PF_VK_CDBYTE;
+        if (w == 256 && (name.rfind("call_value", 0) == 0 || name.rfind("callvalue", 0) == 0))
+            return PF_VK_VALUE;
+        return PF_VK_GENERIC;
+    }
+
+    int32_t mkvar(const std::string& name, uint32_t w, const VarTerm& term, const C8* parent,
+                  const std::pair<uint32_t, uint32_t>* read) {
+        const uint32_t kind = var_kind(name, w);
+        uint32_t h0 = 0, h1 = 0;
+        if (kind == PF_VK_ACTOR) {
+            if (!actors_forced) {
+                actor_start = d.force_consts(actors);
+                actors_forced = true;
+            }
+            h0 = actor_start;
+            h1 = (uint32_t)actors.size();
+        } else if (kind == PF_VK_SMALL) {
+            h0 = 4 + 32 * 8;
+        } else if (kind == PF_VK_CDBYTE) {
+            uint32_t i;
+            cdbyte_name(name, &i);
+            if (i < 4) {
+                h0 = 8 * (3 - i);
+                h1 = 0xFFFFFFFFu;
+            } else {
+                h0 = 8 * (31 - (i - 4) % 32);
+                h1 = (i - 4) / 32;
+            }
+        }
+        C8 pv;
+        bool hp = false;
+        if (parent) {
+            pv = *parent;
+            hp = true;
+        } else {
+            auto it = par_name.find(name);
+            if (it != par_name.end()) {
+                pv = c8_of(it->second, 256);
+                hp = true;
+            } else if (read) {
+                auto jt = par_read.find(*read);
+                if (jt != par_read.end()) {
+                    pv = jt->second;
+                    hp = true;
+                }
+            }
+        }
+        if (hp) pv = c8_of(big_of(pv), w);  // Batch masks parents to the width
+        bool created;
+        const int32_t node = d.var(name, w, kind, h0, h1, hp, pv, &created);
+        if (created) var_terms.push_back(term);
+        return node;
+    }
+
+    // ---- generic lowering -----------------------------------------------------------
+    const Val& w(uint32_t t) {
+        auto it = memo.find(t);
+        if (it != memo.end()) return it->second;
+        Val v = lower_bv(t);
+        return memo.emplace(t, std::move(v)).first->second;
+    }
+
+    int32_t node(uint32_t t) {
+        const Val& v = w(t);
+        if (v.wide) lerr("%u-bit value used where <= 256 bits are required", width(t));
+        return v.node;
+    }
+
+    int32_t b(uint32_t t) {
+        auto it = memo.find(t);
+        if (it != memo.end()) return it->second.node;
+        const int32_t n = lower_bool(t);
+        memo.emplace(t, Val{false, n, {}});
+        return n;
+    }
+
+    static Val V(int32_t n) { return Val{false, n, {}}; }
+    static Val VW(Chunks c) { return Val{true, -1, std::move(c)}; }
+
+    Chunks chunks(uint32_t t) { return rechunk(pieces(t)); }
+
+    Chunks const_pieces(const Big& val, uint32_t wd) {
+        Chunks out;
+        Big v = val;
+        uint32_t rest = wd;
+        while (rest > 0) {
+            const uint32_t k = std::min<uint32_t>(rest, 256);
+            out.push_back({d.cnst(c8_of(v, k), k), k});
+            v = shr_big(v, k);
+            rest -= k;
+        }
+        return out;
+    }
+
+    Chunks pieces(uint32_t t) {
+        const TermRec& r = T(t);
+        const uint32_t wd = width(t);
+        if (wd <= 256) return {{node(t), wd}};
+        if (r.op == T_CONCAT) {
+            Chunks out;
+            for (size_t i = r.args.size(); i-- > 0;) {
+                Chunks p = pieces(r.args[i]);
+                out.insert(out.end(), p.begin(), p.end());
+            }
+            return out;
+        }
+        if (r.op == T_ZEXT) {
+            Chunks out = pieces(r.args[0]);
+            int64_t rest = r.i0;
+            while (rest > 0) {
+                const uint32_t k = (uint32_t)std::min<int64_t>(rest, 256);
+                out.push_back({d.cnst(0, k), k});
+                rest -= k;
+            }
+            return out;
+        }
+        if (r.op == T_BV) return const_pieces(r.val, wd);
+        const Val& v = w(t);
+        if (v.wide) return v.ch;
+        lerr("wide op %u", r.op);
+    }
+
+    Chunks rechunk(const Chunks& ps) {
+        Chunks out, cur;
+        uint32_t fill = 0;
+        for (const auto& pw : ps) {
+            const int32_t nd = pw.first;
+            const uint32_t wd = pw.second;
+            uint32_t off = 0;
+            while (off < wd) {
+                const uint32_t take = std::min(256 - fill, wd - off);
+                const int32_t part = (off == 0 && take == wd) ? nd : d.op(PF_W_EXTRACT, take, {nd}, off);
+                cur.push_back({part, take});
+                fill += take;
+                off += take;
+                if (fill == 256) {
+                    out.push_back(join(cur));
+                    cur.clear();
+                    fill = 0;
+                }
+            }
+        }
+        if (!cur.empty()) out.push_back(join(cur));
+        return out;
+    }
+
+    std::pair<int32_t, uint32_t> join(const Chunks& cur) {
+        int32_t nd = cur.back().first;
+        uint32_t wd = cur.back().second;
+        for (size_t i = cur.size() - 1; i-- > 0;) {
+            const int32_t part = cur[i].first;
+            const uint32_t pw = cur[i].second;
+            nd = d.op(PF_W_CONCAT, wd + pw, {nd, part}, pw);
+            wd += pw;
+        }
+        return {nd, wd};
+    }
+
+    Chunks slice(const Chunks& ch, uint32_t lo, uint32_t wid) {
+        Chunks ps;
+        uint32_t base = 0;
+        for (const auto& cw : ch) {
+            const uint32_t a = std::max(lo, base), bb = std::min(lo + wid, base + cw.second);
+            if (a < bb) {
+                if (a == base && bb == base + cw.second)
+                    ps.push_back(cw);
+                else
+                    ps.push_back({d.op(PF_W_EXTRACT, bb - a, {cw.first}, a - base), bb - a});
+            }
+            base += cw.second;
+        }
+        return rechunk(ps);
+    }
+
+    int32_t bit_to_w(int32_t bn, uint32_t wd) {
+        return d.op(PF_W_ITE, wd, {bn, d.cnst(1, wd), d.cnst(0, wd)});
+    }
+
+    Chunks wide_addsub(const Chunks& A, const Chunks& B, bool sub) {
+        const uint32_t opc = sub ? PF_W_SUB : PF_W_ADD;
+        Chunks out;
+        int32_t carry = -1;
+        const size_t n = std::min(A.size(), B.size());
+        for (size_t i = 0; i < n; i++) {
+            const int32_t x = A[i].first, y = B[i].first;
+            const uint32_t wx = A[i].second;
+            const int32_t t = d.op(opc, wx, {x, y});
+            int32_t s_ = t, cw = -1;
+            if (carry >= 0) {
+                cw = bit_to_w(carry, wx);
+                s_ = d.op(opc, wx, {t, cw});
+            }
+            if (i + 1 < A.size()) {
+                int32_t c1 = sub ? d.op(PF_B_ULT, wx, {x, y}) : d.op(PF_B_ULT, wx, {t, x});
+                if (carry >= 0) {
+                    const int32_t c2 = sub ? d.op(PF_B_ULT, wx, {t, cw}) : d.op(PF_B_ULT, wx, {s_, t});
+                    c1 = d.op(PF_B_OR, 1, {c1, c2});
+                }
+                carry = c1;
+            }
+            out.push_back({s_, wx});
+        }
+        return out;
+    }
+
+    int32_t wide_cmp(uint32_t op, uint32_t a, uint32_t bt) {
+        const Chunks A = chunks(a), B = chunks(bt);
+        const bool signed_ = op == PFLT_BVSLT || op == PFLT_BVSLE;
+        const bool strict = op == PFLT_BVULT || op == PFLT_BVSLT;
+        int32_t lt = -1;
+        const size_t n = std::min(A.size(), B.size());
+        for (size_t i = 0; i < n; i++) {
+            const bool top = i == A.size() - 1;
+            const uint32_t c = (signed_ && top) ? PF_B_SLT : PF_B_ULT;
+            const int32_t x = A[i].first, y = B[i].first;
+            const uint32_t wx = A[i].second;
+            int32_t li = d.op(c, wx, {x, y});
+            if (lt >= 0) li = d.op(PF_B_OR, 1, {li, d.op(PF_B_AND, 1, {d.op(PF_B_EQ, wx, {x, y}), lt})});
+            lt = li;
+        }
+        if (strict) return lt;
+        return d.op(PF_B_NOT, 1, {wide_cmp(signed_ ? PFLT_BVSLT : PFLT_BVULT, bt, a)});
+    }
+
+    Val lower_wide(uint32_t t) {
+        const TermRec& r = T(t);
+        const uint32_t wd = width(t);
+        if (r.op == T_CONCAT || r.op == T_ZEXT || r.op == T_BV) return VW(chunks(t));
+        if (r.op == T_VAR) {
+            Chunks out;
+            uint32_t lo = 0;
+            auto pit = par_name.find(r.name);
+            const bool hp = pit != par_name.end();
+            while (lo < wd) {
+                const uint32_t cw = std::min<uint32_t>(256, wd - lo);
+                C8 pv;
+                if (hp) pv = c8_of(shr_big(pit->second, lo), cw);
+                char nm[32];
+                snprintf(nm, sizeof(nm), "#%u", lo / 256);
+                VarTerm vt{PFLT_VT_EXTRACT, t, lo, lo + cw - 1};
+                out.push_back({mkvar(r.name + nm, cw, vt, hp ? &pv : nullptr, nullptr), cw});
+                lo += cw;
+            }
+            return VW(out);
+        }
+        if (r.op == T_APPLY) return apply(t);
+        if (r.op == T_ITE) {
+            const int32_t c = b(r.args[0]);
+            const Chunks a = chunks(r.args[1]), bb = chunks(r.args[2]);
+            Chunks out;
+            for (size_t i = 0; i < std::min(a.size(), bb.size()); i++)
+                out.push_back({d.op(PF_W_ITE, a[i].second, {c, a[i].first, bb[i].first}), a[i].second});
+            return VW(out);
+        }
+        if (r.op == T_EXTRACT) return VW(slice(chunks(r.args[0]), (uint32_t)r.i1, wd));
+        if (r.op == PFLT_BVADD || r.op == PFLT_BVSUB) {
+            const Chunks A = chunks(r.args[0]);  // operands in order (node numbering)
+            const Chunks B = chunks(r.args[1]);
+            return VW(wide_addsub(A, B, r.op == PFLT_BVSUB));
+        }
+        if (r.op == T_BVNEG) {
+            const Chunks A = chunks(r.args[0]);
+            Chunks zero;
+            for (const auto& c : A) zero.push_back({d.cnst(0, c.second), c.second});
+            return VW(wide_addsub(zero, A, true));
+        }
+        if (r.op == PFLT_BVAND || r.op == PFLT_BVOR || r.op == PFLT_BVXOR) {
+            const uint32_t opc = r.op == PFLT_BVAND ? PF_W_AND : (r.op == PFLT_BVOR ? PF_W_OR : PF_W_XOR);
+            const Chunks A = chunks(r.args[0]), B = chunks(r.args[1]);
+            Chunks out;
+            for (size_t i = 0; i < std::min(A.size(), B.size()); i++)
+                out.push_back({d.op(opc, A[i].second, {A[i].first, B[i].first}), A[i].second});
+            return VW(out);
+        }
+        if (r.op == T_BVNOT) {
+            Chunks out;
+            for (const auto& c : chunks(r.args[0])) out.push_back({d.op(PF_W_NOT, c.second, {c.first}), c.second});
+            return VW(out);
+        }
+        if ((r.op == PFLT_BVSHL || r.op == PFLT_BVLSHR) && T(r.args[1]).op == T_BV) {
+            const Big& kb = T(r.args[1]).val;
+            if (bitlen(kb) > 31 || limb(kb, 0) >= wd) return VW(rechunk(const_pieces(Big{}, wd)));
+            const uint32_t k = limb(kb, 0);
+            const Chunks A = chunks(r.args[0]);
+            Chunks zeros;
+            if (k) zeros = rechunk(const_pieces(Big{}, k));
+            Chunks cat;
+            if (r.op == PFLT_BVSHL) {
+                cat = zeros;
+                const Chunks s = slice(A, 0, wd - k);
+                cat.insert(cat.end(), s.begin(), s.end());
+            } else {
+                cat = slice(A, k, wd - k);
+                cat.insert(cat.end(), zeros.begin(), zeros.end());
+            }
+            return VW(rechunk(cat));
+        }
+        lerr("%u-bit %s", wd, r.name.empty() ? "op" : r.name.c_str());
+    }
+
+    Val lower_bv(uint32_t t) {
+        const TermRec& r = T(t);
+        const uint32_t wd = width(t);
+        if (wd > 256) return lower_wide(t);
+        if (r.op == T_BV) return V(d.cnst(c8_of(r.val, wd), wd));
+        if (r.op == T_VAR) return V(mkvar(r.name, wd, VarTerm{PFLT_VT_TERM, t, 0, 0}, nullptr, nullptr));
+        if (const uint32_t opc = wbin_op(r.op)) return V(d.op(opc, wd, {node(r.args[0]), node(r.args[1])}));
+        if (r.op == T_BVNOT) return V(d.op(PF_W_NOT, wd, {node(r.args[0])}));
+        if (r.op == T_BVNEG) return V(d.op(PF_W_NEG, wd, {node(r.args[0])}));
+        if (r.op == T_EXTRACT) {
+            const uint32_t lo = (uint32_t)r.i1, src = r.args[0];
+            if (width(src) <= 256) return V(d.op(PF_W_EXTRACT, wd, {node(src)}, lo));
+            const Chunks s = slice(chunks(src), lo, wd);
+            return V(s[0].first);
+        }
+        if (r.op == T_CONCAT) {
+            int32_t nd = node(r.args[0]);
+            uint32_t acc = width(r.args[0]);
+            for (size_t i = 1; i < r.args.size(); i++) {
+                const uint32_t pw = width(r.args[i]);
+                nd = d.op(PF_W_CONCAT, acc + pw, {nd, node(r.args[i])}, pw);
+                acc += pw;
+            }
+            return V(nd);
+        }
+        if (r.op == T_ZEXT) return V(d.op(PF_W_MOV, wd, {node(r.args[0])}));
+        if (r.op == T_ITE) {
+            const int32_t c = b(r.args[0]);
+            const int32_t x = node(r.args[1]);
+            const int32_t y = node(r.args[2]);
+            return V(d.op(PF_W_ITE, wd, {c, x, y}));
+        }
+        if (r.op == T_SELECT) return V(select(r.args[0], r.args[1]));
+        if (r.op == T_APPLY) return apply(t);
+        lerr("unsupported bit-vector op %s", r.name.c_str());
+    }
+
+    int32_t lower_bool(uint32_t t) {
+        const TermRec& r = T(t);
+        switch (r.op) {
+            case T_TRUE: return d.bconst(true);
+            case T_FALSE: return d.bconst(false);
+            case T_BVAR: {
+                auto it = par_name.find(r.name);
+                C8 pv;
+                const bool hp = it != par_name.end();
+                if (hp) pv = c8_of(it->second, 1);
+                bool created;
+                const int32_t nd = d.var(r.name, 1, PF_VK_BOOL, 0, 0, hp, pv, &created);
+                if (created) var_terms.push_back(VarTerm{PFLT_VT_TERM, t, 0, 0});
+                return nd;
+            }
+            case T_NOT: return d.op(PF_B_NOT, 1, {b(r.args[0])});
+            case T_AND:
+            case T_OR: {
+                const uint32_t opc = r.op == T_AND ? PF_B_AND : PF_B_OR;
+                int32_t acc = b(r.args[0]);
+                for (size_t i = 1; i < r.args.size(); i++) acc = d.op(opc, 1, {acc, b(r.args[i])});
+                return acc;
+            }
+            case T_XOR: {
+                const int32_t x = b(r.args[0]);
+                return d.op(PF_B_XOR, 1, {x, b(r.args[1])});
+            }
+            case T_IFF: {
+                const int32_t x = b(r.args[0]);
+                return d.op(PF_B_NOT, 1, {d.op(PF_B_XOR, 1, {x, b(r.args[1])})});
+            }
+            case T_ITE: {
+                const int32_t c = b(r.args[0]);
+                const int32_t x = b(r.args[1]);
+                return d.op(PF_B_ITE, 1, {c, x, b(r.args[2])});
+            }
+            case T_EQ: {
+                const uint32_t a = r.args[0], bt = r.args[1];
+                if (width(a) > 256 || width(bt) > 256) {
+                    const Chunks ca = chunks(a), cb = chunks(bt);
+                    int32_t acc = -1;
+                    for (size_t i = 0; i < std::min(ca.size(), cb.size()); i++) {
+                        const int32_t e = d.op(PF_B_EQ, ca[i].second, {ca[i].first, cb[i].first});
+                        acc = acc < 0 ? e : d.op(PF_B_AND, 1, {acc, e});
+                    }
+                    return acc;
+                }
+                const int32_t x = node(a);
+                return d.op(PF_B_EQ, width(a), {x, node(bt)});
+            }
+            default: break;
+        }
+        if (const uint32_t opc = bcmp_op(r.op)) {
+            const uint32_t a = r.args[0], bt = r.args[1];
+            if (width(a) > 256 && (r.op == PFLT_BVULT || r.op == PFLT_BVULE || r.op == PFLT_BVSLT ||
+                                   r.op == PFLT_BVSLE))
+                return wide_cmp(r.op, a, bt);
+            const int32_t x = node(a);
+            return d.op(opc, width(a), {x, node(bt)});
+        }
+        lerr("unsupported bool op %s", r.name.c_str());
+    }
+
+    // ---- arrays -----------------------------------------------------------------------
+    int32_t select(uint32_t arr, uint32_t idx) {
+        const TermRec& A = T(arr);
+        if (A.op == T_STORE) {
+            const uint32_t base = A.args[0], k = A.args[1], v = A.args[2];
+            if (k == idx) return node(v);
+            if (T(k).op == T_BV && T(idx).op == T_BV)
+                return big_eq(T(k).val, T(idx).val) ? node(v) : select(base, idx);
+            const int32_t rest = select(base, idx);
+            const int32_t c = d.op(PF_B_EQ, width(idx), {node(idx), node(k)});
+            return d.op(PF_W_ITE, A.w2, {c, node(v), rest});
+        }
+        if (A.op == T_K) return node(A.args[0]);
+        if (A.op == T_ITE) {
+            const int32_t c = b(A.args[0]);
+            const int32_t x = select(A.args[1], idx);
+            const int32_t y = select(A.args[2], idx);
+            return d.op(PF_W_ITE, A.w2, {c, x, y});
+        }
+        if (A.op != T_ARRAY) lerr("select over %s", A.name.c_str());
+        const std::string& name = A.name;
+        const uint32_t rng = A.w2;
+        if (width(idx) > 256) lerr("array index wider than 256 bits");
+        auto it = arrays.find(name);
+        if (it == arrays.end()) {
+            array_order.push_back(name);
+            it = arrays.emplace(name, std::vector<std::array<int32_t, 4>>()).first;
+        }
+        for (const auto& e : it->second)
+            if ((uint32_t)e[0] == idx) return e[3];
+        const int32_t inode = node(idx);
+        std::string vname;
+        if (T(idx).op == T_BV) {
+            // f"{name}[{idx.val}]": the index in decimal
+            vname = name + "[" + big_decimal(T(idx).val) + "]";
+        } else {
+            vname = name + "@" + std::to_string(arrays[name].size());
+        }
+        const std::pair<uint32_t, uint32_t> rd{arr, idx};
+        int32_t val = mkvar(vname, rng, VarTerm{PFLT_VT_SELECT, arr, idx, 0}, nullptr, &rd);
+        auto& entries = arrays[name];
+        for (size_t i = entries.size(); i-- > 0;) {
+            const auto& e = entries[i];
+            if (T((uint32_t)e[0]).op == T_BV && T(idx).op == T_BV) continue;
+            val = d.op(PF_W_ITE, rng, {d.op(PF_B_EQ, width(idx), {inode, e[2]}), e[3], val});
+        }
+        entries.push_back({(int32_t)idx, (int32_t)arr, inode, val});
+        return val;
+    }
+
+    static std::string big_decimal(const Big& v) {
+        Big x = v;
+        while (!x.empty() && x.back() == 0) x.pop_back();
+        if (x.empty()) return "0";
+        std::string s;
+        while (!x.empty()) {
+            uint64_t rem = 0;
+            for (size_t i = x.size(); i-- > 0;) {
+                const uint64_t cur = (rem << 32) | x[i];
+                x[i] = (uint32_t)(cur / 10);
+                rem = cur % 10;
+            }
+            s.push_back((char)('0' + rem));
+            while (!x.empty() && x.back() == 0) x.pop_back();
+        }
+        std::reverse(s.begin(), s.end());
+        return s;
+    }
+
+    // ---- uninterpreted functions ---------------------------------------------------------
+    int32_t hash_args(const std::vector<uint32_t>& args, uint32_t salt) {
+        int32_t h = -1;
+        for (uint32_t a : args) {
+            for (const auto& c : chunks(a)) {
+                const int32_t x = c.second == 256 ? c.first : d.op(PF_W_MOV, 256, {c.first});
+                h = d.op(PF_W_HASH, 256, {h < 0 ? x : d.op(PF_W_XOR, 256, {h, x})}, salt);
+            }
+        }
+        return h;
+    }
+
+    static bool keccak_name(const std::string& f, uint32_t* n, bool* inv) {
+        static const char pre[] = "keccak256_";
+        if (f.compare(0, sizeof(pre) - 1, pre) != 0) return false;
+        size_t i = sizeof(pre) - 1, j = i;
+        while (j < f.size() && isdigit((unsigned char)f[j])) j++;
+        if (j == i) return false;
+        *n = (uint32_t)strtoul(f.c_str() + i, nullptr, 10);
+        if (j == f.size()) {
+            *inv = false;
+            return true;
+        }
+        if (f.compare(j, std::string::npos, "-1") == 0) {
+            *inv = true;
+            return true;
+        }
+        return false;
+    }
+
+    Val apply(uint32_t t) {
+        const TermRec& r = T(t);
+        uint32_t n;
+        bool inv;
+        if (keccak_name(r.name, &n, &inv)) {
+            if (!inv) return V(keccak(n, r.args[0], t));
+            return keccak_inv(n, r.args[0], t);
+        }
+        if (r.name == "Power" && r.args.size() == 2 && width(t) == 256) return V(power(t));
+        uf_apps.push_back(t);
+        const int32_t h = hash_args(r.args, crc32_of(r.name));
+        return V(width(t) == 256 ? h : d.op(PF_W_EXTRACT, width(t), {h}, 0));
+    }
+
+    int32_t eq_terms_const(uint32_t a, const Big& c) {  // _eq_value(a, c) = _eq_terms(a, const(c))
+        const uint32_t wa = width(a);
+        if (wa <= 256) {
+            const int32_t x = node(a);
+            return d.op(PF_B_EQ, wa, {x, d.cnst(c8_of(c, wa), wa)});
+        }
+        const Chunks A = chunks(a);
+        const Chunks B = rechunk(const_pieces(mask_big(c, wa), wa));
+        int32_t acc = -1;
+        for (size_t i = 0; i < std::min(A.size(), B.size()); i++) {
+            const int32_t e = d.op(PF_B_EQ, A[i].second, {A[i].first, B[i].first});
+            acc = acc < 0 ? e : d.op(PF_B_AND, 1, {acc, e});
+        }
+        return acc;
+    }
+
+    int32_t eq_terms(uint32_t a, uint32_t bt) {
+        if (width(a) != width(bt)) return d.bconst(false);
+        if (width(a) <= 256) {
+            const int32_t x = node(a);
+            return d.op(PF_B_EQ, width(a), {x, node(bt)});
+        }
+        const Chunks A = chunks(a), B = chunks(bt);
+        int32_t acc = -1;
+        for (size_t i = 0; i < std::min(A.size(), B.size()); i++) {
+            const int32_t e = d.op(PF_B_EQ, A[i].second, {A[i].first, B[i].first});
+            acc = acc < 0 ? e : d.op(PF_B_AND, 1, {acc, e});
+        }
+        return acc;
+    }
+
+    int32_t keccak(uint32_t n, uint32_t arg, uint32_t t) {
+        auto& apps = keccak_apps[n];
+        for (const auto& a : apps)
+            if (a.first == arg) return a.second;
+        const int32_t h = hash_args({arg}, crc32_of("keccak256_" + std::to_string(n)));
+        int32_t val = h;
+        auto sit = kspecs.find(n);
+        if (sit != kspecs.end()) {
+            const KSpec& spec = sit->second;
+            if (spec.has_lo) {
+                Big m117;
+                for (int i = 0; i < 4; i++) m117.push_back(i < 3 ? 0xffffffffu : (1u << 21) - 1u);
+                const int32_t k = d.op(PF_W_AND, 256, {h, d.cnst(c8_of(m117, 256), 256)});
+                val = d.op(PF_W_ADD, 256, {d.cnst(spec.base, 256), d.op(PF_W_SHL, 256, {k, d.cnst(6, 256)})});
+            }
+            for (const auto& ck : spec.concrete) {
+                const int32_t eqs = eq_terms_const(arg, ck.first);
+                val = d.op(PF_W_ITE, 256, {eqs, d.cnst(ck.second, 256), val});
+            }
+        }
+        // injectivity on the set: f(a) = f(b) -> a = b
+        for (const auto& a : apps) {
+            const int32_t same_f = d.op(PF_B_EQ, 256, {val, a.second});
+            const int32_t same_x = eq_terms(arg, a.first);
+            side.push_back(d.op(PF_B_OR, 1, {d.op(PF_B_NOT, 1, {same_f}), same_x}));
+        }
+        keccak_apps[n].push_back({arg, val});
+        uf_apps.push_back(t);
+        return val;
+    }
+
+    Val keccak_inv(uint32_t n, uint32_t y, uint32_t t) {
+        const TermRec& Y = T(y);
+        uint32_t yn;
+        bool yinv;
+        if (Y.op == T_APPLY && keccak_name(Y.name, &yn, &yinv) && !yinv && yn == n) {
+            w(y);  // make sure f(x) is registered (injectivity constraints)
+            return w(Y.args[0]);
+        }
+        if (n > 256) lerr("inverse keccak of a wide input on a non-application");
+        const int32_t ynode = node(y);
+        const std::string vname = "keccak256_" + std::to_string(n) + "-1@" + std::to_string(inv_apps[n].size());
+        int32_t val = mkvar(vname, n, VarTerm{PFLT_VT_TERM, t, 0, 0}, nullptr, nullptr);
+        auto& entries = inv_apps[n];
+        for (size_t i = entries.size(); i-- > 0;)
+            val = d.op(PF_W_ITE, n, {d.op(PF_B_EQ, 256, {ynode, entries[i].first}), entries[i].second, val});
+        auto kit = keccak_apps.find(n);
+        if (kit != keccak_apps.end()) {
+            const auto& ka = kit->second;
+            for (size_t i = ka.size(); i-- > 0;) {
+                const int32_t eq = d.op(PF_B_EQ, 256, {ynode, ka[i].second});
+                val = d.op(PF_W_ITE, n, {eq, node(ka[i].first), val});
+            }
+        }
+        inv_apps[n].push_back({ynode, val});
+        uf_apps.push_back(t);
+        return V(val);
+    }
+
+    int32_t power(uint32_t t) {
+        const TermRec& r = T(t);
+        const uint32_t bt = r.args[0], et = r.args[1];
+        for (const auto& pa : power_apps)
+            if (std::get<0>(pa) == bt && std::get<1>(pa) == et) return std::get<2>(pa);
+        int32_t val;
+        const bool sym = !(T(bt).op == T_BV && T(et).op == T_BV);
+        if (!sym) {
+            val = d.cnst(pow8(c8_of(T(bt).val, 256), c8_of(T(et).val, 256)), 256);
+        } else {
+            const int32_t bn = node(bt), en = node(et);
+            size_t nsym = 0;
+            for (const auto& pa : power_apps) nsym += std::get<3>(pa) ? 1 : 0;
+            val = mkvar("Power@" + std::to_string(nsym), 256, VarTerm{PFLT_VT_TERM, t, 0, 0}, nullptr, nullptr);
+            for (size_t i = power_apps.size(); i-- > 0;) {
+                const auto& pa = power_apps[i];
+                if (!std::get<3>(pa)) continue;
+                const int32_t e1 = d.op(PF_B_EQ, 256, {bn, node(std::get<0>(pa))});
+                const int32_t same = d.op(PF_B_AND, 1, {e1, d.op(PF_B_EQ, 256, {en, node(std::get<1>(pa))})});
+                val = d.op(PF_W_ITE, 256, {same, std::get<2>(pa), val});
+            }
+            const int32_t one = d.cnst(1, 256);  // Python's argument order: 1 first
+            const int32_t sh = d.op(PF_W_SHL, 256, {d.op(PF_W_AND, 256, {en, d.cnst(31, 256)}), d.cnst(3, 256)});
+            const int32_t rule = d.op(PF_W_SHL, 256, {one, sh});
+            val = d.op(PF_W_ITE, 256, {d.op(PF_B_EQ, 256, {bn, d.cnst(256, 256)}), rule, val});
+            for (const auto& f : power_facts) {
+                const int32_t e1 = d.op(PF_B_EQ, 256, {bn, d.cnst(f.first.first, 256)});
+                const int32_t same = d.op(PF_B_AND, 1, {e1, d.op(PF_B_EQ, 256, {en, d.cnst(f.first.second, 256)})});
+                val = d.op(PF_W_ITE, 256, {same, d.cnst(f.second, 256), val});
+            }
+        }
+        power_apps.emplace_back(bt, et, val, sym);
+        uf_apps.push_back(t);
+        return val;
+    }
+
+    void collect_power_facts(const std::vector<uint32_t>& roots) {
+        std::vector<uint32_t> stack(roots.begin(), roots.end());
+        std::vector<char> seen(S.t.size(), 0);
+        while (!stack.empty()) {
+            const uint32_t x = stack.back();
+            stack.pop_back();
+            if (seen[x]) continue;
+            seen[x] = 1;
+            const TermRec& r = T(x);
+            if (r.op == T_APPLY && r.name == "Power" && r.args.size() == 2 && T(r.args[0]).op == T_BV &&
+                T(r.args[1]).op == T_BV) {
+                const C8 c1 = c8_of(T(r.args[0]).val, 256), c2 = c8_of(T(r.args[1]).val, 256);
+                const C8 pv = pow8(c1, c2);
+                bool found = false;
+                for (auto& f : power_facts)
+                    if (f.first.first == c1 && f.first.second == c2) {
+                        f.second = pv;
+                        found = true;
+                    }
+                if (!found) power_facts.push_back({{c1, c2}, pv});
+            }
+            for (uint32_t a : r.args) stack.push_back(a);
+        }
+    }
+
+    void lower(const std::vector<uint32_t>& roots) {
+        collect_power_facts(roots);
+        for (uint32_t c : roots) {
+            if (T(c).sortk != 0) lerr("constraint is not a Bool");
+            if (T(c).op == T_TRUE) continue;
+            const int32_t r = b(c);
+            if (!d.nodes[r].is_bool) lerr("root is not a Bool");
+            d.roots.push_back(r);
+        }
+        for (int32_t s : side) d.roots.push_back(s);
+    }
+};
+
+// ---- results ------------------------------------------------------------------------------
+struct Result {
+    Dag dag;
+    std::vector<VarTerm> var_terms;
+    std::vector<uint32_t> uf_apps;
+    std::vector<uint32_t> reads;   // (array id, index id) pairs, arrays in insertion order
+    std::vector<uint32_t> read_counts;  // entries per array, same order
+    std::vector<uint32_t> code;    // n_ins x 4
+    std::vector<uint32_t> consts;  // n_const x 8
+    std::vector<uint32_t> packed_nodes, pool;  // pack_nodes of the DAG (tests)
+    std::string names;             // variable names, '\0'-separated
+    uint32_t n_wregs = 0;
+    int n_sat = 0;
+};
+
+void pack(const Dag& d, std::vector<uint32_t>* nodes, std::vector<uint32_t>* pool) {
+    nodes->clear();
+    pool->clear();
+    uint32_t np = 0;
+    for (const DNode& n : d.nodes) {
+        uint32_t aux = n.aux;
+        if (n.kind == K_CONST) {
+            aux = np++;
+            pool->insert(pool->end(), n.cv.l, n.cv.l + 8);
+        }
+        const uint32_t a0 = n.nargs > 0 ? (uint32_t)n.args[0] : 0u, a1 = n.nargs > 1 ? (uint32_t)n.args[1] : 0u,
+                       a2 = n.nargs > 2 ? (uint32_t)n.args[2] : 0u;
+        const uint32_t rec[8] = {n.kind, n.width, n.nargs, a0, a1, a2, aux, n.is_bool ? 1u : 0u};
+        nodes->insert(nodes->end(), rec, rec + 8);
+    }
+    if (nodes->empty()) nodes->assign(8, 0u);
+}
+
+}  // namespace
+
+extern "C" {
+
+void* pflt_store_new(void) { return new Store(); }
+
+void pflt_store_free(void* st) { delete (Store*)st; }
+
+size_t pflt_store_size(void* st) { return ((Store*)st)->t.size(); }
+
+int64_t pflt_add(void* st, uint32_t op, uint32_t sortk, uint32_t w1, uint32_t w2, const uint32_t* args,
+                 uint32_t nargs, int64_t i0, int64_t i1, const uint32_t* limbs, uint32_t nlimbs,
+                 const char* name) {
+    Store* S = (Store*)st;
+    TermRec r;
+    r.op = op;
+    r.sortk = sortk;
+    r.w1 = w1;
+    r.w2 = w2;
+    for (uint32_t i = 0; i < nargs; i++) {
+        if (args[i] >= S->t.size()) {
+            t_err = "pflt_add: argument not in the store";
+            return -1;
+        }
+        r.args.push_back(args[i]);
+    }
+    r.i0 = i0;
+    r.i1 = i1;
+    if (limbs) r.val.assign(limbs, limbs + nlimbs);
+    if (name) r.name = name;
+    S->t.push_back(std::move(r));
+    return (int64_t)S->t.size() - 1;
+}
+
+void* pflt_lower(void* st, const uint32_t* roots, size_t n_roots, const uint32_t* registry,
+                 size_t n_registry, const char* par_names, const uint32_t* par_name_vals, size_t n_par_names,
+                 const uint32_t* par_reads, const uint32_t* par_read_vals, size_t n_par_reads,
+                 uint32_t flags, uint32_t seed, int* rc_out) {
+    (void)seed;
+    Store* S = (Store*)st;
+    Result* R = new Result();
+    try {
+        Lowering L(*S);
+        // registry: n_actors, actors x 8; n_specs; per spec: n, has_lo, base x 8, n_concrete,
+        // per concrete: value limbs (ceil(n / 32)), digest x 8
+        size_t p = 0;
+        auto take = [&](void) -> uint32_t {
+            if (p >= n_registry) lerr("registry blob truncated");
+            return registry[p++];
+        };
+        const uint32_t na = take();
+        for (uint32_t i = 0; i < na; i++) {
+            C8 c;
+            for (int k = 0; k < 8; k++) c.l[k] = take();
+            L.actors.push_back(c);
+        }
+        const uint32_t ns = take();
+        for (uint32_t s = 0; s < ns; s++) {
+            const uint32_t n = take();
+            KSpec sp;
+            sp.has_lo = take() != 0;
+            for (int k = 0; k < 8; k++) sp.base.l[k] = take();
+            const uint32_t nc = take();
+            for (uint32_t c = 0; c < nc; c++) {
+                Big v;
+                for (uint32_t k = 0; k < (n + 31) / 32; k++) v.push_back(take());
+                C8 dg;
+                for (int k = 0; k < 8; k++) dg.l[k] = take();
+                sp.concrete.push_back({v, dg});
+            }
+            L.kspecs[n] = sp;
+        }
+        // parent values by name: per name, its limb count then the limbs (any width)
+        const char* nm = par_names;
+        const uint32_t* pv = par_name_vals;
+        for (size_t i = 0; i < n_par_names; i++) {
+            const uint32_t nl = *pv++;
+            L.par_name.emplace(std::string(nm), Big(pv, pv + nl));
+            pv += nl;
+            nm += strlen(nm) + 1;
+        }
+        for (size_t i = 0; i < n_par_reads; i++) {
+            C8 c;
+            memcpy(c.l, par_read_vals + 8 * i, 32);
+            L.par_read.emplace(std::make_pair(par_reads[2 * i], par_reads[2 * i + 1]), c);
+        }
+        std::vector<uint32_t> rs(roots, roots + n_roots);
+        for (uint32_t r : rs)
+            if (r >= S->t.size()) lerr("root not in the store");
+        L.lower(rs);
+        R->var_terms = L.var_terms;
+        R->uf_apps = L.uf_apps;
+        for (const std::string& name : L.array_order) {
+            const auto& es = L.arrays[name];
+            R->read_counts.push_back((uint32_t)es.size());
+            for (const auto& e : es) {
+                R->reads.push_back((uint32_t)e[1]);
+                R->reads.push_back((uint32_t)e[0]);
+            }
+        }
+        Dag& d = L.d;
+        // hints (seed.apply_hints): the hint model becomes every variable's parent value
+        if ((flags & PFLT_HINTS) && !d.vars.empty()) {
+            pack(d, &R->packed_nodes, &R->pool);
+            std::vector<uint32_t> widths, soft, out(8 * d.vars.size());
+            for (const DVar& v : d.vars) {
+                widths.push_back(v.width);
+                for (int k = 0; k < 8; k++) soft.push_back(v.has_parent ? v.parent.l[k] : 0u);
+            }
+            std::vector<uint32_t> roots2(d.roots.begin(), d.roots.end());
+            if (roots2.empty()) roots2.push_back(0);
+            int n_sat = 0;
+            const int rc = pfl_hints(R->packed_nodes.data(), d.nodes.size(), R->pool.data(), R->pool.size() / 8,
+                                     roots2.data(), d.roots.size(), widths.data(), d.vars.size(), soft.data(),
+                                     out.data(), &n_sat);
+            if (rc != 0) {
+                t_err = "pfl_hints failed";
+                throw TermError{-1};
+            }
+            R->n_sat = n_sat;
+            for (size_t i = 0; i < d.vars.size(); i++) {
+                C8 c;
+                memcpy(c.l, out.data() + 8 * i, 32);
+                d.vars[i].parent = c8_of(big_of(c), d.vars[i].width);
+                d.vars[i].has_parent = true;
+            }
+        }
+        if (flags & PFLT_PROGRAM) {
+            d.finalize_word_hints();
+            pack(d, &R->packed_nodes, &R->pool);
+            std::vector<uint32_t> forced;
+            for (const C8& c : d.forced) forced.insert(forced.end(), c.l, c.l + 8);
+            std::vector<uint32_t> roots2(d.roots.begin(), d.roots.end());
+            if (roots2.empty()) roots2.push_back(0);
+            const uint32_t tries[2] = {PF_NW_NARROW, PF_NW};
+            int rc = -2;
+            for (int ti = 0; ti < 2; ti++) {
+                size_t cap_i = 16 * d.nodes.size() + 64 + 4 * d.roots.size();
+                size_t cap_c = R->pool.size() / 8 + d.forced.size() + 1;
+                size_t ni = 0, nc = 0;
+                for (int attempt = 0; attempt < 4; attempt++) {
+                    R->code.assign(4 * cap_i, 0u);
+                    R->consts.assign(8 * cap_c, 0u);
+                    rc = pfl_lower(R->packed_nodes.data(), d.nodes.size(), R->pool.data(), R->pool.size() / 8,
+                                   roots2.data(), d.roots.size(), forced.empty() ? nullptr : forced.data(),
+                                   d.forced.size(), tries[ti], R->code.data(), cap_i, &ni, R->consts.data(),
+                                   cap_c, &nc);
+                    if (rc != -3) break;
+                    cap_i *= 4;
+                    cap_c *= 4;
+                }
+                if (rc == 0) {
+                    R->code.resize(4 * ni);
+                    R->consts.resize(8 * nc);
+                    bool spills = false;
+                    for (size_t i = 0; i < ni; i++) spills |= (R->code[4 * i] & 0xffu) == PF_W_SPILL;
+                    R->n_wregs = tries[ti];
+                    if (ti == 0 && spills) continue;  // the wide register file instead
+                    break;
+                }
+                if (rc != -2) break;
+            }
+            if (rc != 0) {
+                t_err = pfl_last_error();
+                throw TermError{rc};
+            }
+        } else {
+            pack(d, &R->packed_nodes, &R->pool);
+        }
+        for (const DVar& v : d.vars) {
+            R->names += v.name;
+            R->names.push_back('\0');
+        }
+        R->dag = std::move(L.d);
+        *rc_out = 0;
+        return R;
+    } catch (const TermError& e) {
+        *rc_out = e.rc;
+        delete R;
+        return nullptr;
+    }
+}
+
+const char* pflt_last_error(void) { return t_err.c_str(); }
+
+void pflt_result_free(void* res) { delete (Result*)res; }
+
+/* sizes: [0] n_vars, [1] names bytes, [2] n_var_terms, [3] n_uf_apps, [4] n_arrays,
+ * [5] n_reads, [6] n_ins, [7] n_const, [8] n_nodes, [9] n_pool, [10] n_roots, [11] n_forced,
+ * [12] n_wregs, [13] n_sat */
+void pflt_result_info(void* res, uint64_t* info) {
+    const Result* R = (const Result*)res;
+    info[0] = R->dag.vars.size();
+    info[1] = R->names.size();
+    info[2] = R->var_terms.size();
+    info[3] = R->uf_apps.size();
+    info[4] = R->read_counts.size();
+    info[5] = R->reads.size() / 2;
+    info[6] = R->code.size() / 4;
+    info[7] = R->consts.size() / 8;
+    info[8] = R->dag.nodes.size();
+    info[9] = R->pool.size() / 8;
+    info[10] = R->dag.roots.size();
+    info[11] = R->dag.forced.size();
+    info[12] = R->n_wregs;
+    info[13] = (uint64_t)R->n_sat;
+}
+
+/* vars: n_vars x 12 u32 = width, kind, hint0, hint1, has_parent, parent x 8 ... (13 words)
+ * var_terms: n x 4; uf_apps: n; reads: n x 2 (array id, index id) + counts per array;
+ * code n_ins x 4; consts n_const x 8; nodes n_nodes x 8; pool n_pool x 8; roots; forced x 8 */
+void pflt_result_get(void* res, uint32_t which, uint32_t* out, char* names_out) {
+    const Result* R = (const Result*)res;
+    switch (which) {
+        case PFLT_GET_VARS:
+            for (const DVar& v : R->dag.vars) {
+                *out++ = v.width;
+                *out++ = v.kind;
+                *out++ = v.hint0;
+                *out++ = v.hint1;
+                *out++ = v.has_parent ? 1u : 0u;
+                for (int k = 0; k < 8; k++) *out++ = v.parent.l[k];
+            }
+            if (names_out) memcpy(names_out, R->names.data(), R->names.size());
+            break;
+        case PFLT_GET_VAR_TERMS:
+            for (const VarTerm& vt : R->var_terms) {
+                *out++ = vt.type;
+                *out++ = vt.a;
+                *out++ = vt.b;
+                *out++ = vt.c;
+            }
+            break;
+        case PFLT_GET_UF_APPS: std::copy(R->uf_apps.begin(), R->uf_apps.end(), out); break;
+        case PFLT_GET_READS:
+            out = std::copy(R->read_counts.begin(), R->read_counts.end(), out);
+            std::copy(R->reads.begin(), R->reads.end(), out);
+            break;
+        case PFLT_GET_CODE: std::copy(R->code.begin(), R->code.end(), out); break;
+        case PFLT_GET_CONSTS: std::copy(R->consts.begin(), R->consts.end(), out); break;
+        case PFLT_GET_NODES: std::copy(R->packed_nodes.begin(), R->packed_nodes.begin() + 8 * R->dag.nodes.size(), out); break;
+        case PFLT_GET_POOL: std::copy(R->pool.begin(), R->pool.end(), out); break;
+        case PFLT_GET_ROOTS:
+            for (int32_t r : R->dag.roots) *out++ = (uint32_t)r;
+            break;
+        case PFLT_GET_FORCED:
+            for (const C8& c : R->dag.forced) out = std::copy(c.l, c.l + 8, out);
+            break;
+        default: break;
+    }
+}
+
+}  // extern "C"

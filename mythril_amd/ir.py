@@ -10,9 +10,10 @@ The opcode numbers are checked against the C header by tests/test_abi.py.
 
 from __future__ import annotations
 
+import re
 import struct
 from dataclasses import dataclass, field
-from typing import List, Optional, Sequence
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -97,6 +98,21 @@ VK_ACTOR = 1
 VK_KECCAK = 2
 VK_SMALL = 3
 VK_BOOL = 4
+VK_CDBYTE = 5
+VK_VALUE = 6
+CDBYTE_RE = re.compile(r"^\d+_calldata\[(\d+)\]$")
+
+
+def cdbyte_hints(name: str) -> Tuple[int, int]:
+    """Schema hints of the PF_VK_CDBYTE variable ``{tx}_calldata[i]``: (bit position of the
+    byte in its big-endian ABI word, word id).  LASER reads calldata words big-endian
+    (state/calldata.py:233-246): bytes 0..3 are the selector (word id 0xFFFFFFFF), byte
+    4 + 32 k + j is byte j of argument word k."""
+    i = int(CDBYTE_RE.match(name).group(1))
+    if i < 4:
+        return 8 * (3 - i), 0xFFFFFFFF
+    k, j = divmod(i - 4, 32)
+    return 8 * (31 - j), k
 
 # ---- flags -----------------------------------------------------------------------
 FLAG_SHORTCIRCUIT = 1

@@ -169,6 +169,45 @@ class Dag:
                     return self.op(ir.B_EQ, wy, x.args[0], self.const(c, wy))
         return None
 
+    _CMP_OPS = (ir.B_EQ, ir.B_ULT, ir.B_ULE, ir.B_SLT, ir.B_SLE)
+
+    def word_constants(self) -> List[int]:
+        """Constants the set compares values against (selectors, bounds, addresses): the
+        calldata-byte generator arm spells whole ABI words from these (include/pf_bytecode.h
+        PF_VK_CDBYTE).  Comparisons with a size variable (LASER's per-byte ``i <s size``
+        guards, calldata.py:233-246) are skipped: their index constants would crowd out
+        the words that matter."""
+        nodes, out, seen = self.nodes, [], set()
+        for nd in nodes:
+            if nd.kind not in self._CMP_OPS:
+                continue
+            a, b = (nodes[x] for x in nd.args)
+            for c, other in ((a, b), (b, a)):
+                if c.kind != K_CONST:
+                    continue
+                if other.kind == K_VAR and self.vars[other.aux].kind == ir.VK_SMALL:
+                    continue
+                if c.aux not in seen:
+                    seen.add(c.aux)
+                    out.append(c.aux)
+        return out[:0xFFF]
+
+    def finalize_word_hints(self) -> None:
+        """Pin the word constants in the pool and point every calldata-byte variable at them
+        (hint0 bits 8..31: count and start); idempotent."""
+        if getattr(self, "_words_done", False):
+            return
+        self._words_done = True
+        cds = [v for v in self.vars if v.kind == ir.VK_CDBYTE]
+        if not cds:
+            return
+        words = self.word_constants()
+        if not words or len(self.forced) >= 0xFFF:
+            return
+        start = self.force_consts(words)
+        for v in cds:
+            v.hint0 = (v.hint0 & 0xFF) | (len(words) << 8) | (start << 20)
+
     def assert_(self, b: int) -> None:
         if not self.nodes[b].is_bool:
             raise LoweringError("root is not a Bool")
@@ -347,6 +386,7 @@ def lower(dag: Dag, seed: int = 0, name: str = "", nw: Optional[int] = None) -> 
     batch).  The native library when built (identical output, tests/test_native_lower.py),
     else the Python reference :func:`lower_py`."""
     if nw is None:
+        dag.finalize_word_hints()
         try:
             prog = lower(dag, seed, name, ir.NW_NARROW)
             if not _spills(prog):

@@ -76,6 +76,7 @@ class GpuStats:
     bucket_hits: int = 0     # buckets answered from the witness cache
     lowering_failures: Dict[str, int] = field(default_factory=dict)
     bucket_origin: Dict[str, int] = field(default_factory=dict)  # witness provenance per bucket
+    recheck_failures: int = 0  # GPU witnesses the host re-check rejected (must stay 0)
     kernel_ms: float = 0.0
     evals: int = 0
     host_s: float = 0.0      # lowering + hints + witness re-checks
@@ -94,6 +95,7 @@ _NEG: "OrderedDict[tuple, None]" = OrderedDict()
 # newest values of symbols (name -> value) and of base-array reads (array name ->
 # {select term -> value}) over the accepted witnesses and noted z3 models: the parent models
 _RECENT_VARS: "OrderedDict[str, int]" = OrderedDict()
+_RECHECK_DEBUG: list = []   # the last few re-check failures (bucket, lowered, values, program, index)
 _RECENT_READS: "OrderedDict[str, OrderedDict]" = OrderedDict()
 
 
@@ -175,7 +177,18 @@ def _set_seed(constraints: Sequence[T.Term]) -> int:
     return h & 0xFFFFFFFF
 
 
+_NATIVE_TERMS = os.environ.get("PF_NATIVE_TERMS", "1") != "0"
+
+
 def _lower_bucket(bucket: List[T.Term], reg: UFRegistry, parent: Optional[dict], hints: bool):
+    """Terms -> (witness metadata, program): natively in libpflower.so when it is built
+    (smt/native_terms.py, the same program node for node), else the Python reference
+    (to_dag.TermLowering -> seed.apply_hints -> lower.lower)."""
+    if _NATIVE_TERMS:
+        from . import native_terms
+
+        if native_terms.store() is not None:
+            return native_terms.lower_bucket(bucket, reg, parent, hints, _set_seed(bucket))
     tl = TermLowering(reg, parent)
     lo = tl.lower(bucket)
     if hints:
@@ -203,6 +216,7 @@ def _lower_chunk(job):
         try:
             lo, prog = _lower_bucket(bucket, reg, parent, hints)
             out.append((Lowered(None, lo.var_terms, lo.uf_apps, lo.array_reads), prog, None))
+            lo = None
         except (LoweringError, ValueError, OverflowError) as e:
             # one bucket the lowering cannot take (or whose native emission fails) is that
             # bucket's failure only: the rest of the batch is still searched
@@ -394,7 +408,14 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
             origin[key] = _origin(idx, progs[k], cfg.hints, parented[k])
             w = Witness(lows[k], v, reg)
             # re-check on the host under the same interpretation before trusting it
-            if all(w.ev(c) for c in key[0]):
+            if not all(w.ev(c) for c in key[0]):
+                # the program disagrees with the terms under this assignment: a lowering
+                # or interpretation bug — sound (the bucket stays unanswered), but counted
+                with _lock:
+                    STATS.recheck_failures += 1
+                    _RECHECK_DEBUG.append((key[0], lows[k], v, progs[k], int(res.found[k])))
+                    del _RECHECK_DEBUG[:-8]
+            else:
                 found[key] = (lows[k], v)
                 with _lock:
                     _CACHE[key] = (lows[k], v)

@@ -74,7 +74,8 @@ class Witness:
         self.array_reads = lowered.array_reads
         self.uf_apps = lowered.uf_apps
         self._memo: Dict[T.Term, object] = {}
-        self._tables: Optional[Dict[str, Dict[int, int]]] = None
+        self._tables: Optional[Dict[str, Dict[int, int]]] = None   # explicit arrays (planted models)
+        self._pos: Optional[Dict[str, Dict[T.Term, int]]] = None
         self._keccak_tables: Dict[int, List[Tuple[int, int]]] = {}
 
     @classmethod
@@ -93,33 +94,71 @@ class Witness:
             w.reads.update(p.reads)
             w.array_reads.update(p.array_reads)
             w.uf_apps.extend(p.uf_apps)
-        w._memo, w._tables, w._keccak_tables = {}, None, {}
+        w._memo, w._tables, w._pos, w._keccak_tables = {}, None, None, {}
         return w
 
     # ---- array interpretation: first earlier index with an equal value ------------------
-    def tables(self) -> Dict[str, Dict[int, int]]:
-        if self._tables is None:
-            self._tables = {}
-            for name, reads in self.array_reads.items():
-                tab: Dict[int, int] = {}
-                for it, sel in reads:
-                    iv = self.ev(it)
-                    if iv not in tab:
-                        tab[iv] = self.reads.get(sel, 0)
-                self._tables[name] = tab
-        return self._tables
+    # A read of base array A at index value iv is the value of the FIRST read of A, in the
+    # lowering's lookup order (to_dag.TermLowering._select), whose index evaluates to iv —
+    # for a read that is itself one of those entries, the first among the entries up to
+    # and including it.  The scan is per read and in order because the index of entry p may
+    # itself read A (or another array) through earlier entries (ABI dynamic offsets: a
+    # calldata read at an offset read from calldata): a table built up front evaluated
+    # those nested reads against an unfinished table (as 0), and the host re-check then
+    # rejected witnesses the kernel had rightly found.
+    def _entry_pos(self, name: str) -> Dict[T.Term, int]:
+        if self._pos is None:
+            self._pos = {}
+        pos = self._pos.get(name)
+        if pos is None:
+            pos = {}
+            for i, (_, sel) in enumerate(self.array_reads.get(name, ())):
+                pos.setdefault(sel, i)
+            self._pos[name] = pos
+        return pos
 
-    def _select(self, arr: T.Term, iv: int) -> int:
+    def _array_read(self, arr: T.Term, idx: Optional[T.Term], iv: int) -> int:
+        name = arr.val
+        reads = self.array_reads.get(name)
+        if not reads:
+            tabs = self._tables or {}
+            return tabs.get(name, {}).get(iv, 0)     # model completion: 0
+        last = len(reads) - 1
+        if idx is not None:
+            r = self._entry_pos(name).get(T.select(arr, idx))
+            if r is not None:
+                last = r
+        for i in range(last + 1):
+            it, sel = reads[i]
+            if self.ev(it) == iv:
+                return self.reads.get(sel, 0)
+        return 0
+
+    def tables(self) -> Dict[str, Dict[int, int]]:
+        """The arrays as {index value: value} maps (every read's index, first read wins)."""
+        out: Dict[str, Dict[int, int]] = {}
+        for name, reads in self.array_reads.items():
+            tab: Dict[int, int] = {}
+            for it, sel in reads:
+                iv = self.ev(it)
+                if iv not in tab:
+                    tab[iv] = self.reads.get(sel, 0)
+            out[name] = tab
+        for name, tab in (self._tables or {}).items():
+            out.setdefault(name, tab)
+        return out
+
+    def _select(self, arr: T.Term, iv: int, idx: Optional[T.Term] = None) -> int:
         if arr.op == "store":
             if self.ev(arr.args[1]) == iv:
                 return self.ev(arr.args[2])
-            return self._select(arr.args[0], iv)
+            return self._select(arr.args[0], iv, idx)
         if arr.op == "K":
             return self.ev(arr.args[0])
         if arr.op == "ite":
-            return self._select(arr.args[1] if self.ev(arr.args[0]) else arr.args[2], iv)
+            return self._select(arr.args[1] if self.ev(arr.args[0]) else arr.args[2], iv, idx)
         if arr.op == "array":
-            return self.tables().get(arr.val, {}).get(iv, 0)  # model completion: 0
+            return self._array_read(arr, idx, iv)
         raise ValueError(f"select over {arr.op}")
 
     # ---- UFs ----------------------------------------------------------------------------
@@ -228,7 +267,7 @@ class Witness:
         if op == "ite":
             return self.ev(t.args[1]) if self.ev(t.args[0]) else self.ev(t.args[2])
         if op == "select":
-            return self._select(t.args[0], self.ev(t.args[1]))
+            return self._select(t.args[0], self.ev(t.args[1]), t.args[1])
         if op == "apply":
             return self._apply(t)
         if op == "=":

@@ -89,6 +89,10 @@ def var_kind(name: str, w: int):
         return ir.VK_ACTOR
     if name.endswith("_calldatasize"):
         return ir.VK_SMALL
+    if w == 8 and ir.CDBYTE_RE.match(name):
+        return ir.VK_CDBYTE
+    if w == 256 and (name.startswith("call_value") or name.startswith("callvalue")):
+        return ir.VK_VALUE   # transaction/symbolic.py:137-138, transaction_models.py:121-124
     return ir.VK_GENERIC
 
 
@@ -125,6 +129,8 @@ class TermLowering:
             hint0, hint1 = self._actor_table()
         elif kind == ir.VK_SMALL:
             hint0 = 4 + 32 * 8
+        elif kind == ir.VK_CDBYTE:
+            hint0, hint1 = ir.cdbyte_hints(name)
         before = len(self.dag.vars)
         if parent is None and self.parent:
             # parent models are keyed by symbol name, or by the read's own (hash-consed)

@@ -202,7 +202,8 @@ def calldata_word(dag: Dag, tx: int, offset: int, size_node: int) -> int:
     parts = []
     for i in range(32):
         idx = offset + i
-        byte = dag.var(f"{tx}_calldata[{idx}]", 8)
+        name = f"{tx}_calldata[{idx}]"
+        byte = dag.var(name, 8, ir.VK_CDBYTE, *ir.cdbyte_hints(name))
         cond = dag.op(ir.B_SLT, 256, dag.const(idx, 256), size_node)
         parts.append(dag.op(ir.W_ITE, 8, cond, byte, dag.const(0, 8)))
     acc = parts[0]
@@ -225,13 +226,14 @@ def mythril_like_set(i: int, n_args: int = 2, parent: Optional[dict] = None) -> 
     sel = dag.op(ir.W_LSHR, 256, word0, dag.const(224, 256))
     dag.assert_(dag.op(ir.B_EQ, 256, sel, dag.const(selector, 256)))
     # caller in {CREATOR, ATTACKER, SOMEGUY}
-    caller = dag.var(f"sender_{tx}", 256)
+    actors = dag.force_consts((CREATOR, ATTACKER, SOMEGUY))
+    caller = dag.var(f"sender_{tx}", 256, ir.VK_ACTOR, hint0=actors, hint1=3)
     eqs = [dag.op(ir.B_EQ, 256, caller, dag.const(a, 256)) for a in (CREATOR, ATTACKER, SOMEGUY)]
     dag.assert_(dag.op(ir.B_OR, 1, dag.op(ir.B_OR, 1, eqs[0], eqs[1]), eqs[2]))
     for k in range(n_args):
         arg = calldata_word(dag, tx, 4 + 32 * k, size)
         bound = int(rng.integers(1, 1 << 16))
         dag.assert_(dag.op(ir.B_ULT, 256, arg, dag.const(bound, 256)))
-    value = dag.var(f"call_value{tx}", 256)
+    value = dag.var(f"call_value{tx}", 256, ir.VK_VALUE)
     dag.assert_(dag.op(ir.B_EQ, 256, value, dag.const(0, 256)))
     return lower(dag, seed=i, name=f"myth{i}")

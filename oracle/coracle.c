@@ -166,9 +166,31 @@ static v256 gen(const SetV* S, uint32_t v, uint32_t cand, uint64_t gseed) {
         k.w[1] = ((uint64_t)r[2] | ((uint64_t)r[3] << 32)) & ((1ull << 53) - 1);
         return andv(addv(from32(S->consts + 8 * (size_t)h0), shlv(k, 6), 0), M);
     }
-    if (kind == 3) { out = Z(); out.w[0] = (h0 == 0xffffffffu) ? r[0] : r[0] % (h0 + 1); return andv(out, M); }
+    if (kind == 3) {
+        out = Z();
+        if ((m[0] & 16u) && h0 >= 4u && h0 != 0xffffffffu) out.w[0] = 4u + 32u * (r[1] % ((h0 - 4u) / 32u + 1u));
+        else out.w[0] = (h0 == 0xffffffffu) ? r[0] : r[0] % (h0 + 1);
+        return andv(out, M);
+    }
+    if (kind == 6 && (m[0] & 16u)) return Z(); /* call value: 0 in half the candidates */
     if (kind == 4) { out = Z(); out.w[0] = r[0] & 1; return out; }
     if (kind == 1 && (m[1] % 4) < h1) return andv(from32(S->consts + 8 * (size_t)(h0 + m[1] % 4)), M);
+    uint32_t wk = (h0 >> 8) & 0xfffu, ws = h0 >> 20;
+    if (wk == 0) { wk = S->n_const; ws = 0; }
+    if (kind == 5 && wk) { /* calldata byte: one constant per (candidate, ABI word) */
+        uint32_t u = cand ^ k0 ^ (h1 * 0x9E3779B9u);
+        u ^= u >> 16; u *= 0x7feb352du; u ^= u >> 15; u *= 0x846ca68bu; u ^= u >> 16;
+        if (u & 1u) {
+            const uint32_t sh = h0 & 0xffu;
+            v256 c = from32(S->consts + 8 * (size_t)(ws + (u >> 1) % wk));
+            uint32_t d = u >> 30;
+            if (d == 1) c = addv(c, (v256){{1, 0, 0, 0}}, 0);
+            if (d == 2) c = addv(c, ONES(), 0);
+            out = Z();
+            out.w[0] = (c.w[(sh >> 6) & 3u] >> (sh & 63u)) & 0xffu;
+            return andv(out, M);
+        }
+    }
     uint32_t sel = m[0] & 15;
     if (sel <= 4) out = rv;
     else if (sel <= 8) {

@@ -250,7 +250,18 @@ def philox4x32(ctr: Sequence[np.ndarray], key: Sequence[int]):
     return [x.astype(np.uint32) for x in (c0, c1, c2, c3)]
 
 
-VK_GENERIC, VK_ACTOR, VK_KECCAK, VK_SMALL, VK_BOOL = 0, 1, 2, 3, 4
+VK_GENERIC, VK_ACTOR, VK_KECCAK, VK_SMALL, VK_BOOL, VK_CDBYTE, VK_VALUE = 0, 1, 2, 3, 4, 5, 6
+
+
+def mix32(x: int) -> int:
+    """include/pf_bytecode.h mix32 (the calldata-byte arm's per-word hash)."""
+    x &= 0xFFFFFFFF
+    x ^= x >> 16
+    x = (x * 0x7FEB352D) & 0xFFFFFFFF
+    x ^= x >> 15
+    x = (x * 0x846CA68B) & 0xFFFFFFFF
+    x ^= x >> 16
+    return x
 
 
 def uf_hash(x: int, salt: int) -> int:
@@ -297,7 +308,13 @@ def gen_values(cands: np.ndarray, var_index: int, schema: Sequence[int], consts:
             out.append((lo + (k << 6)) & M(w))
             continue
         if kind == VK_SMALL:
-            out.append((ri[0] % (hint0 + 1)) & M(w))
+            if (mi[0] & 16) and 4 <= hint0 < 0xFFFFFFFF:
+                out.append((4 + 32 * (ri[1] % ((hint0 - 4) // 32 + 1))) & M(w))
+            else:
+                out.append((ri[0] % (hint0 + 1)) & M(w))
+            continue
+        if kind == VK_VALUE and (mi[0] & 16):
+            out.append(0)
             continue
         if kind == VK_BOOL:
             out.append(ri[0] & 1)
@@ -305,6 +322,15 @@ def gen_values(cands: np.ndarray, var_index: int, schema: Sequence[int], consts:
         if kind == VK_ACTOR and (mi[1] % 4) < hint1:
             out.append(consts[hint0 + mi[1] % 4] & M(w))
             continue
+        wk, ws = (hint0 >> 8) & 0xFFF, hint0 >> 20
+        if wk == 0:
+            wk, ws = len(consts), 0
+        if kind == VK_CDBYTE and wk:
+            u = mix32(c ^ key[0] ^ (hint1 * 0x9E3779B9))
+            if u & 1:
+                word = (consts[ws + (u >> 1) % wk] + (0, 1, -1, 0)[u >> 30]) & M(256)
+                out.append((word >> (hint0 & 0xFF)) & 0xFF & M(w))
+                continue
         sel = mi[0] & 15
         if sel <= 4:
             v = rv

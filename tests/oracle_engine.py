@@ -47,6 +47,9 @@ class OracleEngine:
                 found[s] = f
         return CheckResult(found, budget * len(db), budget * len(db), 0, 0.0)
 
+    def keccak256(self, messages):
+        return [O.keccak256(bytes(m)) for m in messages]
+
     def materialize(self, db, set_ids, cand_ids, seed=0):
         out = []
         for s, c in zip(set_ids, cand_ids):

@@ -33,12 +33,20 @@ def test_corpus_discharge_and_models(engine):
             assert bool(m.eval(t)), q.origin
 
 
-def test_bucket_cache_answers_repeated_queries(engine):
+def test_bucket_cache_answers_repeated_queries(engine, monkeypatch):
+    """A repeated batch is answered from the bucket caches: never a lost witness, and with
+    parent models off (a deterministic search) exactly the same answers.  With parents on, a
+    re-posed query may gain a witness — its new buckets start from the first pass's."""
     c = corpus.build(4, 2, seed=9)
-    gpu_check.reset_cache()
     sets = [q.constraints for q in c.queries]
-    first = get_models(sets, registry=c.kfm.registry)
-    hits0 = gpu_check.STATS.bucket_hits
-    again = get_models(sets, registry=c.kfm.registry)
-    assert gpu_check.STATS.bucket_hits > hits0
-    assert [m is None for m in first] == [m is None for m in again]
+    for parents in (False, True):
+        monkeypatch.setattr(gpu_check.CONFIG, "parents", parents)
+        gpu_check.reset_cache()
+        first = get_models(sets, registry=c.kfm.registry)
+        hits0 = gpu_check.STATS.bucket_hits
+        again = get_models(sets, registry=c.kfm.registry)
+        assert gpu_check.STATS.bucket_hits > hits0
+        assert all(a is not None for a, f in zip(again, first) if f is not None)
+        if not parents:
+            assert [m is None for m in first] == [m is None for m in again]
+    assert gpu_check.STATS.recheck_failures == 0

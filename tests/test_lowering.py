@@ -187,3 +187,33 @@ def test_word_slicing_rewrites_preserve_values(monkeypatch):
         vs = eval_dag_values(simp, values(simp, raw))
         for a, b in zip(e_plain, e_simp):
             assert vp[a] == vs[b], (trial, a, b)
+
+
+def test_witness_reads_nested_calldata_offsets_like_the_program():
+    """An ABI dynamic argument: a calldata read at an offset itself read from calldata
+    (state/calldata.py:233-246 words, BECToken's batchTransfer).  The host Witness must
+    interpret the nested reads exactly as the lowered program does (first earlier read with
+    an equal index, in lookup order) — a table built before the nested reads were resolved
+    rejected GPU witnesses in the host re-check."""
+    from mythril_amd.smt import terms as T
+    from mythril_amd.smt.interp import Witness
+    from mythril_amd.smt.to_dag import TermLowering, UFRegistry
+
+    cd = T.array("1_calldata", 256, 8)
+    off = T.concat(*[T.select(cd, T.const(i, 256)) for i in range(4, 8)])   # offset word (32 bits)
+    base = T.binop("bvadd", T.zero_extend(224, off), T.const(4, 256))
+    n = T.concat(*[T.select(cd, T.binop("bvadd", base, T.const(j, 256))) for j in range(2)])
+    cs = [T.cmp("bvult", T.const(0, 16), n), T.cmp("bvult", off, T.const(16, 32))]
+    lo = TermLowering(UFRegistry()).lower(cs)
+    prog = lower(lo.dag)
+    sv = O.SetView.from_batch(ir.Batch([prog]), 0)
+    rng = random.Random(3)
+    agree = sat = 0
+    for _ in range(400):
+        vals = [rng.choice((0, 1, 4, 5, 8, 9, rng.getrandbits(8))) & ir.mask(v.width) for v in lo.dag.vars]
+        want = sv.evaluate(vals)
+        w = Witness(lo, vals, UFRegistry())
+        got = all(bool(w.ev(c)) for c in cs)
+        agree += got == want
+        sat += want
+    assert agree == 400 and sat > 0

@@ -1,0 +1,264 @@
+"""The native term lowering (csrc/pf_terms.cpp, include/pf_lower.h "term store") against the
+Python reference (smt/to_dag.py TermLowering + lower.py Dag + seed.apply_hints +
+lower.lower): identical node tables, roots, forced constants, variables (names, kinds, schema
+hints, parents), witness metadata (var_terms, uf_apps, array_reads) and programs — on the
+LASER-shaped corpus (calldata words, actor sets, storage store chains, keccak mapping slots
+with the manager's conditions), wide values (z3's 257-bit no-overflow forms, 512-bit keccak
+inputs), Power, UFs, arrays over ite, and parent models.  The same LoweringErrors too.
+"""
+
+import random
+
+import numpy as np
+import pytest
+
+import oracle_engine
+import pyoracle as O
+
+from mythril_amd import corpus, ir, seed
+from mythril_amd.lower import LoweringError, lower, pack_nodes
+from mythril_amd.smt import gpu_check
+from mythril_amd.smt import native_terms as NT
+from mythril_amd.smt import terms as T
+from mythril_amd.smt.independence import buckets
+from mythril_amd.smt.to_dag import ACTORS, KeccakSpec, TermLowering, UFRegistry
+
+pytestmark = pytest.mark.skipif(NT.store() is None, reason="libpflower.so not built")
+
+
+def _compare_dag(b, reg, parent=None):
+    """Python and native DAGs of one bucket: equal, or the same LoweringError."""
+    try:
+        lo = TermLowering(reg, parent).lower(b)
+        perr = None
+    except LoweringError as e:
+        lo, perr = None, str(e)
+    try:
+        r = NT.lower_native(b, reg, parent, 0)
+        nerr = None
+    except LoweringError as e:
+        r, nerr = None, str(e)
+    assert (perr is None) == (nerr is None), (perr, nerr)
+    if perr is not None:
+        return None
+    nodes, pool_a, _ = pack_nodes(lo.dag)
+    nn = r.info[8]
+    assert nn == len(lo.dag.nodes)
+    assert np.array_equal(r.get(NT.GET_NODES, nn, 8).reshape(-1), nodes.reshape(-1)[:8 * nn])
+    npool = r.get(NT.GET_POOL, r.info[9], 8)
+    assert np.array_equal(npool.reshape(-1), pool_a.reshape(-1)[:npool.size])
+    assert list(r.get(NT.GET_ROOTS, r.info[10], 1)) == lo.dag.roots
+    forced = [NT._int_of(x) for x in r.get(NT.GET_FORCED, r.info[11], 8).tolist()]
+    assert forced == lo.dag.forced
+    vs = r.variables()
+    assert [(v.name, v.width, v.kind, v.hint0, v.hint1) for v in vs] == \
+        [(v.name, v.width, v.kind, v.hint0, v.hint1) for v in lo.dag.vars]
+    assert [v.parent for v in vs] == [None if v.parent is None else v.parent & ir.mask(v.width)
+                                      for v in lo.dag.vars]
+    L = r.lowered()
+    assert L.var_terms == lo.var_terms
+    assert [(a, tuple(b_), c) for a, b_, c in L.uf_apps] == [(a, tuple(b_), c) for a, b_, c in lo.uf_apps]
+    assert L.array_reads == lo.array_reads
+    return lo
+
+
+def _compare_program(b, reg, parent=None, hints=True, seed_=7):
+    try:
+        lo = TermLowering(reg, parent).lower(b)
+        if hints:
+            seed.apply_hints(lo.dag)
+        prog = lower(lo.dag, seed=seed_)
+        perr = None
+    except LoweringError as e:
+        perr = str(e)
+    try:
+        _, prog2 = NT.lower_bucket(b, reg, parent, hints, seed_)
+        nerr = None
+    except LoweringError as e:
+        nerr = str(e)
+    assert (perr is None) == (nerr is None), (perr, nerr)
+    if perr is not None:
+        return
+    b1, b2 = ir.Batch([prog]), ir.Batch([prog2])
+    for name in ("code", "consts", "schema", "parents", "descs"):
+        assert np.array_equal(getattr(b1, name), getattr(b2, name)), name
+
+
+@pytest.fixture(scope="module")
+def corpus_buckets():
+    import mythril_amd.engine as E
+
+    eng = oracle_engine.OracleEngine()
+    saved = E.get_engine
+    E.get_engine = lambda device=None: eng   # the corpus hashes concrete keccaks (host oracle)
+    try:
+        c = corpus.build(10, 2, seed=11)
+    finally:
+        E.get_engine = saved
+    out, seen = [], set()
+    for q in c.queries:
+        for b in buckets(q.constraints):
+            if tuple(b) not in seen:
+                seen.add(tuple(b))
+                out.append(b)
+    return c.kfm.registry, out
+
+
+def test_corpus_dags_match(corpus_buckets):
+    reg, bks = corpus_buckets
+    lowered = sum(_compare_dag(b, reg) is not None for b in bks)
+    assert lowered > 0.9 * len(bks)
+
+
+def test_corpus_programs_match(corpus_buckets):
+    reg, bks = corpus_buckets
+    for b in bks:
+        _compare_program(b, reg, hints=True)
+    for b in bks[:40]:
+        _compare_program(b, reg, hints=False)
+
+
+def test_parent_models_match(corpus_buckets):
+    """Parents by symbol name and by array read (gpu_check._recent_parent's two key kinds)."""
+    reg, bks = corpus_buckets
+    rng = random.Random(4)
+    for b in bks[:60]:
+        lo = TermLowering(reg).lower(b)
+        parent = {}
+        for t in lo.var_terms:
+            if t.op in ("var", "bvar") and rng.random() < 0.7:
+                parent[t.val] = rng.getrandbits(300)
+            elif t.op == "select" and rng.random() < 0.7:
+                parent[t] = rng.getrandbits(256)
+        _compare_dag(b, reg, parent)
+        _compare_program(b, reg, parent, hints=False)
+        _compare_program(b, reg, parent, hints=True)
+
+
+def _wide_cases():
+    x, y = T.var("x", 256), T.var("y", 256)
+    X, Y = T.var("X", 512), T.var("Y", 512)
+    zx, zy = T.zero_extend(1, x), T.zero_extend(1, y)
+    s257 = T.binop("bvadd", zx, zy)
+    carry = T.extract(256, 256, s257)
+    return [
+        T.eq(carry, T.const(0, 1)),
+        T.eq(T.extract(256, 256, T.binop("bvadd", T.concat(T.const(0, 1), x), T.concat(T.const(0, 1), y))),
+             T.const(0, 1)),
+        T.eq(T.extract(256, 256, T.binop("bvsub", zx, zy)), T.const(1, 1)),
+        T.eq(T.extract(256, 1, T.bvneg(zx)), T.extract(256, 1, T.binop("bvsub", T.const(0, 257), zx))),
+        T.cmp("bvult", X, Y), T.cmp("bvule", X, Y), T.cmp("bvslt", X, Y),
+        T.cmp("bvsle", T.extract(299, 0, X), T.extract(299, 0, Y)),
+        T.eq(T.concat(T.const(0, 256), x), X),
+        T.eq(T.binop("bvxor", T.binop("bvand", X, Y), T.binop("bvor", X, Y)), T.binop("bvxor", X, Y)),
+        T.eq(T.bvnot(X), T.binop("bvsub", T.const(-1, 512), X)),
+        T.eq(T.extract(300, 100, X), T.extract(300, 100, Y)),
+        T.eq(T.binop("bvshl", X, T.const(100, 512)), T.binop("bvshl", Y, T.const(100, 512))),
+        T.cmp("bvult", T.binop("bvlshr", X, T.const(300, 512)), T.extract(511, 0, Y)),
+        T.eq(T.ite(T.cmp("bvult", x, y), X, Y), X),
+        T.cmp("bvult", T.binop("bvmul", X, Y), X),          # unsupported wide op: same error
+    ]
+
+
+def test_wide_values_match():
+    reg = UFRegistry()
+    for c in _wide_cases():
+        _compare_dag([c], reg)
+        _compare_program([c], reg)
+    _compare_dag(_wide_cases()[:6], reg, {"X": (1 << 511) | 5, "x": 7})
+
+
+def test_keccak_power_and_ufs_match():
+    """keccak256_<n> with intervals and concrete hashes, inverses (as application and as
+    lookup), 512-bit inputs, Power facts and symbolic applications, other UFs, arrays over
+    store / ite / K."""
+    reg = UFRegistry()
+    reg.keccak[512] = KeccakSpec(lo=3 * ((2 ** 256 - 1) // 10 ** 40))
+    reg.keccak[512].concrete[(5 << 256) | 1] = 0xABCDEF
+    reg.keccak[256] = KeccakSpec(lo=None, concrete={9: 0x1234})
+    a, b = T.var("a", 256), T.var("b", 256)
+    key = T.concat(a, T.const(1, 256))
+    f = T.apply("keccak256_512", 256, key)
+    f2 = T.apply("keccak256_512", 256, T.concat(b, T.const(1, 256)))
+    inv = T.apply("keccak256_512-1", 512, f)
+    y = T.var("y", 256)
+    inv_free = T.apply("keccak256_256-1", 256, y)
+    g = T.apply("keccak256_256", 256, b)
+    p1 = T.apply("Power", 256, T.const(256, 256), a)
+    p2 = T.apply("Power", 256, b, a)
+    p3 = T.apply("Power", 256, T.const(3, 256), T.const(5, 256))
+    u = T.apply("myuf", 160, a, T.extract(63, 0, b))
+    arr = T.array("Storage", 256, 256)
+    st = T.store(T.store(T.const_array(256, T.const(0, 256)), a, b), T.const(7, 256), y)
+    ite_arr = T.ite(T.cmp("bvult", a, b), st, arr)
+    cases = [
+        [T.eq(inv, key), T.cmp("bvult", f, f2)],
+        [T.eq(T.apply("keccak256_256-1", 256, g), b), T.eq(inv_free, a), T.eq(g, y)],
+        [T.cmp("bvslt", T.const(0, 256), p1), T.eq(p1, T.const(1 << 16, 256)), T.eq(p3, T.const(243, 256)),
+         T.cmp("bvult", T.const(0, 256), p2), T.eq(p2, T.apply("Power", 256, b, a))],
+        [T.eq(u, T.extract(159, 0, y)), T.cmp("bvult", T.select(ite_arr, y), T.select(arr, a))],
+        [T.eq(T.select(st, T.const(7, 256)), T.select(arr, T.binop("bvadd", a, T.const(4, 256))))],
+    ]
+    for cs in cases:
+        _compare_dag(cs, reg)
+        _compare_program(cs, reg)
+        _compare_program(cs, reg, hints=False)
+
+
+def test_unsupported_ops_raise_the_same():
+    x = T.var("x", 256)
+    weird = T.Term("bvrotl_odd", ("bv", 256), (x,))
+    with pytest.raises(LoweringError):
+        NT.lower_native([T.eq(weird, x)], UFRegistry(), None, 0)
+    with pytest.raises(LoweringError):
+        TermLowering(UFRegistry()).lower([T.eq(weird, x)])
+
+
+def test_calldata_byte_hints_and_actor_table(corpus_buckets):
+    """The LASER kinds (actor table, ABI sizes, calldata-word bytes, call values) and the
+    word constants are pinned identically (finalize_word_hints)."""
+    reg, bks = corpus_buckets
+    kinds = set()
+    for b in bks[:80]:
+        try:
+            _, prog = NT.lower_bucket(b, reg, None, False, 1)
+        except LoweringError:
+            continue
+        kinds |= {v.kind for v in prog.vars}
+    assert {ir.VK_ACTOR, ir.VK_SMALL, ir.VK_CDBYTE, ir.VK_VALUE} <= kinds
+    assert tuple(reg.actors) == ACTORS
+
+
+def test_gpu_check_uses_the_native_path(monkeypatch):
+    """check_sets lowers through the term store (and answers as the Python path does)."""
+    eng = oracle_engine.install(monkeypatch)
+    x = T.var("call_value1", 256)
+    cs = [T.cmp("bvult", x, T.const(100, 256)), T.cmp("bvult", T.const(5, 256), x)]
+    n0 = NT.store().L.pflt_store_size(NT.store().h)
+    m = gpu_check.check_sets([cs])[0]
+    assert m is not None and 5 < m.w.vars["call_value1"] < 100
+    assert NT.store().L.pflt_store_size(NT.store().h) > n0 or x in NT.store().ids
+    assert eng.launches == 1
+    monkeypatch.setattr(gpu_check, "_NATIVE_TERMS", False)
+    gpu_check.reset_cache()
+    m2 = gpu_check.check_sets([cs])[0]
+    assert m2.w.vars["call_value1"] == m.w.vars["call_value1"]
+
+
+def test_native_witness_evaluates_like_the_program(corpus_buckets):
+    """Witness metadata from the native path drives the host evaluator (smt/interp.py)
+    exactly as the program computes, on random assignments."""
+    from mythril_amd.smt.interp import Witness
+
+    reg, bks = corpus_buckets
+    rng = random.Random(9)
+    for b in bks[:40]:
+        try:
+            lo, prog = NT.lower_bucket(b, reg, None, False, 3)
+        except LoweringError:
+            continue
+        sv = O.SetView.from_batch(ir.Batch([prog]), 0)
+        for _ in range(8):
+            vals = [rng.choice((0, 1, 4, 36, 68, rng.getrandbits(v.width))) & ir.mask(v.width) for v in prog.vars]
+            w = Witness(lo, vals, reg)
+            assert sv.evaluate(vals) == all(bool(w.ev(c)) for c in b)

@@ -24,21 +24,6 @@ from mythril_amd.smt import terms as T  # noqa: E402
 from mythril_amd.smt.independence import buckets  # noqa: E402
 
 
-def live_groups(qs):
-    """Fork pairs (same origin minus the :T/:F side) and boundary queries, in issue order."""
-    out, cur, key = [], [], None
-    for q in qs:
-        k = q.origin.rsplit(":", 1)[0] if q.origin.endswith((":T", ":F")) else q.origin
-        if k != key and cur:
-            out.append(cur)
-            cur = []
-        key = k
-        cur.append(q)
-    if cur:
-        out.append(cur)
-    return out
-
-
 def main():
     n_sc = int(sys.argv[1]) if len(sys.argv) > 1 else 24
     budget = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
@@ -57,7 +42,7 @@ def main():
     gpu_check.reset_cache()
     live = [None] * len(qs)
     idx = {id(q): i for i, q in enumerate(qs)}
-    for g in live_groups(qs):
+    for g in corpus.live_order_groups(qs):
         r = gpu_check.check_sets([q.constraints for q in g], registry=reg, config=cfg)
         for q, m in zip(g, r):
             live[idx[id(q)]] = m
