@@ -177,45 +177,64 @@ struct DVar {
     C8 parent;
 };
 
+struct NodeKey {  // the hash-consing key of a node (lower.py Node tuple)
+    uint32_t kind, width, nargs, aux;
+    int32_t args[3];
+    uint32_t is_bool;
+    C8 cv;
+    bool operator==(const NodeKey& o) const { return memcmp(this, &o, sizeof(NodeKey)) == 0; }
+};
+
+struct NodeKeyHash {
+    size_t operator()(const NodeKey& k) const {
+        const uint32_t* w = (const uint32_t*)&k;
+        uint64_t h = 0x9E3779B97F4A7C15ull;
+        for (size_t i = 0; i < sizeof(NodeKey) / 4; i++) h = (h ^ w[i]) * 0x100000001B3ull;
+        return (size_t)(h ^ (h >> 29));
+    }
+};
+
 struct Dag {
     std::vector<DNode> nodes;
     std::vector<int32_t> roots;
     std::vector<DVar> vars;
     std::vector<C8> forced;
-    std::unordered_map<std::string, int32_t> memo;
+    std::unordered_map<NodeKey, int32_t, NodeKeyHash> memo;
     std::unordered_map<std::string, int32_t> var_index;
 
-    static std::string key_of(const DNode& n) {
-        std::string k;
-        k.append((const char*)&n.kind, 4);
-        k.append((const char*)&n.width, 4);
-        k.append((const char*)&n.nargs, 4);
-        k.append((const char*)n.args, 4 * n.nargs);
-        k.append((const char*)&n.aux, 4);
-        if (n.kind == K_CONST) k.append((const char*)n.cv.l, 32);
-        k.push_back(n.is_bool ? 1 : 0);
-        return k;
-    }
+    Dag() { memo.reserve(4096); }
 
-    int32_t add(uint32_t kind, uint32_t width, std::initializer_list<int32_t> args, uint32_t aux,
-                bool is_bool, const C8* cv = nullptr) {
+    int32_t add_n(uint32_t kind, uint32_t width, const int32_t* args, uint32_t nargs, uint32_t aux,
+                  bool is_bool, const C8* cv = nullptr) {
+        NodeKey k;
+        memset(&k, 0, sizeof(k));
+        k.kind = kind;
+        k.width = width;
+        k.nargs = nargs;
+        for (uint32_t i = 0; i < nargs; i++) k.args[i] = args[i];
+        k.aux = aux;
+        k.is_bool = is_bool ? 1u : 0u;
+        if (cv && kind == K_CONST) k.cv = *cv;
+        auto it = memo.find(k);
+        if (it != memo.end()) return it->second;
         DNode n;
         memset(&n, 0, sizeof(n));
         n.kind = kind;
         n.width = width;
-        n.nargs = (uint32_t)args.size();
-        int i = 0;
-        for (int32_t a : args) n.args[i++] = a;
+        n.nargs = nargs;
+        for (uint32_t i = 0; i < nargs; i++) n.args[i] = args[i];
         n.aux = aux;
         if (cv) n.cv = *cv;
         n.is_bool = is_bool;
-        const std::string k = key_of(n);
-        auto it = memo.find(k);
-        if (it != memo.end()) return it->second;
         const int32_t id = (int32_t)nodes.size();
         nodes.push_back(n);
         memo.emplace(k, id);
         return id;
+    }
+
+    int32_t add(uint32_t kind, uint32_t width, std::initializer_list<int32_t> args, uint32_t aux,
+                bool is_bool, const C8* cv = nullptr) {
+        return add_n(kind, width, args.begin(), (uint32_t)args.size(), aux, is_bool, cv);
     }
 
     uint32_t force_consts(const std::vector<C8>& vals) {
@@ -252,20 +271,13 @@ struct Dag {
     const C8* cval(int32_t i) const { return nodes[i].kind == K_CONST ? &nodes[i].cv : nullptr; }
 
     int32_t op(uint32_t opc, uint32_t w, std::initializer_list<int32_t> args, uint32_t aux = 0) {
-        std::vector<int32_t> a(args);
-        const int32_t r = simplify(opc, w, a, aux);
+        const int32_t r = simplify(opc, w, args.begin(), aux);
         if (r >= 0) return r;
-        const bool is_bool = opc >= PF_B_CONST;
-        switch (a.size()) {
-            case 1: return add(opc, w, {a[0]}, aux, is_bool);
-            case 2: return add(opc, w, {a[0], a[1]}, aux, is_bool);
-            case 3: return add(opc, w, {a[0], a[1], a[2]}, aux, is_bool);
-            default: return add(opc, w, {}, aux, is_bool);
-        }
+        return add_n(opc, w, args.begin(), (uint32_t)args.size(), aux, opc >= PF_B_CONST);
     }
 
     // Dag._simplify: the word-slicing rewrites (lower.py)
-    int32_t simplify(uint32_t opc, uint32_t w, const std::vector<int32_t>& args, uint32_t aux) {
+    int32_t simplify(uint32_t opc, uint32_t w, const int32_t* args, uint32_t aux) {
         if (opc == PF_W_UDIV) {
             const C8* c = cval(args[1]);
             if (c) {

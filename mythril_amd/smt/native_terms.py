@@ -56,6 +56,8 @@ def _limbs8(v: int) -> List[int]:
 
 
 def _int_of(row) -> int:
+    if isinstance(row, np.ndarray):
+        return int.from_bytes(row.astype("<u4").tobytes(), "little")
     return sum(int(x) << (32 * i) for i, x in enumerate(row))
 
 
@@ -208,11 +210,14 @@ class _Result:
         names = ctypes.create_string_buffer(max(nb, 1))
         self.st.L.pflt_result_get(self.h, GET_VARS, out.ctypes.data_as(_u32p), names)
         labels = names.raw[:nb].split(b"\0")[:nv]
+        rows = out[:13 * nv].reshape(nv, 13)
+        pbytes = np.ascontiguousarray(rows[:, 5:13]).astype("<u4").tobytes()
+        head = rows[:, :5].tolist()
         vs = []
         for i in range(nv):
-            row = out[13 * i:13 * i + 13]
-            parent = _int_of(row[5:13]) if row[4] else None
-            vs.append(ir.Var(labels[i].decode(), int(row[0]), int(row[1]), int(row[2]), int(row[3]), parent))
+            w_, k_, h0, h1, hp = head[i]
+            parent = int.from_bytes(pbytes[32 * i:32 * i + 32], "little") if hp else None
+            vs.append(ir.Var(labels[i].decode(), w_, k_, h0, h1, parent))
         return vs
 
     def lowered(self) -> Lowered:
@@ -244,8 +249,9 @@ class _Result:
 
     def program(self, seed: int) -> ir.PackedProgram:
         code = self.get(GET_CODE, self.info[6], 4)
-        cv = self.get(GET_CONSTS, self.info[7], 8)
-        consts = [_int_of(r) for r in cv.tolist()]
+        nc = self.info[7]
+        raw = self.get(GET_CONSTS, nc, 8).astype("<u4").tobytes()
+        consts = [int.from_bytes(raw[32 * i:32 * i + 32], "little") for i in range(nc)]
         return ir.PackedProgram(code.copy(), consts, self.variables(), seed, "")
 
 
