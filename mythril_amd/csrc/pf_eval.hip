@@ -152,6 +152,13 @@ namespace {
 // write-back, where lgkmcnt(0) also waits for the next instruction's scalar fetch issued at
 // the top of this one — every bytecode instruction then paid the fetch latency.
 #define PF_WAIT_ALL() __builtin_amdgcn_s_waitcnt(0)
+// vector-memory loads only (vmcnt(0) expcnt(7) lgkmcnt(15)): the generator's loads are
+// vector gathers, and lgkmcnt would also wait for the next instruction's scalar fetch
+#ifdef PF_GEN_WAIT_VM
+#define PF_WAIT_GEN() __builtin_amdgcn_s_waitcnt(0x0F70)
+#else
+#define PF_WAIT_GEN() PF_WAIT_ALL()
+#endif
 
 // per-limb mask for width w.  w is wave-uniform (it comes from the scalar-loaded
 // instruction); the mask is formed from the top limb index and its partial mask with
@@ -693,7 +700,7 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
                     for (int i = 0; i < 8; i++)
                         z.l[i] = active ? soa[((size_t)aux * 8u + i) * soa_n + cand] : 0u;
                 }
-                PF_WAIT_ALL();
+                PF_WAIT_GEN();
                 if (op == PF_B_VAR) {
                     BSET(d, z.l[0]);
                     PF_NEXT();

@@ -167,7 +167,23 @@ def store() -> Optional[TermStore]:
     return _STORE
 
 
+_BLOBS: Dict[tuple, np.ndarray] = {}
+
+
 def _registry_blob(reg: UFRegistry) -> np.ndarray:
+    """The registry in pflt_lower's layout, cached per registry state (hashes only get added:
+    the per-width counts and interval starts identify the state)."""
+    key = (id(reg), tuple(reg.actors),
+           tuple((n, s.lo, len(s.concrete)) for n, s in reg.keccak.items()))
+    blob = _BLOBS.get(key)
+    if blob is None:
+        if len(_BLOBS) > 64:
+            _BLOBS.clear()
+        blob = _BLOBS[key] = _registry_blob_build(reg)
+    return blob
+
+
+def _registry_blob_build(reg: UFRegistry) -> np.ndarray:
     blob: List[int] = [len(reg.actors)]
     for a in reg.actors:
         blob += _limbs8(a)

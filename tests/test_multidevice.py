@@ -119,3 +119,60 @@ def test_gpu_mask_engine_and_check_many(engine):
     assert r2.cands_decided > 0
     for db in (whole, a, b):
         db.free()
+
+
+def test_plugin_batch_spreads_over_all_visible_devices(monkeypatch):
+    """The live analysis is one process: once the plugin is loaded (install() defaults
+    PF_DEVICES to "all"), the engine it gets drives every visible device, and a
+    tx-boundary batch (stop_sym_trans hook, svm.py:306-307) is split into one shard per
+    device — 3 stand-in devices here."""
+    import fake_z3 as z3
+    import mythril_standin
+    from mythril_amd import _lib, integration
+
+    ns = mythril_standin.install(monkeypatch, z3)
+    made = {}
+
+    def fake_engine(device=0, devices=None):
+        made["devices"] = devices
+        eng = _MultiOracle(len(devices))
+        made["eng"] = eng
+        return eng
+
+    class _L:
+        def pf_device_count(self):
+            return 3
+
+    monkeypatch.setattr(_lib, "lib", lambda: _L())
+    monkeypatch.setattr(E, "Engine", fake_engine)
+    monkeypatch.setattr(E, "_engine", None)
+    monkeypatch.setattr(gpu_check.CONFIG, "workers", 1)
+    monkeypatch.setattr(gpu_check.CONFIG, "budget", 1024)
+    monkeypatch.setattr(integration, "sync_keccak_registry", lambda kfm, registry=None: None)
+    gpu_check.reset_cache()
+    B = ns.Bool
+    states = []
+    for k in range(12):
+        x = z3.BitVec(f"call_value{k}", 256)
+        states.append(ns.WorldState([B(z3.ULT(x, z3.BitVecVal(100 + k, 256))),
+                                     B(z3.ULT(z3.BitVecVal(k, 256), x))]))
+
+    class SVM:
+        def __init__(self):
+            self.hooks = {}
+            self.open_states = states
+
+        def laser_hook(self, name):
+            def deco(fn):
+                self.hooks.setdefault(name, []).append(fn)
+                return fn
+            return deco
+
+    svm = SVM()
+    integration._plugin_classes()[1](**{})().initialize(svm)
+    svm.hooks["stop_sym_trans"][0]()
+    assert made["devices"] == [0, 1, 2]
+    assert sorted({d for d, _ in made["eng"].uploads}) == [0, 1, 2]
+    assert all(s.constraints.is_possible() for s in states)
+    monkeypatch.setattr(E, "_engine", None)
+    gpu_check.reset_cache()
