@@ -148,6 +148,28 @@ void pflt_result_free(void* result);
 void pflt_result_info(void* result, uint64_t* info);  /* 14 sizes, see pf_terms.cpp */
 void pflt_result_get(void* result, uint32_t which, uint32_t* out, char* names_out);
 
+/* A stored term, read-only (pointers valid until the next pflt_add). */
+typedef struct pflt_term_view {
+    uint32_t op, sortk, w1, w2, nargs;
+    const uint32_t* args;
+    int64_t i0, i1;
+    const uint32_t* limbs;
+    uint32_t nlimbs;
+    const char* name;
+} pflt_term_view;
+int pflt_view(void* store, uint32_t id, pflt_term_view* out);
+
+/* Host re-check of a bucket witness (csrc/pf_recheck.cpp; mythril_amd/smt/interp.py
+ * Witness.ev, bit for bit): var_desc = n_vars x 4 u32 (the result's var_terms descriptors:
+ * type, a, b, c) with values n_vars x 8 u32; uf_apps = application term ids in registration
+ * order; reads = (array id, index id) pairs, grouped per array in lookup order; registry as
+ * for pflt_lower.  out[i] = value of roots[i] (0/1).  Returns 0, or -1 when a term is not
+ * evaluable here (the caller re-checks in Python). */
+int pflt_recheck(void* store, const uint32_t* var_desc, size_t n_vars, const uint32_t* values,
+                 const uint32_t* uf_apps, size_t n_uf, const uint32_t* reads, size_t n_reads,
+                 const uint32_t* registry, size_t n_registry, const uint32_t* roots, size_t n_roots,
+                 uint8_t* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -30,7 +30,7 @@ def _stale() -> bool:
 
 
 LOWER_OUT = os.path.join(HERE, "libpflower.so")
-LOWER_SOURCES = ["pf_lower.cpp", "pf_seed.cpp", "pf_terms.cpp", os.path.join("..", "..", "include", "pf_lower.h"),
+LOWER_SOURCES = ["pf_lower.cpp", "pf_seed.cpp", "pf_terms.cpp", "pf_recheck.cpp", os.path.join("..", "..", "include", "pf_lower.h"),
                  os.path.join("..", "..", "include", "pf_bytecode.h")]
 
 
@@ -41,7 +41,7 @@ def build_lower(force: bool = False, verbose: bool = False) -> str:
         return LOWER_OUT
     cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-o", LOWER_OUT + ".tmp",
            os.path.join(CSRC, "pf_lower.cpp"), os.path.join(CSRC, "pf_seed.cpp"),
-           os.path.join(CSRC, "pf_terms.cpp")]
+           os.path.join(CSRC, "pf_terms.cpp"), os.path.join(CSRC, "pf_recheck.cpp")]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True, cwd=CSRC)

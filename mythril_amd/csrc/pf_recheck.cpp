@@ -1,0 +1,584 @@
+// pf_recheck.cpp — libpflower.so: the host re-check of a GPU witness, natively
+// (include/pf_lower.h, pflt_recheck).
+//
+// The native form of mythril_amd/smt/interp.py:Witness.ev — the same interpretation of
+// every term the lowering accepts, bit for bit: SMT-LIB2 bit-vector semantics at any width
+// (z3's total division), arrays read in the lowering's lookup order (the first read of the
+// array whose index evaluates equal), keccak256_<n> as the registered concrete hash or
+// base_n + 64 (H(x) mod 2^117), inverses by lookup among the set's applications, Power by
+// argument value, other UFs as keyed hashes (PF_W_HASH).  gpu_check runs it on every bucket
+// witness before trusting it (soundness: a GPU "sat" must satisfy the terms, not only the
+// program); tests/test_native_terms.py checks it against Witness.ev.  Host code, no HIP.
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/pf_lower.h"
+
+namespace {
+
+// ---- values of any width: little-endian u32 limbs, exactly ceil(w / 32) of them ----------
+typedef std::vector<uint32_t> V;
+
+size_t nl_of(uint32_t w) { return (w + 31) / 32; }
+
+V vzero(uint32_t w) { return V(nl_of(w), 0u); }
+
+V vmask(const V& a, uint32_t w) {
+    V r(nl_of(w), 0u);
+    for (size_t i = 0; i < r.size() && i < a.size(); i++) r[i] = a[i];
+    if (w % 32 && !r.empty()) r.back() &= (1u << (w % 32)) - 1u;
+    return r;
+}
+
+bool vbit(const V& a, uint32_t i) { return i / 32 < a.size() && ((a[i / 32] >> (i % 32)) & 1u); }
+
+bool vis_zero(const V& a) {
+    for (uint32_t x : a)
+        if (x) return false;
+    return true;
+}
+
+int vcmp(const V& a, const V& b) {  // unsigned
+    const size_t n = std::max(a.size(), b.size());
+    for (size_t i = n; i-- > 0;) {
+        const uint32_t x = i < a.size() ? a[i] : 0u, y = i < b.size() ? b[i] : 0u;
+        if (x != y) return x < y ? -1 : 1;
+    }
+    return 0;
+}
+
+V vadd(const V& a, const V& b, uint32_t w) {
+    V r(nl_of(w), 0u);
+    uint64_t c = 0;
+    for (size_t i = 0; i < r.size(); i++) {
+        c += (uint64_t)(i < a.size() ? a[i] : 0u) + (i < b.size() ? b[i] : 0u);
+        r[i] = (uint32_t)c;
+        c >>= 32;
+    }
+    return vmask(r, w);
+}
+
+V vnot(const V& a, uint32_t w) {
+    V r(nl_of(w), 0u);
+    for (size_t i = 0; i < r.size(); i++) r[i] = ~(i < a.size() ? a[i] : 0u);
+    return vmask(r, w);
+}
+
+V vneg(const V& a, uint32_t w) {
+    V one = vzero(w);
+    if (!one.empty()) one[0] = 1;
+    return vadd(vnot(a, w), one, w);
+}
+
+V vsub(const V& a, const V& b, uint32_t w) { return vadd(a, vneg(b, w), w); }
+
+V vmul(const V& a, const V& b, uint32_t w) {
+    const size_t n = nl_of(w);
+    V r(n, 0u);
+    for (size_t i = 0; i < n && i < a.size(); i++) {
+        uint64_t c = 0;
+        for (size_t j = 0; i + j < n; j++) {
+            c += (uint64_t)a[i] * (j < b.size() ? b[j] : 0u) + r[i + j];
+            r[i + j] = (uint32_t)c;
+            c >>= 32;
+        }
+    }
+    return vmask(r, w);
+}
+
+V vshl(const V& a, uint64_t s, uint32_t w) {
+    V r = vzero(w);
+    if (s >= w) return r;
+    const size_t q = (size_t)(s / 32), b = (size_t)(s % 32);
+    for (size_t i = r.size(); i-- > q;) {
+        const size_t j = i - q;
+        uint32_t x = j < a.size() ? a[j] << b : 0u;
+        if (b && j >= 1 && j - 1 < a.size()) x |= a[j - 1] >> (32 - b);
+        r[i] = x;
+    }
+    return vmask(r, w);
+}
+
+V vlshr(const V& a, uint64_t s, uint32_t w) {
+    V r = vzero(w);
+    if (s >= w) return r;
+    const V m = vmask(a, w);
+    const size_t q = (size_t)(s / 32), b = (size_t)(s % 32);
+    for (size_t i = 0; i + q < m.size(); i++) {
+        uint32_t x = m[i + q] >> b;
+        if (b && i + q + 1 < m.size()) x |= m[i + q + 1] << (32 - b);
+        r[i] = x;
+    }
+    return r;
+}
+
+bool vneg_sign(const V& a, uint32_t w) { return w && vbit(a, w - 1); }
+
+V vashr(const V& a, uint64_t s, uint32_t w) {
+    const bool neg = vneg_sign(a, w);
+    if (s >= w) return neg ? vnot(vzero(w), w) : vzero(w);
+    V r = vlshr(a, s, w);
+    if (neg)
+        for (uint32_t i = w - (uint32_t)s; i < w; i++) r[i / 32] |= 1u << (i % 32);
+    return r;
+}
+
+void vdivmod(const V& a, const V& b, uint32_t w, V* q, V* r) {  // unsigned, b != 0
+    *q = vzero(w);
+    *r = vzero(w + 1);
+    for (uint32_t i = w; i-- > 0;) {
+        *r = vshl(*r, 1, w + 1);
+        if (vbit(a, i)) (*r)[0] |= 1u;
+        if (vcmp(*r, b) >= 0) {
+            *r = vsub(*r, b, w + 1);
+            (*q)[i / 32] |= 1u << (i % 32);
+        }
+    }
+    *r = vmask(*r, w);
+}
+
+uint64_t vsmall(const V& a, bool* big) {  // value if it fits 64 bits
+    *big = false;
+    for (size_t i = 2; i < a.size(); i++)
+        if (a[i]) *big = true;
+    return (uint64_t)(a.size() > 0 ? a[0] : 0u) | ((uint64_t)(a.size() > 1 ? a[1] : 0u) << 32);
+}
+
+V vabs(const V& a, uint32_t w) { return vneg_sign(a, w) ? vneg(a, w) : vmask(a, w); }
+
+V binop(uint32_t op, const V& a, const V& b, uint32_t w) {  // terms._FOLD2
+    switch (op) {
+        case PFLT_BVADD: return vadd(a, b, w);
+        case PFLT_BVSUB: return vsub(a, b, w);
+        case PFLT_BVMUL: return vmul(a, b, w);
+        case PFLT_BVAND: case PFLT_BVOR: case PFLT_BVXOR: {
+            V r = vzero(w);
+            for (size_t i = 0; i < r.size(); i++) {
+                const uint32_t x = i < a.size() ? a[i] : 0u, y = i < b.size() ? b[i] : 0u;
+                r[i] = op == PFLT_BVAND ? (x & y) : (op == PFLT_BVOR ? (x | y) : (x ^ y));
+            }
+            return r;
+        }
+        case PFLT_BVSHL: case PFLT_BVLSHR: case PFLT_BVASHR: {
+            bool big;
+            const uint64_t s = vsmall(b, &big);
+            const uint64_t sh = big ? UINT64_MAX : s;
+            return op == PFLT_BVSHL ? vshl(a, sh, w) : (op == PFLT_BVLSHR ? vlshr(a, sh, w) : vashr(a, sh, w));
+        }
+        case PFLT_BVUDIV: case PFLT_BVUREM: {
+            if (vis_zero(b)) return op == PFLT_BVUDIV ? vnot(vzero(w), w) : vmask(a, w);
+            V q, r;
+            vdivmod(a, b, w, &q, &r);
+            return op == PFLT_BVUDIV ? q : r;
+        }
+        case PFLT_BVSDIV: {
+            const bool sa = vneg_sign(a, w), sb = vneg_sign(b, w);
+            if (vis_zero(b)) {
+                V one = vzero(w);
+                one[0] = 1;
+                return sa ? one : vnot(vzero(w), w);
+            }
+            V q, r;
+            vdivmod(vabs(a, w), vabs(b, w), w, &q, &r);
+            return sa == sb ? q : vneg(q, w);
+        }
+        case PFLT_BVSREM: {
+            if (vis_zero(b)) return vmask(a, w);
+            V q, r;
+            vdivmod(vabs(a, w), vabs(b, w), w, &q, &r);
+            return vneg_sign(a, w) ? vneg(r, w) : r;
+        }
+        case PFLT_BVSMOD: {  // Python's floor modulo of the signed values: sign of b
+            if (vis_zero(b)) return vmask(a, w);
+            V q, r;
+            vdivmod(vabs(a, w), vabs(b, w), w, &q, &r);
+            const bool sa = vneg_sign(a, w), sb = vneg_sign(b, w);
+            if (vis_zero(r)) return r;
+            V m = sa ? vneg(r, w) : r;  // truncated remainder, sign of a
+            if (sa != sb) m = vadd(m, vmask(b, w), w);
+            return m;
+        }
+        case PFLT_BVEXP: {
+            V r = vzero(w), x = vmask(a, w);
+            if (!r.empty()) r[0] = 1;
+            if (w == 0) return r;
+            const size_t eb = b.size() * 32;
+            for (size_t i = 0; i < eb; i++) {
+                if (vbit(b, (uint32_t)i)) r = vmul(r, x, w);
+                x = vmul(x, x, w);
+            }
+            return vmask(r, w);
+        }
+        default: return vzero(w);
+    }
+}
+
+bool cmpop(uint32_t op, const V& a, const V& b, uint32_t w) {  // terms._CMP
+    switch (op) {
+        case PFLT_BVULT: return vcmp(a, b) < 0;
+        case PFLT_BVULE: return vcmp(a, b) <= 0;
+        case PFLT_BVSLT: case PFLT_BVSLE: {
+            const bool sa = vneg_sign(a, w), sb = vneg_sign(b, w);
+            if (sa != sb) return sa;
+            const int c = vcmp(a, b);
+            return op == PFLT_BVSLT ? c < 0 : c <= 0;
+        }
+        case PFLT_BVUADD_NOOVF: {
+            const V s = vadd(a, b, w + 1);
+            return !vbit(s, w);
+        }
+        case PFLT_BVUMUL_NOOVF: {
+            const V p = vmul(a, b, 2 * w + 1);
+            for (uint32_t i = w; i < 2 * w + 1; i++)
+                if (vbit(p, i)) return false;
+            return true;
+        }
+        default: return false;
+    }
+}
+
+// ---- PF_W_HASH (include/pf_bytecode.h) -----------------------------------------------------
+void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
+    for (int i = 0; i < 10; i++) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c[0], p1 = (uint64_t)0xCD9E8D57u * c[2];
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0, n1 = (uint32_t)p1;
+        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1, n3 = (uint32_t)p0;
+        c[0] = n0; c[1] = n1; c[2] = n2; c[3] = n3;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+}
+
+V uf_hash(const V& x8, uint32_t salt) {
+    uint32_t xs[8];
+    for (int i = 0; i < 8; i++) xs[i] = i < (int)x8.size() ? x8[i] : 0u;
+    uint32_t h[4] = {xs[0], xs[1], xs[2], xs[3]};
+    philox(h, salt, 0x5BD1E995u);
+    uint32_t g[4] = {xs[4] ^ h[0], xs[5] ^ h[1], xs[6] ^ h[2], xs[7] ^ h[3]};
+    philox(g, salt, 0x27D4EB2Fu);
+    return V{h[0], h[1], h[2], h[3], g[0], g[1], g[2], g[3]};
+}
+
+uint32_t crc32_str(const std::string& s) {
+    uint32_t c = 0xffffffffu;
+    for (unsigned char ch : s) {
+        c ^= ch;
+        for (int k = 0; k < 8; k++) c = (c >> 1) ^ (0xEDB88320u & (0u - (c & 1u)));
+    }
+    return c ^ 0xffffffffu;
+}
+
+// chunks of a w-bit value: 256-bit pieces, LSB first (interp._chunks)
+std::vector<V> chunks256(const V& v, uint32_t w) {
+    std::vector<V> out;
+    uint32_t off = 0;
+    while (off < w) {
+        const uint32_t cw = std::min<uint32_t>(256, w - off);
+        out.push_back(vmask(vlshr(v, off, std::max<uint32_t>(w, 1)), cw));
+        off += 256;
+    }
+    return out;
+}
+
+struct KSpec {
+    bool has_lo;
+    V base;
+    std::vector<std::pair<V, V>> concrete;
+};
+
+struct Ev {
+    // the term store is read through the public accessors of pf_terms.cpp
+    void* st;
+    std::unordered_map<std::string, V> vars;
+    std::unordered_map<std::string, bool> bools;
+    std::map<std::pair<uint32_t, uint32_t>, V> read_vals;  // (array id, index id) -> value
+    std::unordered_map<uint32_t, V> app_vals;              // apply term id -> value
+    std::map<std::string, std::vector<std::pair<uint32_t, uint32_t>>> reads;  // array name -> (arr, idx)
+    std::vector<uint32_t> uf_apps;
+    std::map<uint32_t, KSpec> kspecs;
+    std::unordered_map<uint32_t, V> memo;
+
+    pflt_term_view T(uint32_t id) const {
+        pflt_term_view t;
+        pflt_view(st, id, &t);
+        return t;
+    }
+    std::string name_of(const pflt_term_view& t) const { return std::string(t.name ? t.name : ""); }
+    uint32_t width(const pflt_term_view& t) const { return t.sortk == 1 ? t.w1 : 0; }
+
+    static V of_limbs(const uint32_t* l, uint32_t n, uint32_t w) { return vmask(V(l, l + n), w); }
+
+    static bool keccak_name(const std::string& f, uint32_t* n, bool* inv) {
+        static const char pre[] = "keccak256_";
+        if (f.compare(0, sizeof(pre) - 1, pre) != 0) return false;
+        size_t i = sizeof(pre) - 1, j = i;
+        while (j < f.size() && f[j] >= '0' && f[j] <= '9') j++;
+        if (j == i) return false;
+        *n = (uint32_t)strtoul(f.c_str() + i, nullptr, 10);
+        if (j == f.size()) { *inv = false; return true; }
+        if (f.compare(j, std::string::npos, "-1") == 0) { *inv = true; return true; }
+        return false;
+    }
+
+    V keccak(uint32_t n, const V& x) {
+        auto it = kspecs.find(n);
+        if (it != kspecs.end())
+            for (const auto& c : it->second.concrete)
+                if (vcmp(c.first, vmask(x, n)) == 0) return vmask(c.second, 256);
+        V h;
+        bool first = true;
+        const uint32_t salt = crc32_str("keccak256_" + std::to_string(n));
+        for (const V& c : chunks256(x, n)) {
+            V in = first ? vmask(c, 256) : binop(PFLT_BVXOR, h, vmask(c, 256), 256);
+            h = uf_hash(in, salt);
+            first = false;
+        }
+        if (it == kspecs.end() || !it->second.has_lo) return h;
+        V k = vmask(h, 117);
+        return vadd(it->second.base, vshl(k, 6, 256), 256);
+    }
+
+    V keccak_inv(uint32_t n, const V& y, uint32_t term) {
+        size_t upto = uf_apps.size();
+        for (size_t i = 0; i < uf_apps.size(); i++)
+            if (uf_apps[i] == term) { upto = i; break; }
+        const std::string fname = "keccak256_" + std::to_string(n), iname = fname + "-1";
+        for (size_t i = 0; i < upto; i++) {
+            const pflt_term_view a = T(uf_apps[i]);
+            if (name_of(a) == fname) {
+                const V x = ev(a.args[0]);
+                if (vcmp(keccak(n, x), y) == 0) return x;
+            }
+        }
+        for (size_t i = 0; i < upto; i++) {
+            const pflt_term_view a = T(uf_apps[i]);
+            if (name_of(a) == iname && app_vals.count(uf_apps[i]) && vcmp(ev(a.args[0]), y) == 0)
+                return app_vals[uf_apps[i]];
+        }
+        auto it = app_vals.find(term);
+        return it != app_vals.end() ? it->second : vzero(n);
+    }
+
+    V power(uint32_t t, const pflt_term_view& tv) {
+        const V b = ev(tv.args[0]), e = ev(tv.args[1]);
+        for (uint32_t app : uf_apps) {
+            const pflt_term_view a = T(app);
+            if (name_of(a) != "Power" || a.nargs != 2) continue;
+            const pflt_term_view a0 = T(a.args[0]), a1 = T(a.args[1]);
+            if (a0.op == PFLT_BV && a1.op == PFLT_BV &&
+                vcmp(of_limbs(a0.limbs, a0.nlimbs, 256), b) == 0 && vcmp(of_limbs(a1.limbs, a1.nlimbs, 256), e) == 0)
+                return binop(PFLT_BVEXP, b, e, 256);
+        }
+        V c256 = vzero(256);
+        c256[0] = 256;
+        if (vcmp(b, c256) == 0) {
+            const uint32_t em = e.empty() ? 0u : (e[0] % 32u);
+            return vshl(V{1u}, 8u * em, 256);
+        }
+        for (uint32_t app : uf_apps) {
+            const pflt_term_view a = T(app);
+            if (name_of(a) != "Power" || a.nargs != 2 || !app_vals.count(app)) continue;
+            if (vcmp(ev(a.args[0]), b) == 0 && vcmp(ev(a.args[1]), e) == 0) return app_vals[app];
+        }
+        (void)t;
+        V one = vzero(256);
+        one[0] = 1;
+        return one;
+    }
+
+    V apply(uint32_t t, const pflt_term_view& tv) {
+        const std::string f = name_of(tv);
+        uint32_t n;
+        bool inv;
+        if (keccak_name(f, &n, &inv)) {
+            const pflt_term_view a = T(tv.args[0]);
+            uint32_t an;
+            bool ainv;
+            if (inv && a.op == PFLT_APPLY && keccak_name(name_of(a), &an, &ainv) && !ainv && an == n)
+                return ev(a.args[0]);
+            const V x = ev(tv.args[0]);
+            return inv ? keccak_inv(n, x, t) : keccak(n, x);
+        }
+        if (f == "Power" && tv.nargs == 2 && width(tv) == 256) return power(t, tv);
+        V h;
+        bool first = true;
+        const uint32_t salt = crc32_str(f);
+        for (uint32_t i = 0; i < tv.nargs; i++) {
+            const pflt_term_view a = T(tv.args[i]);
+            for (const V& c : chunks256(ev(tv.args[i]), width(a))) {
+                V in = first ? vmask(c, 256) : binop(PFLT_BVXOR, h, vmask(c, 256), 256);
+                h = uf_hash(in, salt);
+                first = false;
+            }
+        }
+        return vmask(h, width(tv));
+    }
+
+    V array_read(uint32_t arr, uint32_t idx, const V& iv) {
+        const pflt_term_view A = T(arr);
+        auto it = reads.find(name_of(A));
+        if (it == reads.end() || it->second.empty()) return vzero(A.w2);
+        const auto& es = it->second;
+        size_t last = es.size() - 1;
+        for (size_t i = 0; i < es.size(); i++)
+            if (es[i].first == arr && es[i].second == idx) { last = i; break; }
+        for (size_t i = 0; i <= last; i++) {
+            if (vcmp(ev(es[i].second), iv) == 0) {
+                auto jt = read_vals.find(es[i]);
+                return jt != read_vals.end() ? jt->second : vzero(A.w2);
+            }
+        }
+        return vzero(A.w2);
+    }
+
+    V select(uint32_t arr, const V& iv, uint32_t idx) {
+        const pflt_term_view A = T(arr);
+        if (A.op == PFLT_STORE) {
+            if (vcmp(ev(A.args[1]), iv) == 0) return ev(A.args[2]);
+            return select(A.args[0], iv, idx);
+        }
+        if (A.op == PFLT_K) return ev(A.args[0]);
+        if (A.op == PFLT_ITE) return select(bool_of(ev(A.args[0])) ? A.args[1] : A.args[2], iv, idx);
+        if (A.op == PFLT_ARRAY) return array_read(arr, idx, iv);
+        throw 1;
+    }
+
+    static bool bool_of(const V& v) { return !vis_zero(v); }
+    static V B(bool b) { return V{b ? 1u : 0u}; }
+
+    V ev(uint32_t t) {
+        auto it = memo.find(t);
+        if (it != memo.end()) return it->second;
+        V r = ev_(t);
+        memo.emplace(t, r);
+        return r;
+    }
+
+    V ev_(uint32_t t) {
+        const pflt_term_view tv = T(t);
+        const uint32_t w = width(tv);
+        switch (tv.op) {
+            case PFLT_BV: return of_limbs(tv.limbs, tv.nlimbs, w);
+            case PFLT_TRUE: return B(true);
+            case PFLT_FALSE: return B(false);
+            case PFLT_VAR: {
+                auto jt = vars.find(name_of(tv));
+                return jt != vars.end() ? vmask(jt->second, w) : vzero(w);
+            }
+            case PFLT_BVAR: {
+                auto jt = bools.find(name_of(tv));
+                return B(jt != bools.end() && jt->second);
+            }
+            case PFLT_BVNOT: return vnot(ev(tv.args[0]), w);
+            case PFLT_BVNEG: return vneg(ev(tv.args[0]), w);
+            case PFLT_EXTRACT: return vmask(vlshr(ev(tv.args[0]), (uint64_t)tv.i1, width(T(tv.args[0]))), w);
+            case PFLT_CONCAT: {
+                V v = vzero(w);
+                uint32_t off = w;
+                for (uint32_t i = 0; i < tv.nargs; i++) {
+                    const uint32_t aw = width(T(tv.args[i]));
+                    off -= aw;
+                    v = binop(PFLT_BVOR, v, vshl(vmask(ev(tv.args[i]), aw), off, w), w);
+                }
+                return v;
+            }
+            case PFLT_ZERO_EXTEND: return vmask(ev(tv.args[0]), w);
+            case PFLT_ITE: return bool_of(ev(tv.args[0])) ? ev(tv.args[1]) : ev(tv.args[2]);
+            case PFLT_SELECT: return select(tv.args[0], ev(tv.args[1]), tv.args[1]);
+            case PFLT_APPLY: return apply(t, tv);
+            case PFLT_EQ: return B(vcmp(ev(tv.args[0]), ev(tv.args[1])) == 0);
+            case PFLT_IFF: return B(bool_of(ev(tv.args[0])) == bool_of(ev(tv.args[1])));
+            case PFLT_AND:
+                for (uint32_t i = 0; i < tv.nargs; i++)
+                    if (!bool_of(ev(tv.args[i]))) return B(false);
+                return B(true);
+            case PFLT_OR:
+                for (uint32_t i = 0; i < tv.nargs; i++)
+                    if (bool_of(ev(tv.args[i]))) return B(true);
+                return B(false);
+            case PFLT_NOT: return B(!bool_of(ev(tv.args[0])));
+            case PFLT_XOR: return B(bool_of(ev(tv.args[0])) != bool_of(ev(tv.args[1])));
+            default: break;
+        }
+        if (tv.op >= PFLT_BVADD && tv.op <= PFLT_BVEXP) return binop(tv.op, ev(tv.args[0]), ev(tv.args[1]), w);
+        if (tv.op >= PFLT_BVULT && tv.op <= PFLT_BVUMUL_NOOVF) {
+            const uint32_t aw = width(T(tv.args[0]));
+            return B(cmpop(tv.op, ev(tv.args[0]), ev(tv.args[1]), aw));
+        }
+        throw 1;  // not evaluable: the caller reports "cannot evaluate"
+    }
+};
+
+}  // namespace
+
+extern "C" int pflt_recheck(void* store, const uint32_t* var_desc, size_t n_vars, const uint32_t* values,
+                            const uint32_t* uf_apps, size_t n_uf, const uint32_t* reads, size_t n_reads,
+                            const uint32_t* registry, size_t n_registry, const uint32_t* roots,
+                            size_t n_roots, uint8_t* out) {
+    try {
+        Ev E;
+        E.st = store;
+        // registry blob: as for pflt_lower (actors first, unused here)
+        size_t p = 0;
+        auto take = [&]() -> uint32_t {
+            if (p >= n_registry) throw 2;
+            return registry[p++];
+        };
+        const uint32_t na = take();
+        p += 8 * na;
+        const uint32_t ns = take();
+        for (uint32_t s = 0; s < ns; s++) {
+            const uint32_t n = take();
+            KSpec sp;
+            sp.has_lo = take() != 0;
+            V base(8);
+            for (int k = 0; k < 8; k++) base[k] = take();
+            sp.base = base;
+            const uint32_t nc = take();
+            for (uint32_t c = 0; c < nc; c++) {
+                V v(nl_of(n));
+                for (auto& x : v) x = take();
+                V dg(8);
+                for (auto& x : dg) x = take();
+                sp.concrete.push_back({vmask(v, n), dg});
+            }
+            E.kspecs[n] = sp;
+        }
+        // the witness (interp.Witness.__init__): var descriptors (type, a, b, c) with values
+        for (size_t i = 0; i < n_vars; i++) {
+            const uint32_t* d = var_desc + 4 * i;
+            const V val(values + 8 * i, values + 8 * i + 8);
+            if (d[0] == PFLT_VT_TERM) {
+                const pflt_term_view t = E.T(d[1]);
+                if (t.op == PFLT_VAR)
+                    E.vars[E.name_of(t)] = val;
+                else if (t.op == PFLT_BVAR)
+                    E.bools[E.name_of(t)] = (val[0] & 1u) != 0;
+                else
+                    E.app_vals[d[1]] = val;
+            } else if (d[0] == PFLT_VT_SELECT) {
+                E.read_vals[{d[1], d[2]}] = val;
+            } else {  // one 256-bit chunk (lo = d[2]) of a wider free symbol
+                const pflt_term_view t = E.T(d[1]);
+                const uint32_t w = E.width(t);
+                V& cur = E.vars[E.name_of(t)];
+                if (cur.empty()) cur = vzero(w);
+                cur = binop(PFLT_BVOR, cur, vshl(val, d[2], w), w);
+            }
+        }
+        E.uf_apps.assign(uf_apps, uf_apps + n_uf);
+        for (size_t i = 0; i < n_reads; i++) {
+            const uint32_t arr = reads[2 * i], idx = reads[2 * i + 1];
+            E.reads[E.name_of(E.T(arr))].push_back({arr, idx});
+        }
+        for (size_t i = 0; i < n_roots; i++) out[i] = Ev::bool_of(E.ev(roots[i])) ? 1u : 0u;
+        return 0;
+    } catch (...) {
+        return -1;
+    }
+}

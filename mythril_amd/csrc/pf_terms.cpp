@@ -1396,6 +1396,24 @@ void* pflt_lower(void* st, const uint32_t* roots, size_t n_roots, const uint32_t
 
 const char* pflt_last_error(void) { return t_err.c_str(); }
 
+int pflt_view(void* st, uint32_t id, pflt_term_view* out) {
+    const Store* S = (const Store*)st;
+    if (id >= S->t.size()) return -1;
+    const TermRec& r = S->t[id];
+    out->op = r.op;
+    out->sortk = r.sortk;
+    out->w1 = r.w1;
+    out->w2 = r.w2;
+    out->nargs = (uint32_t)r.args.size();
+    out->args = r.args.data();
+    out->i0 = r.i0;
+    out->i1 = r.i1;
+    out->limbs = r.val.data();
+    out->nlimbs = (uint32_t)r.val.size();
+    out->name = r.name.c_str();
+    return 0;
+}
+
 void pflt_result_free(void* res) { delete (Result*)res; }
 
 /* sizes: [0] n_vars, [1] names bytes, [2] n_var_terms, [3] n_uf_apps, [4] n_arrays,

@@ -406,9 +406,17 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
             # constraint-directed hint model itself; any other index was found by the search
             idx = int(res.found[k])
             origin[key] = _origin(idx, progs[k], cfg.hints, parented[k])
-            w = Witness(lows[k], v, reg)
-            # re-check on the host under the same interpretation before trusting it
-            if not all(w.ev(c) for c in key[0]):
+            # re-check on the host under the same interpretation before trusting it:
+            # natively (pflt_recheck, the Witness interpretation bit for bit) when built
+            ok = None
+            if _NATIVE_TERMS:
+                from . import native_terms
+
+                ok = native_terms.recheck(list(key[0]), lows[k], v, reg)
+            if ok is None:
+                w = Witness(lows[k], v, reg)
+                ok = all(w.ev(c) for c in key[0])
+            if not ok:
                 # the program disagrees with the terms under this assignment: a lowering
                 # or interpretation bug — sound (the bucket stays unanswered), but counted
                 with _lock:

@@ -318,3 +318,48 @@ def lower_bucket(bucket: List[T.Term], reg: UFRegistry, parent: Optional[dict], 
     """gpu_check._lower_bucket natively: (witness metadata, program)."""
     r = lower_native(bucket, reg, parent, PROGRAM | (HINTS if hints else 0), seed)
     return r.lowered(), r.program(seed)
+
+
+def recheck(bucket: List[T.Term], lo: Lowered, values: List[int], reg: UFRegistry) -> Optional[bool]:
+    """The host re-check of a bucket witness natively (pflt_recheck, csrc/pf_recheck.cpp):
+    every conjunct true under the witness (interp.Witness's interpretation).  None when the
+    library cannot evaluate some term (the caller re-checks in Python)."""
+    st = store()
+    if st is None or not hasattr(st.L, "pflt_recheck"):
+        return None
+    L = st.L
+    if not getattr(L, "_recheck_bound", False):
+        L.pflt_recheck.restype = ctypes.c_int
+        L.pflt_recheck.argtypes = [ctypes.c_void_p, _u32p, ctypes.c_size_t, _u32p, _u32p, ctypes.c_size_t,
+                                   _u32p, ctypes.c_size_t, _u32p, ctypes.c_size_t, _u32p, ctypes.c_size_t,
+                                   ctypes.POINTER(ctypes.c_uint8)]
+        L._recheck_bound = True
+    with st.lock:
+        ex = st.export
+        desc: List[int] = []
+        for t in lo.var_terms:
+            if t.op == "select":
+                desc += [VT_SELECT, ex(t.args[0]), ex(t.args[1]), 0]
+            elif t.op == "extract" and t.args[0].op == "var":
+                desc += [VT_EXTRACT, ex(t.args[0]), t.val[1], t.val[0]]
+            else:
+                desc += [VT_TERM, ex(t), 0, 0]
+        vals = np.frombuffer(b"".join(((v or 0) & ((1 << 256) - 1)).to_bytes(32, "little") for v in values)
+                             or b"\0" * 32, dtype="<u4").astype(np.uint32)
+        ufs = [ex(app) for _, _, app in lo.uf_apps]
+        reads: List[int] = []
+        for entries in lo.array_reads.values():
+            for idx, sel in entries:
+                reads += [ex(sel.args[0]), ex(idx)]
+        roots = [ex(c) for c in bucket]
+        a = lambda xs: np.array(xs or [0], dtype=np.uint32)  # noqa: E731
+        d_, u_, r_, ro_ = a(desc), a(ufs), a(reads), a(roots)
+        regb = _registry_blob(reg)
+        out = np.zeros(max(len(roots), 1), dtype=np.uint8)
+        rc = L.pflt_recheck(st.h, d_.ctypes.data_as(_u32p), len(lo.var_terms), vals.ctypes.data_as(_u32p),
+                            u_.ctypes.data_as(_u32p), len(ufs), r_.ctypes.data_as(_u32p), len(reads) // 2,
+                            regb.ctypes.data_as(_u32p), len(regb), ro_.ctypes.data_as(_u32p), len(roots),
+                            out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))
+    if rc != 0:
+        return None
+    return bool(out[:len(roots)].all())

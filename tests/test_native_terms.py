@@ -262,3 +262,41 @@ def test_native_witness_evaluates_like_the_program(corpus_buckets):
             vals = [rng.choice((0, 1, 4, 36, 68, rng.getrandbits(v.width))) & ir.mask(v.width) for v in prog.vars]
             w = Witness(lo, vals, reg)
             assert sv.evaluate(vals) == all(bool(w.ev(c)) for c in b)
+
+
+def test_native_recheck_agrees_with_the_witness(corpus_buckets):
+    """pflt_recheck (csrc/pf_recheck.cpp) gives Witness.ev's verdict on every conjunct —
+    on satisfying and on failing assignments, over corpus buckets (arrays, keccak, actors),
+    wide values and UF / Power sets."""
+    from mythril_amd.smt.interp import Witness
+
+    reg, bks = corpus_buckets
+    rng = random.Random(21)
+    checked = agreed = sat = 0
+    sets = [(b, reg) for b in bks[:120]]
+    reg2 = UFRegistry()
+    reg2.keccak[512] = KeccakSpec(lo=3 * ((2 ** 256 - 1) // 10 ** 40))
+    reg2.keccak[512].concrete[(5 << 256) | 1] = 0xABCDEF
+    a, b = T.var("a", 256), T.var("b", 256)
+    f = T.apply("keccak256_512", 256, T.concat(a, T.const(1, 256)))
+    sets += [([c], UFRegistry()) for c in _wide_cases()[:15]]
+    sets += [([T.eq(T.apply("keccak256_512-1", 512, f), T.concat(a, T.const(1, 256))),
+               T.cmp("bvult", f, T.apply("keccak256_512", 256, T.concat(b, T.const(1, 256))))], reg2),
+             ([T.cmp("bvslt", T.const(0, 256), T.apply("Power", 256, T.const(256, 256), a)),
+               T.eq(T.apply("myuf", 160, a, T.extract(63, 0, b)), T.extract(159, 0, b))], reg2)]
+    for bucket, rg in sets:
+        try:
+            lo, prog = NT.lower_bucket(bucket, rg, None, True, 3)
+        except LoweringError:
+            continue
+        for trial in range(6):
+            if trial == 0:   # the hint model (often a witness)
+                vals = [v.parent or 0 for v in prog.vars]
+            else:
+                vals = [rng.choice((0, 1, 4, 68, rng.getrandbits(v.width))) & ir.mask(v.width) for v in prog.vars]
+            want = all(bool(Witness(lo, vals, rg).ev(c)) for c in bucket)
+            got = NT.recheck(bucket, lo, vals, rg)
+            checked += 1
+            agreed += got == want
+            sat += want
+    assert checked > 300 and agreed == checked and sat > 20
