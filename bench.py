@@ -153,7 +153,7 @@ def discharge(args):
     t_live = time.perf_counter() - t_live
     live_kinds = [m.origin for m in live if m is not None]
     # cold single-query latency (the fork-prune call site answers one query at a time)
-    sample = [q for q in c.queries if q.label == "sat"][:24]
+    sample = [q for q in c.queries if q.label == "sat"][:96]
     lat = []
     gpu_check.STATS.phase_s.clear()
     for q in sample:
@@ -186,7 +186,9 @@ def discharge(args):
             "unsat_labelled": len(unsat), "unsat_labelled_false_positives": len(fps),
             "false_positive_origins": fps[:5],
             "single_query_ms": {"median": float(np.median(lat)) if lat else None,
-                                "mean": float(np.mean(lat)) if lat else None, "queries": len(lat),
+                                "mean": float(np.mean(lat)) if lat else None,
+                                "p95": float(np.percentile(lat, 95)) if lat else None,
+                                "max": float(np.max(lat)) if lat else None, "queries": len(lat),
                                 "phase_mean_ms": sq_phase},
             "buckets_searched": stats_batch[0], "kernel_ms": stats_batch[1], "host_s": stats_batch[2],
             "phase_s": phase_s, "lowering_workers": n_workers, "pool_start_s": round(t_pool, 3),

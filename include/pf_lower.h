@@ -159,6 +159,14 @@ typedef struct pflt_term_view {
 } pflt_term_view;
 int pflt_view(void* store, uint32_t id, pflt_term_view* out);
 
+/* Independence buckets of one query (mythril_amd/smt/independence.py:buckets — the same
+ * partition, bucket order and conjunct order; reference: independence_solver.py:38-83):
+ * roots = the query's constraints; out_ids gets the flattened conjuncts bucket by bucket
+ * (capacity >= their number), out_sizes each bucket's size.  Returns the number of buckets,
+ * -1 when a capacity is too small, -2 on an unknown id.  Keys are memoised per term. */
+int64_t pflt_buckets(void* store, const uint32_t* roots, size_t n_roots, uint32_t* out_ids, size_t cap_ids,
+                     uint32_t* out_sizes, size_t cap_sizes);
+
 /* Host re-check of a bucket witness (csrc/pf_recheck.cpp; mythril_amd/smt/interp.py
  * Witness.ev, bit for bit): var_desc = n_vars x 4 u32 (the result's var_terms descriptors:
  * type, a, b, c) with values n_vars x 8 u32; uf_apps = application term ids in registration

@@ -156,6 +156,12 @@ struct TermRec {
 
 struct Store {
     std::vector<TermRec> t;
+    // independence keys (smt/independence.py), memoised per term: sorted key ids and the
+    // widths whose inverse keccak the term applies to a non-application
+    std::vector<int32_t> kmemo;  // term id -> index into keysets (-1: not computed)
+    std::vector<std::vector<uint32_t>> keysets, finvs;
+    std::unordered_map<std::string, uint32_t> key_ids;
+    std::vector<std::string> key_names;
 };
 
 // ---- the DAG (mythril_amd/lower.py Dag) ---------------------------------------------------
@@ -1395,6 +1401,175 @@ void* pflt_lower(void* st, const uint32_t* roots, size_t n_roots, const uint32_t
 }
 
 const char* pflt_last_error(void) { return t_err.c_str(); }
+
+}  // extern "C"
+
+namespace {
+
+uint32_t key_id(Store* S, const std::string& k) {
+    auto it = S->key_ids.find(k);
+    if (it != S->key_ids.end()) return it->second;
+    const uint32_t id = (uint32_t)S->key_names.size();
+    S->key_names.push_back(k);
+    S->key_ids.emplace(k, id);
+    return id;
+}
+
+bool keccak_app(const std::string& f, std::string* n, bool* inv) {  // ^keccak256_(\d+)(-1)?$
+    static const char pre[] = "keccak256_";
+    if (f.compare(0, sizeof(pre) - 1, pre) != 0) return false;
+    size_t i = sizeof(pre) - 1, j = i;
+    while (j < f.size() && isdigit((unsigned char)f[j])) j++;
+    if (j == i) return false;
+    *n = f.substr(i, j - i);
+    if (j == f.size()) { *inv = false; return true; }
+    if (f.compare(j, std::string::npos, "-1") == 0) { *inv = true; return true; }
+    return false;
+}
+
+void merge_sorted(std::vector<uint32_t>* into, const std::vector<uint32_t>& b) {
+    std::vector<uint32_t> out;
+    out.reserve(into->size() + b.size());
+    std::set_union(into->begin(), into->end(), b.begin(), b.end(), std::back_inserter(out));
+    into->swap(out);
+}
+
+// dependence_keys + free_inverse_widths of every term below root (iterative post-order)
+int32_t dep_keys(Store* S, uint32_t root) {
+    if (S->kmemo.size() < S->t.size()) S->kmemo.resize(S->t.size(), -1);
+    if (S->kmemo[root] >= 0) return S->kmemo[root];
+    std::vector<std::pair<uint32_t, bool>> stack{{root, false}};
+    while (!stack.empty()) {
+        const auto [x, expanded] = stack.back();
+        stack.pop_back();
+        if (S->kmemo[x] >= 0) continue;
+        const TermRec& r = S->t[x];
+        if (!expanded) {
+            stack.push_back({x, true});
+            for (uint32_t a : r.args)
+                if (S->kmemo[a] < 0) stack.push_back({a, false});
+            continue;
+        }
+        std::vector<uint32_t> own, finv;
+        if (r.op == PFLT_VAR || r.op == PFLT_BVAR) own.push_back(key_id(S, "v:" + r.name));
+        else if (r.op == PFLT_ARRAY) own.push_back(key_id(S, "a:" + r.name));
+        else if (r.op == PFLT_APPLY) {
+            std::string n;
+            bool inv;
+            if (keccak_app(r.name, &n, &inv)) {
+                own.push_back(key_id(S, "k:" + n));
+                if (inv) {
+                    const TermRec& a = S->t[r.args[0]];
+                    if (!(a.op == PFLT_APPLY && a.name == "keccak256_" + n)) finv.push_back(key_id(S, n));
+                }
+            } else if (r.name == "Power") {
+                own.push_back(key_id(S, "f:Power"));
+            }
+        }
+        std::sort(own.begin(), own.end());
+        std::sort(finv.begin(), finv.end());
+        for (uint32_t a : r.args) {
+            merge_sorted(&own, S->keysets[S->kmemo[a]]);
+            merge_sorted(&finv, S->finvs[S->kmemo[a]]);
+        }
+        S->kmemo[x] = (int32_t)S->keysets.size();
+        S->keysets.push_back(std::move(own));
+        S->finvs.push_back(std::move(finv));
+    }
+    return S->kmemo[root];
+}
+
+}  // namespace
+
+extern "C" {
+
+/* Independence buckets of one query (smt/independence.py:buckets, the same partition and
+ * order): conjuncts = the roots with top-level ands flattened and true dropped; buckets
+ * share no symbol, array, Power, or keccak family (a width with a free inverse lookup).
+ * out_ids: the conjuncts bucket by bucket (capacity >= total conjuncts); out_sizes: each
+ * bucket's size.  Returns the number of buckets, or -1 (capacity) / -2 (bad id). */
+int64_t pflt_buckets(void* st, const uint32_t* roots, size_t n_roots, uint32_t* out_ids, size_t cap_ids,
+                     uint32_t* out_sizes, size_t cap_sizes) {
+    Store* S = (Store*)st;
+    std::vector<uint32_t> cs;
+    std::vector<uint32_t> stack;
+    for (size_t i = n_roots; i-- > 0;) stack.push_back(roots[i]);
+    while (!stack.empty()) {
+        const uint32_t c = stack.back();
+        stack.pop_back();
+        if (c >= S->t.size()) return -2;
+        const TermRec& r = S->t[c];
+        if (r.op == PFLT_AND) {
+            for (size_t i = r.args.size(); i-- > 0;) stack.push_back(r.args[i]);
+        } else if (r.op != PFLT_TRUE) {
+            cs.push_back(c);
+        }
+    }
+    std::vector<uint32_t> families;
+    std::vector<int32_t> kidx(cs.size());
+    for (size_t i = 0; i < cs.size(); i++) {
+        kidx[i] = dep_keys(S, cs[i]);
+        merge_sorted(&families, S->finvs[kidx[i]]);
+    }
+    // union-find over key ids
+    std::unordered_map<uint32_t, uint32_t> parent;
+    auto find = [&](uint32_t k) {
+        while (parent[k] != k) {
+            parent[k] = parent[parent[k]];
+            k = parent[k];
+        }
+        return k;
+    };
+    std::vector<std::vector<uint32_t>> kept(cs.size());
+    for (size_t i = 0; i < cs.size(); i++) {
+        for (uint32_t k : S->keysets[kidx[i]]) {
+            const std::string& nm = S->key_names[k];
+            if (nm.compare(0, 2, "k:") == 0) {
+                auto it = S->key_ids.find(nm.substr(2));
+                if (it == S->key_ids.end() || !std::binary_search(families.begin(), families.end(), it->second))
+                    continue;
+            }
+            kept[i].push_back(k);
+        }
+        bool have = false;
+        uint32_t first = 0;
+        for (uint32_t k : kept[i]) {
+            if (!parent.count(k)) parent[k] = k;
+            if (!have) {
+                first = find(k);
+                have = true;
+            } else {
+                const uint32_t rk = find(k);
+                if (rk != first) parent[rk] = first;
+            }
+        }
+    }
+    std::vector<uint32_t> group_root, ground;
+    std::vector<std::vector<uint32_t>> groups;
+    std::unordered_map<uint32_t, size_t> gpos;
+    for (size_t i = 0; i < cs.size(); i++) {
+        if (kept[i].empty()) {
+            ground.push_back(cs[i]);
+            continue;
+        }
+        const uint32_t rt = find(kept[i][0]);
+        auto it = gpos.find(rt);
+        if (it == gpos.end()) {
+            gpos.emplace(rt, groups.size());
+            groups.push_back({cs[i]});
+        } else {
+            groups[it->second].push_back(cs[i]);
+        }
+    }
+    if (!ground.empty()) groups.push_back(ground);
+    if (cs.size() > cap_ids || groups.size() > cap_sizes) return -1;
+    size_t o = 0;
+    for (size_t g = 0; g < groups.size(); g++) {
+        out_sizes[g] = (uint32_t)groups[g].size();
+        for (uint32_t c : groups[g]) out_ids[o++] = c;
+    }
+    return (int64_t)groups.size();
+}
 
 int pflt_view(void* st, uint32_t id, pflt_term_view* out) {
     const Store* S = (const Store*)st;

@@ -316,7 +316,13 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
             set_buckets.append(None)
             continue
         parent = parents[i] if parents else None
-        bks = buckets(cs) if cfg.split else [cs]
+        bks = None
+        if cfg.split and _NATIVE_TERMS:
+            from . import native_terms
+
+            bks = native_terms.buckets(cs)      # the same partition (pflt_buckets)
+        if bks is None:
+            bks = buckets(cs) if cfg.split else [cs]
         ks = []
         for b in bks:
             # a witness answers its bucket whatever parent model seeded the search

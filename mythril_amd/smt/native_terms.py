@@ -363,3 +363,37 @@ def recheck(bucket: List[T.Term], lo: Lowered, values: List[int], reg: UFRegistr
     if rc != 0:
         return None
     return bool(out[:len(roots)].all())
+
+
+def buckets(constraints: List[T.Term]) -> Optional[List[List[T.Term]]]:
+    """independence.buckets natively (pflt_buckets: the same partition and order, keys
+    memoised per stored term); None when the library lacks it."""
+    st = store()
+    if st is None or not hasattr(st.L, "pflt_buckets"):
+        return None
+    L = st.L
+    if not getattr(L, "_buckets_bound", False):
+        L.pflt_buckets.restype = ctypes.c_int64
+        L.pflt_buckets.argtypes = [ctypes.c_void_p, _u32p, ctypes.c_size_t, _u32p, ctypes.c_size_t,
+                                   _u32p, ctypes.c_size_t]
+        L._buckets_bound = True
+    with st.lock:
+        roots = np.array([st.export(c) for c in constraints] or [0], dtype=np.uint32)
+        cap = 4 * len(constraints) + 256
+        while True:
+            ids = np.zeros(cap, dtype=np.uint32)
+            sizes = np.zeros(cap, dtype=np.uint32)
+            nb = L.pflt_buckets(st.h, roots.ctypes.data_as(_u32p), len(constraints), ids.ctypes.data_as(_u32p),
+                                cap, sizes.ctypes.data_as(_u32p), cap)
+            if nb != -1:
+                break
+            cap *= 4
+        if nb < 0:
+            return None
+        terms = st.terms
+        out, o = [], 0
+        idl = ids.tolist()
+        for n in sizes[:nb].tolist():
+            out.append([terms[i] for i in idl[o:o + n]])
+            o += n
+        return out

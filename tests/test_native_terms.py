@@ -300,3 +300,34 @@ def test_native_recheck_agrees_with_the_witness(corpus_buckets):
             agreed += got == want
             sat += want
     assert checked > 300 and agreed == checked and sat > 20
+
+
+def test_native_buckets_match(corpus_buckets):
+    """pflt_buckets gives independence.buckets' partition, bucket order and conjunct order —
+    on whole corpus queries (keccak conditions conjoined, free inverse lookups) and on the
+    keccak / Power sets."""
+    import mythril_amd.engine as E
+
+    eng = oracle_engine.OracleEngine()
+    saved = E.get_engine
+    E.get_engine = lambda device=None: eng
+    try:
+        c = corpus.build(10, 2, seed=11)
+    finally:
+        E.get_engine = saved
+    for q in c.queries:
+        assert NT.buckets(q.constraints) == buckets(q.constraints)
+    a, b = T.var("a", 256), T.var("b", 256)
+    y = T.var("y", 256)
+    f = T.apply("keccak256_512", 256, T.concat(a, T.const(1, 256)))
+    g = T.apply("keccak256_512", 256, T.concat(b, T.const(1, 256)))
+    cases = [
+        [T.cmp("bvult", f, T.const(5, 256)), T.cmp("bvult", g, T.const(7, 256))],   # no inverse: apart
+        [T.cmp("bvult", f, T.const(5, 256)), T.cmp("bvult", g, T.const(7, 256)),
+         T.eq(T.apply("keccak256_512-1", 512, y), T.concat(a, T.const(1, 256)))],    # free inverse: one family
+        [T.and_(T.eq(a, T.const(1, 256)), T.TRUE, T.eq(b, T.const(2, 256))), T.TRUE, T.cmp("bvult", T.const(1, 8), T.const(2, 8))],
+        [T.cmp("bvslt", T.const(0, 256), T.apply("Power", 256, a, b)),
+         T.eq(T.apply("Power", 256, T.const(256, 256), T.const(3, 256)), T.const(1 << 24, 256)), T.eq(y, y)],
+    ]
+    for cs in cases:
+        assert NT.buckets(cs) == buckets(cs)
