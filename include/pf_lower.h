@@ -125,6 +125,7 @@ int pfl_version(void);
 #define PFLT_GET_POOL 7
 #define PFLT_GET_ROOTS 8
 #define PFLT_GET_FORCED 9
+#define PFLT_GET_IN_ROOTS 10  /* the bucket's conjuncts as given */
 
 void* pflt_store_new(void);
 void pflt_store_free(void* store);
@@ -145,7 +146,7 @@ void* pflt_lower(void* store, const uint32_t* roots, size_t n_roots, const uint3
                  uint32_t flags, uint32_t seed, int* rc_out);
 const char* pflt_last_error(void);
 void pflt_result_free(void* result);
-void pflt_result_info(void* result, uint64_t* info);  /* 14 sizes, see pf_terms.cpp */
+void pflt_result_info(void* result, uint64_t* info);  /* 17 sizes, see pf_terms.cpp */
 void pflt_result_get(void* result, uint32_t which, uint32_t* out, char* names_out);
 
 /* A stored term, read-only (pointers valid until the next pflt_add). */
@@ -177,6 +178,55 @@ int pflt_recheck(void* store, const uint32_t* var_desc, size_t n_vars, const uin
                  const uint32_t* uf_apps, size_t n_uf, const uint32_t* reads, size_t n_reads,
                  const uint32_t* registry, size_t n_registry, const uint32_t* roots, size_t n_roots,
                  uint8_t* out);
+
+/* ---- batches (the live path's per-call pipeline, mythril_amd/smt/gpu_check.check_sets) ----
+ * Parent models: a handle holding values by symbol name and by base-array read, built from
+ * explicit values (pflt_parent_new: the par_* layout of pflt_lower) or from the store's
+ * recent-value tables (pflt_recent_parent: the newest value of each symbol / read the
+ * bucket's dependence keys name — gpu_check._recent_parent; NULL when none is known).  The
+ * tables are filled by pflt_note_vars (z3 model values) and pflt_note_result (an accepted
+ * bucket witness: gpu_check._note_witness), least-recently-updated first out (recent_size
+ * symbols; 1024 arrays of 256 reads). */
+void* pflt_parent_new(const char* names, const uint32_t* name_vals, size_t n_names, const uint32_t* reads,
+                      const uint32_t* read_vals, size_t n_reads);
+void pflt_parent_free(void* parents);
+void pflt_parent_info(const void* parents, uint64_t* info); /* n_names, name bytes, value words, n_reads */
+void pflt_parent_get(const void* parents, char* names, uint32_t* name_vals, uint32_t* reads, uint32_t* read_vals);
+void pflt_recent_clear(void* store);
+void pflt_note_vars(void* store, const char* names, const uint32_t* vals, size_t n, size_t recent_size);
+void pflt_note_result(void* store, const void* result, const uint32_t* values, size_t recent_size);
+void* pflt_recent_parent(void* store, const uint32_t* roots, size_t n_roots);
+
+/* One bucket of a pflt_lower_many call. */
+typedef struct pflt_job {
+    const uint32_t* roots;  /* the bucket's conjuncts */
+    size_t n_roots;
+    const void* parents;    /* a parent-model handle or NULL */
+    uint32_t flags;         /* PFLT_HINTS | PFLT_PROGRAM */
+    uint32_t seed;
+} pflt_job;
+/* Lower n buckets on n_threads host threads (the store is only read: no pflt_add may run
+ * meanwhile).  results[j] is always a handle: pflt_result_status 0, or pflt_lower's rc with
+ * the message in pflt_result_error. */
+void pflt_lower_many(void* store, const pflt_job* jobs, size_t n, const uint32_t* registry, size_t n_registry,
+                     uint32_t n_threads, void** results);
+int pflt_result_status(const void* result);
+const char* pflt_result_error(const void* result);
+int pflt_result_parented(const void* result);
+/* Free the program and DAG tables of a result (kept: variables, witness metadata, roots). */
+void pflt_result_shrink(void* result);
+/* The flat arrays of a pf_batch_create batch (mythril_amd/ir.py Batch) from n results:
+ * sizes = total instructions, constants, variables, parent values; then code (x4 u32, word 3
+ * = reach_lut[op * lut_w + width]), consts (x8), schema (x4), parents (x8), descs (x8). */
+void pflt_pack_sizes(void* const* results, size_t n, uint64_t* sizes);
+void pflt_pack_batch(void* const* results, size_t n, const uint32_t* seeds, const uint32_t* reach_lut,
+                     uint32_t lut_w, uint32_t* code, uint32_t* consts, uint32_t* schema, uint32_t* parents,
+                     uint32_t* descs);
+/* pflt_recheck of n results at once on n_threads threads: values = each result's variables
+ * x 8 u32, results back to back; status[j] = 1 (every conjunct true), 0 (some false), -1
+ * (not evaluable here: re-check in Python). */
+void pflt_recheck_many(void* store, void* const* results, size_t n, const uint32_t* values,
+                       const uint32_t* registry, size_t n_registry, uint32_t n_threads, int8_t* status);
 
 #ifdef __cplusplus
 }

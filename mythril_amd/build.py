@@ -39,7 +39,7 @@ def build_lower(force: bool = False, verbose: bool = False) -> str:
     if not force and os.path.exists(LOWER_OUT) and all(
             os.path.getmtime(os.path.join(CSRC, s)) <= os.path.getmtime(LOWER_OUT) for s in LOWER_SOURCES):
         return LOWER_OUT
-    cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-o", LOWER_OUT + ".tmp",
+    cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-pthread", "-o", LOWER_OUT + ".tmp",
            os.path.join(CSRC, "pf_lower.cpp"), os.path.join(CSRC, "pf_seed.cpp"),
            os.path.join(CSRC, "pf_terms.cpp"), os.path.join(CSRC, "pf_recheck.cpp")]
     if verbose:

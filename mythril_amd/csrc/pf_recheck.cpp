@@ -15,6 +15,8 @@
 #include <map>
 #include <string>
 #include <unordered_map>
+#include <atomic>
+#include <thread>
 #include <vector>
 
 #include "../../include/pf_lower.h"
@@ -514,9 +516,7 @@ struct Ev {
     }
 };
 
-}  // namespace
-
-extern "C" int pflt_recheck(void* store, const uint32_t* var_desc, size_t n_vars, const uint32_t* values,
+int recheck_core(void* store, const uint32_t* var_desc, size_t n_vars, const uint32_t* values,
                             const uint32_t* uf_apps, size_t n_uf, const uint32_t* reads, size_t n_reads,
                             const uint32_t* registry, size_t n_registry, const uint32_t* roots,
                             size_t n_roots, uint8_t* out) {
@@ -581,4 +581,61 @@ extern "C" int pflt_recheck(void* store, const uint32_t* var_desc, size_t n_vars
     } catch (...) {
         return -1;
     }
+}
+
+}  // namespace
+
+extern "C" int pflt_recheck(void* store, const uint32_t* var_desc, size_t n_vars, const uint32_t* values,
+                            const uint32_t* uf_apps, size_t n_uf, const uint32_t* reads, size_t n_reads,
+                            const uint32_t* registry, size_t n_registry, const uint32_t* roots,
+                            size_t n_roots, uint8_t* out) {
+    return recheck_core(store, var_desc, n_vars, values, uf_apps, n_uf, reads, n_reads, registry, n_registry,
+                        roots, n_roots, out);
+}
+
+// the witness metadata of a lowering result (pflt_result_get), re-checked like pflt_recheck
+extern "C" void pflt_recheck_many(void* store, void* const* results, size_t n, const uint32_t* values,
+                                  const uint32_t* registry, size_t n_registry, uint32_t n_threads,
+                                  int8_t* status) {
+    std::vector<size_t> off(n + 1, 0);
+    for (size_t j = 0; j < n; j++) {
+        uint64_t info[17];
+        pflt_result_info(results[j], info);
+        off[j + 1] = off[j] + 8 * info[0];
+    }
+    auto one = [&](size_t j) {
+        uint64_t info[17];
+        void* R = results[j];
+        pflt_result_info(R, info);
+        const size_t nvt = info[2], nuf = info[3], na = info[4], nr = info[5], nro = info[14];
+        std::vector<uint32_t> desc(4 * nvt + 1), ufs(nuf + 1), rd(na + 2 * nr + 1), roots(nro + 1);
+        pflt_result_get(R, PFLT_GET_VAR_TERMS, desc.data(), nullptr);
+        pflt_result_get(R, PFLT_GET_UF_APPS, ufs.data(), nullptr);
+        pflt_result_get(R, PFLT_GET_READS, rd.data(), nullptr);
+        pflt_result_get(R, PFLT_GET_IN_ROOTS, roots.data(), nullptr);
+        // var_terms pair with the program's variables (interp.Witness zips them)
+        const size_t nv = std::min<size_t>(nvt, info[0]);
+        std::vector<uint8_t> out(nro + 1, 0);
+        const int rc = recheck_core(store, desc.data(), nv, values + off[j], ufs.data(), nuf, rd.data() + na, nr,
+                                    registry, n_registry, roots.data(), nro, out.data());
+        if (rc != 0) {
+            status[j] = -1;
+            return;
+        }
+        int8_t ok = 1;
+        for (size_t i = 0; i < nro; i++) ok &= out[i] ? 1 : 0;
+        status[j] = ok;
+    };
+    const size_t nt = std::min<size_t>(n_threads ? n_threads : 1, n);
+    if (nt <= 1) {
+        for (size_t j = 0; j < n; j++) one(j);
+        return;
+    }
+    std::atomic<size_t> next{0};
+    std::vector<std::thread> pool;
+    for (size_t t = 0; t < nt; t++)
+        pool.emplace_back([&]() {
+            for (size_t j; (j = next.fetch_add(1)) < n;) one(j);
+        });
+    for (auto& th : pool) th.join();
 }

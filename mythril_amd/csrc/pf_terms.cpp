@@ -21,8 +21,11 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <atomic>
+#include <list>
 #include <map>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <utility>
 #include <vector>
@@ -154,8 +157,70 @@ struct TermRec {
     std::string name;
 };
 
+// Parent model of one bucket: values by symbol name (any width) and by base-array read
+// (array id, index id) — pflt_lower's par_* arguments, or gpu_check._recent_parent's dict.
+struct Parents {
+    std::unordered_map<std::string, Big> names;
+    std::map<std::pair<uint32_t, uint32_t>, C8> reads;
+    std::vector<std::string> name_order;                      // dump order (tests)
+    std::vector<std::pair<uint32_t, uint32_t>> read_order;
+    bool empty() const { return names.empty() && reads.empty(); }
+    void set_name(const std::string& n, const Big& v) {
+        if (names.emplace(n, v).second) name_order.push_back(n);
+        else names[n] = v;
+    }
+    void set_read(std::pair<uint32_t, uint32_t> k, const C8& v) {
+        if (reads.emplace(k, v).second) read_order.push_back(k);
+        else reads[k] = v;
+    }
+};
+
+// A least-recently-updated map (Python's OrderedDict with move_to_end on every write and
+// popitem(last=False) to trim) — gpu_check._RECENT_VARS / _RECENT_READS.
+template <class K, class V, class H = std::hash<K>>
+struct Lru {
+    std::list<K> order;
+    std::unordered_map<K, std::pair<typename std::list<K>::iterator, V>, H> m;
+    V& touch(const K& k) {  // get-or-create, moved to the newest end
+        auto it = m.find(k);
+        if (it != m.end()) {
+            order.splice(order.end(), order, it->second.first);
+            return it->second.second;
+        }
+        order.push_back(k);
+        return m.emplace(k, std::make_pair(std::prev(order.end()), V())).first->second.second;
+    }
+    const V* get(const K& k) const {
+        auto it = m.find(k);
+        return it == m.end() ? nullptr : &it->second.second;
+    }
+    void trim(size_t n) {
+        while (m.size() > n) {
+            m.erase(order.front());
+            order.pop_front();
+        }
+    }
+    void clear() {
+        order.clear();
+        m.clear();
+    }
+};
+
+struct PairHash {
+    size_t operator()(const std::pair<uint32_t, uint32_t>& p) const {
+        return std::hash<uint64_t>()(((uint64_t)p.first << 32) | p.second);
+    }
+};
+
+struct Recent {  // newest accepted witness / z3-model values, for parent models
+    Lru<std::string, Big> vars;
+    // per array name: (array id, index id) of a base-array read -> value
+    Lru<std::string, Lru<std::pair<uint32_t, uint32_t>, C8, PairHash>> reads;
+};
+
 struct Store {
     std::vector<TermRec> t;
+    Recent recent;
     // independence keys (smt/independence.py), memoised per term: sorted key ids and the
     // widths whose inverse keccak the term applies to a non-application
     std::vector<int32_t> kmemo;  // term id -> index into keysets (-1: not computed)
@@ -476,10 +541,10 @@ struct Lowering {
     std::vector<std::tuple<uint32_t, uint32_t, int32_t, bool>> power_apps;
     std::vector<std::pair<std::pair<C8, C8>, C8>> power_facts;
     // parents: by symbol name, by (array id, index id)
-    std::unordered_map<std::string, Big> par_name;
-    std::map<std::pair<uint32_t, uint32_t>, C8> par_read;
+    const std::unordered_map<std::string, Big>& par_name;
+    const std::map<std::pair<uint32_t, uint32_t>, C8>& par_read;
 
-    explicit Lowering(const Store& s) : S(s) {}
+    Lowering(const Store& s, const Parents& p) : S(s), par_name(p.names), par_read(p.reads) {}
 
     const TermRec& T(uint32_t id) const { return S.t[id]; }
     uint32_t width(uint32_t id) const { return T(id).sortk == 1 ? T(id).w1 : 0; }
@@ -1197,6 +1262,10 @@ struct Result {
     std::string names;             // variable names, '\0'-separated
     uint32_t n_wregs = 0;
     int n_sat = 0;
+    int rc = 0;                    // 0, or the failure code (-2 LoweringError -> z3, -1 / -3 ...)
+    std::string err;               // the failure message
+    std::vector<uint32_t> in_roots;  // the bucket's conjuncts (the re-check's roots)
+    bool parented = false;         // a parent model seeded some variable
 };
 
 void pack(const Dag& d, std::vector<uint32_t>* nodes, std::vector<uint32_t>* pool) {
@@ -1217,49 +1286,34 @@ void pack(const Dag& d, std::vector<uint32_t>* nodes, std::vector<uint32_t>* poo
     if (nodes->empty()) nodes->assign(8, 0u);
 }
 
-}  // namespace
-
-extern "C" {
-
-void* pflt_store_new(void) { return new Store(); }
-
-void pflt_store_free(void* st) { delete (Store*)st; }
-
-size_t pflt_store_size(void* st) { return ((Store*)st)->t.size(); }
-
-int64_t pflt_add(void* st, uint32_t op, uint32_t sortk, uint32_t w1, uint32_t w2, const uint32_t* args,
-                 uint32_t nargs, int64_t i0, int64_t i1, const uint32_t* limbs, uint32_t nlimbs,
-                 const char* name) {
-    Store* S = (Store*)st;
-    TermRec r;
-    r.op = op;
-    r.sortk = sortk;
-    r.w1 = w1;
-    r.w2 = w2;
-    for (uint32_t i = 0; i < nargs; i++) {
-        if (args[i] >= S->t.size()) {
-            t_err = "pflt_add: argument not in the store";
-            return -1;
-        }
-        r.args.push_back(args[i]);
+// parent values: per name its limb count then the limbs (any width); reads (array id,
+// index id) with 8 limbs each
+void fill_parents(Parents* P, const char* par_names, const uint32_t* par_name_vals, size_t n_par_names,
+                  const uint32_t* par_reads, const uint32_t* par_read_vals, size_t n_par_reads) {
+    const char* nm = par_names;
+    const uint32_t* pv = par_name_vals;
+    for (size_t i = 0; i < n_par_names; i++) {
+        const uint32_t nl = *pv++;
+        P->set_name(std::string(nm), Big(pv, pv + nl));
+        pv += nl;
+        nm += strlen(nm) + 1;
     }
-    r.i0 = i0;
-    r.i1 = i1;
-    if (limbs) r.val.assign(limbs, limbs + nlimbs);
-    if (name) r.name = name;
-    S->t.push_back(std::move(r));
-    return (int64_t)S->t.size() - 1;
+    for (size_t i = 0; i < n_par_reads; i++) {
+        C8 c;
+        memcpy(c.l, par_read_vals + 8 * i, 32);
+        P->set_read(std::make_pair(par_reads[2 * i], par_reads[2 * i + 1]), c);
+    }
 }
 
-void* pflt_lower(void* st, const uint32_t* roots, size_t n_roots, const uint32_t* registry,
-                 size_t n_registry, const char* par_names, const uint32_t* par_name_vals, size_t n_par_names,
-                 const uint32_t* par_reads, const uint32_t* par_read_vals, size_t n_par_reads,
-                 uint32_t flags, uint32_t seed, int* rc_out) {
-    (void)seed;
-    Store* S = (Store*)st;
+// One bucket: terms -> DAG -> hints -> program (pflt_lower).  Reads the store only, so
+// buckets lower concurrently (pflt_lower_many).  Never throws: a failure is R->rc / R->err.
+Result* lower_job(const Store& S, const std::vector<uint32_t>& rs, const Parents& P, const uint32_t* registry,
+                  size_t n_registry, uint32_t flags) {
     Result* R = new Result();
+    R->in_roots = rs;
+    R->parented = !P.empty();
     try {
-        Lowering L(*S);
+        Lowering L(S, P);
         // registry: n_actors, actors x 8; n_specs; per spec: n, has_lo, base x 8, n_concrete,
         // per concrete: value limbs (ceil(n / 32)), digest x 8
         size_t p = 0;
@@ -1289,23 +1343,8 @@ void* pflt_lower(void* st, const uint32_t* roots, size_t n_roots, const uint32_t
             }
             L.kspecs[n] = sp;
         }
-        // parent values by name: per name, its limb count then the limbs (any width)
-        const char* nm = par_names;
-        const uint32_t* pv = par_name_vals;
-        for (size_t i = 0; i < n_par_names; i++) {
-            const uint32_t nl = *pv++;
-            L.par_name.emplace(std::string(nm), Big(pv, pv + nl));
-            pv += nl;
-            nm += strlen(nm) + 1;
-        }
-        for (size_t i = 0; i < n_par_reads; i++) {
-            C8 c;
-            memcpy(c.l, par_read_vals + 8 * i, 32);
-            L.par_read.emplace(std::make_pair(par_reads[2 * i], par_reads[2 * i + 1]), c);
-        }
-        std::vector<uint32_t> rs(roots, roots + n_roots);
         for (uint32_t r : rs)
-            if (r >= S->t.size()) lerr("root not in the store");
+            if (r >= S.t.size()) lerr("root not in the store");
         L.lower(rs);
         R->var_terms = L.var_terms;
         R->uf_apps = L.uf_apps;
@@ -1391,13 +1430,68 @@ void* pflt_lower(void* st, const uint32_t* roots, size_t n_roots, const uint32_t
             R->names.push_back('\0');
         }
         R->dag = std::move(L.d);
-        *rc_out = 0;
+        decltype(R->dag.memo)().swap(R->dag.memo);  // the hash-consing table is done with
         return R;
     } catch (const TermError& e) {
-        *rc_out = e.rc;
+        R->rc = e.rc;
+        R->err = t_err;
+    } catch (const std::exception& e) {
+        R->rc = -1;
+        R->err = std::string("pflt_lower: ") + e.what();
+    }
+    return R;
+}
+
+}  // namespace
+
+extern "C" {
+
+void* pflt_store_new(void) { return new Store(); }
+
+void pflt_store_free(void* st) { delete (Store*)st; }
+
+size_t pflt_store_size(void* st) { return ((Store*)st)->t.size(); }
+
+int64_t pflt_add(void* st, uint32_t op, uint32_t sortk, uint32_t w1, uint32_t w2, const uint32_t* args,
+                 uint32_t nargs, int64_t i0, int64_t i1, const uint32_t* limbs, uint32_t nlimbs,
+                 const char* name) {
+    Store* S = (Store*)st;
+    TermRec r;
+    r.op = op;
+    r.sortk = sortk;
+    r.w1 = w1;
+    r.w2 = w2;
+    for (uint32_t i = 0; i < nargs; i++) {
+        if (args[i] >= S->t.size()) {
+            t_err = "pflt_add: argument not in the store";
+            return -1;
+        }
+        r.args.push_back(args[i]);
+    }
+    r.i0 = i0;
+    r.i1 = i1;
+    if (limbs) r.val.assign(limbs, limbs + nlimbs);
+    if (name) r.name = name;
+    S->t.push_back(std::move(r));
+    return (int64_t)S->t.size() - 1;
+}
+
+void* pflt_lower(void* st, const uint32_t* roots, size_t n_roots, const uint32_t* registry,
+                 size_t n_registry, const char* par_names, const uint32_t* par_name_vals, size_t n_par_names,
+                 const uint32_t* par_reads, const uint32_t* par_read_vals, size_t n_par_reads,
+                 uint32_t flags, uint32_t seed, int* rc_out) {
+    (void)seed;
+    Parents P;
+    fill_parents(&P, par_names, par_name_vals, n_par_names, par_reads, par_read_vals, n_par_reads);
+    Result* R = lower_job(*(const Store*)st, std::vector<uint32_t>(roots, roots + n_roots), P, registry,
+                          n_registry, flags);
+    *rc_out = R->rc;
+    if (R->rc != 0) {
+        t_err = R->err;
         delete R;
         return nullptr;
     }
+    return R;
 }
 
 const char* pflt_last_error(void) { return t_err.c_str(); }
@@ -1593,7 +1687,7 @@ void pflt_result_free(void* res) { delete (Result*)res; }
 
 /* sizes: [0] n_vars, [1] names bytes, [2] n_var_terms, [3] n_uf_apps, [4] n_arrays,
  * [5] n_reads, [6] n_ins, [7] n_const, [8] n_nodes, [9] n_pool, [10] n_roots, [11] n_forced,
- * [12] n_wregs, [13] n_sat */
+ * [12] n_wregs, [13] n_sat, [14] n_in_roots, [15] parented, [16] some variable has a parent value */
 void pflt_result_info(void* res, uint64_t* info) {
     const Result* R = (const Result*)res;
     info[0] = R->dag.vars.size();
@@ -1610,6 +1704,11 @@ void pflt_result_info(void* res, uint64_t* info) {
     info[11] = R->dag.forced.size();
     info[12] = R->n_wregs;
     info[13] = (uint64_t)R->n_sat;
+    info[14] = R->in_roots.size();
+    info[15] = R->parented ? 1u : 0u;
+    bool hp = false;
+    for (const DVar& v : R->dag.vars) hp |= v.has_parent;
+    info[16] = hp ? 1u : 0u;
 }
 
 /* vars: n_vars x 12 u32 = width, kind, hint0, hint1, has_parent, parent x 8 ... (13 words)
@@ -1652,7 +1751,226 @@ void pflt_result_get(void* res, uint32_t which, uint32_t* out, char* names_out) 
         case PFLT_GET_FORCED:
             for (const C8& c : R->dag.forced) out = std::copy(c.l, c.l + 8, out);
             break;
+        case PFLT_GET_IN_ROOTS: std::copy(R->in_roots.begin(), R->in_roots.end(), out); break;
         default: break;
+    }
+}
+
+}  // extern "C"
+
+// ---- batches: parent models, concurrent lowering, batch packing ---------------------------
+namespace {
+
+void note_read(Store* S, uint32_t arr, uint32_t idx, const C8& v) {
+    auto& tab = S->recent.reads.touch(S->t[arr].name);
+    tab.touch({arr, idx}) = v;
+    tab.trim(256);
+}
+
+}  // namespace
+
+extern "C" {
+
+void* pflt_parent_new(const char* names, const uint32_t* name_vals, size_t n_names, const uint32_t* reads,
+                      const uint32_t* read_vals, size_t n_reads) {
+    Parents* P = new Parents();
+    fill_parents(P, names, name_vals, n_names, reads, read_vals, n_reads);
+    return P;
+}
+
+void pflt_parent_free(void* p) { delete (Parents*)p; }
+
+void pflt_parent_info(const void* p, uint64_t* info) {
+    const Parents* P = (const Parents*)p;
+    uint64_t nb = 0, nw = 0;
+    for (const std::string& n : P->name_order) {
+        nb += n.size() + 1;
+        nw += 1 + P->names.at(n).size();
+    }
+    info[0] = P->name_order.size();
+    info[1] = nb;
+    info[2] = nw;
+    info[3] = P->read_order.size();
+}
+
+void pflt_parent_get(const void* p, char* names, uint32_t* name_vals, uint32_t* reads, uint32_t* read_vals) {
+    const Parents* P = (const Parents*)p;
+    for (const std::string& n : P->name_order) {
+        memcpy(names, n.c_str(), n.size() + 1);
+        names += n.size() + 1;
+        const Big& v = P->names.at(n);
+        *name_vals++ = (uint32_t)v.size();
+        name_vals = std::copy(v.begin(), v.end(), name_vals);
+    }
+    for (const auto& k : P->read_order) {
+        *reads++ = k.first;
+        *reads++ = k.second;
+        read_vals = std::copy(P->reads.at(k).l, P->reads.at(k).l + 8, read_vals);
+    }
+}
+
+void pflt_recent_clear(void* st) {
+    Store* S = (Store*)st;
+    S->recent.vars.clear();
+    S->recent.reads.clear();
+}
+
+void pflt_note_vars(void* st, const char* names, const uint32_t* vals, size_t n, size_t recent_size) {
+    Store* S = (Store*)st;
+    for (size_t i = 0; i < n; i++) {
+        const uint32_t nl = *vals++;
+        S->recent.vars.touch(std::string(names)) = Big(vals, vals + nl);
+        vals += nl;
+        names += strlen(names) + 1;
+    }
+    S->recent.vars.trim(recent_size);
+}
+
+void pflt_note_result(void* st, const void* res, const uint32_t* values, size_t recent_size) {
+    Store* S = (Store*)st;
+    const Result* R = (const Result*)res;
+    const size_t n = std::min(R->var_terms.size(), R->dag.vars.size());
+    for (size_t i = 0; i < n; i++) {
+        const VarTerm& vt = R->var_terms[i];
+        const uint32_t* v = values + 8 * i;
+        if (vt.type == PFLT_VT_TERM) {
+            const TermRec& r = S->t[vt.a];
+            if (r.op == PFLT_VAR || r.op == PFLT_BVAR) S->recent.vars.touch(r.name) = Big(v, v + 8);
+        } else if (vt.type == PFLT_VT_SELECT && S->t[vt.a].op == PFLT_ARRAY) {
+            C8 c;
+            memcpy(c.l, v, 32);
+            note_read(S, vt.a, vt.b, c);
+        }
+    }
+    S->recent.vars.trim(recent_size);
+    S->recent.reads.trim(1024);
+}
+
+void* pflt_recent_parent(void* st, const uint32_t* roots, size_t n_roots) {
+    Store* S = (Store*)st;
+    std::vector<uint32_t> keys;
+    for (size_t i = 0; i < n_roots; i++) {
+        if (roots[i] >= S->t.size()) return nullptr;
+        merge_sorted(&keys, S->keysets[dep_keys(S, roots[i])]);
+    }
+    Parents* P = new Parents();
+    for (uint32_t k : keys) {
+        const std::string& nm = S->key_names[k];
+        if (nm.compare(0, 2, "v:") == 0) {
+            if (const Big* v = S->recent.vars.get(nm.substr(2))) P->set_name(nm.substr(2), *v);
+        } else if (nm.compare(0, 2, "a:") == 0) {
+            if (const auto* tab = S->recent.reads.get(nm.substr(2)))
+                for (const auto& rk : tab->order) P->set_read(rk, tab->m.at(rk).second);
+        }
+    }
+    if (P->empty()) {
+        delete P;
+        return nullptr;
+    }
+    return P;
+}
+
+void pflt_lower_many(void* st, const pflt_job* jobs, size_t n, const uint32_t* registry, size_t n_registry,
+                     uint32_t n_threads, void** results) {
+    const Store& S = *(const Store*)st;
+    static const Parents none;
+    auto one = [&](size_t j) {
+        const pflt_job& jb = jobs[j];
+        results[j] = lower_job(S, std::vector<uint32_t>(jb.roots, jb.roots + jb.n_roots),
+                               jb.parents ? *(const Parents*)jb.parents : none, registry, n_registry, jb.flags);
+    };
+    const size_t nt = std::min<size_t>(n_threads ? n_threads : 1, n);
+    if (nt <= 1) {
+        for (size_t j = 0; j < n; j++) one(j);
+        return;
+    }
+    std::atomic<size_t> next{0};
+    std::vector<std::thread> pool;
+    for (size_t t = 0; t < nt; t++)
+        pool.emplace_back([&]() {
+            for (size_t j; (j = next.fetch_add(1)) < n;) one(j);
+        });
+    for (auto& th : pool) th.join();
+}
+
+int pflt_result_status(const void* res) { return ((const Result*)res)->rc; }
+
+const char* pflt_result_error(const void* res) { return ((const Result*)res)->err.c_str(); }
+
+int pflt_result_parented(const void* res) { return ((const Result*)res)->parented ? 1 : 0; }
+
+void pflt_result_shrink(void* res) {
+    Result* R = (Result*)res;
+    std::vector<uint32_t>().swap(R->code);
+    std::vector<uint32_t>().swap(R->consts);
+    std::vector<uint32_t>().swap(R->packed_nodes);
+    std::vector<uint32_t>().swap(R->pool);
+    std::vector<DNode>().swap(R->dag.nodes);
+    std::vector<int32_t>().swap(R->dag.roots);
+    std::vector<C8>().swap(R->dag.forced);
+    decltype(R->dag.var_index)().swap(R->dag.var_index);
+}
+
+void pflt_pack_sizes(void* const* results, size_t n, uint64_t* out) {
+    uint64_t ni = 0, nc = 0, nv = 0, np = 0;
+    for (size_t j = 0; j < n; j++) {
+        const Result* R = (const Result*)results[j];
+        ni += R->code.size() / 4;
+        nc += R->consts.size() / 8;
+        nv += R->dag.vars.size();
+        for (const DVar& v : R->dag.vars) np += v.has_parent ? 1 : 0;
+    }
+    out[0] = ni;
+    out[1] = nc;
+    out[2] = nv;
+    out[3] = np;
+}
+
+void pflt_pack_batch(void* const* results, size_t n, const uint32_t* seeds, const uint32_t* reach_lut,
+                     uint32_t lut_w, uint32_t* code, uint32_t* consts, uint32_t* schema, uint32_t* parents,
+                     uint32_t* descs) {
+    uint32_t oc = 0, ok = 0, ov = 0, op = 0;
+    for (size_t j = 0; j < n; j++) {
+        const Result* R = (const Result*)results[j];
+        const uint32_t ni = (uint32_t)(R->code.size() / 4), nk = (uint32_t)(R->consts.size() / 8),
+                       nv = (uint32_t)R->dag.vars.size();
+        bool has_par = false;
+        for (const DVar& v : R->dag.vars) has_par |= v.has_parent;
+        uint32_t* d = descs + 8 * j;
+        d[0] = oc;
+        d[1] = ni;
+        d[2] = ok;
+        d[3] = nk;
+        d[4] = ov;
+        d[5] = nv;
+        d[6] = seeds[j];
+        d[7] = has_par ? op : PF_NO_PARENT;
+        for (uint32_t i = 0; i < ni; i++) {
+            const uint32_t* w = R->code.data() + 4 * i;
+            uint32_t* o = code + 4 * (size_t)(oc + i);
+            o[0] = w[0];
+            o[1] = w[1];
+            o[2] = w[2];
+            const uint32_t opc = w[0] & 0xffu, wd = (w[0] >> 8) & 0x3ffu;
+            o[3] = wd < lut_w ? reach_lut[(size_t)opc * lut_w + wd] : 0u;
+        }
+        memcpy(consts + 8 * (size_t)ok, R->consts.data(), 4 * R->consts.size());
+        for (uint32_t i = 0; i < nv; i++) {
+            const DVar& v = R->dag.vars[i];
+            uint32_t* s = schema + 4 * (size_t)(ov + i);
+            s[0] = v.kind | (v.width << 8);
+            s[1] = v.hint0;
+            s[2] = v.hint1;
+            s[3] = PF_NO_PARENT;
+            if (has_par && v.has_parent) {
+                s[3] = op;
+                memcpy(parents + 8 * (size_t)op, v.parent.l, 32);
+                op++;
+            }
+        }
+        oc += ni;
+        ok += nk;
+        ov += nv;
     }
 }
 

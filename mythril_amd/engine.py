@@ -153,6 +153,20 @@ class Engine:
             off += k
         return res
 
+    def materialize_limbs(self, db: DeviceBatch, set_ids: Sequence[int], cand_ids: Sequence[int],
+                          seed: int = 0) -> np.ndarray:
+        """materialize() as limbs: the variables of every (set, candidate) pair back to back,
+        one row of 8 little-endian u32 each (rows = sum of the sets' variable counts)."""
+        set_ids = np.ascontiguousarray(set_ids, dtype=np.uint32)
+        cand_ids = np.ascontiguousarray(cand_ids, dtype=np.uint32)
+        total = int(db.batch.descs[set_ids, 5].sum()) if len(set_ids) else 0
+        out = np.zeros(max(total, 1) * LIMBS, dtype=np.uint32)
+        if len(set_ids):
+            _lib.check(_lib.lib().pf_materialize(db.handle, seed, _lib.ptr_u32(set_ids),
+                                                _lib.ptr_u32(cand_ids), len(set_ids),
+                                                _lib.ptr_u32(out)), "pf_materialize")
+        return out[:total * LIMBS].reshape(total, LIMBS)
+
     def eval_assignments(self, db: DeviceBatch, set_id: int, soa: np.ndarray) -> np.ndarray:
         """SAT flag of each explicit candidate; soa is [var][limb][cand] uint32."""
         soa = np.ascontiguousarray(soa, dtype=np.uint32)

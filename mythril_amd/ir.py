@@ -371,6 +371,12 @@ class Batch:
 
     def __init__(self, programs: Sequence[Program]):
         self.programs = list(programs)
+        if self.programs and all(getattr(p, "native_result", None) is not None for p in self.programs):
+            # natively lowered (smt/native_terms.py): packed from the results in C++
+            from .smt.native_terms import pack_batch
+
+            self.code, self.consts, self.schema, self.parents, self.descs = pack_batch(self.programs)
+            return
         code, consts, schema, parents, descs = [], [], [], [], []
         packed = []   # (offset in code, words) of natively lowered programs
         for p in self.programs:
@@ -427,8 +433,8 @@ class Batch:
 _REACH_LUT = None
 
 
-def _reach_cost_words(words: np.ndarray) -> np.ndarray:
-    """reach_cost of packed instructions, vectorised: a (op, width) lookup table."""
+def reach_lut() -> np.ndarray:
+    """reach_cost by (op, width): a 256 x 1024 u32 table."""
     global _REACH_LUT
     if _REACH_LUT is None:
         lut = np.zeros((256, 1024), dtype=np.uint32)
@@ -436,9 +442,14 @@ def _reach_cost_words(words: np.ndarray) -> np.ndarray:
             for w in range(1, MAX_WIDTH + 1):
                 lut[op, w] = reach_cost(op, w)
         _REACH_LUT = lut
+    return _REACH_LUT
+
+
+def _reach_cost_words(words: np.ndarray) -> np.ndarray:
+    """reach_cost of packed instructions, vectorised: a (op, width) lookup table."""
     op = words[:, 0] & 0xFF
     w = (words[:, 0] >> 8) & 0x3FF
-    return _REACH_LUT[op, w]
+    return reach_lut()[op, w]
 
 
 def pack_assignments(prog: Program, cands: Sequence[Sequence[int]]) -> np.ndarray:

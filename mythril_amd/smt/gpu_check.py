@@ -25,6 +25,8 @@ from collections import OrderedDict
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
+import numpy as np
+
 from .. import ir, seed
 from ..lower import LoweringError, lower
 from .independence import buckets
@@ -105,6 +107,10 @@ def reset_cache() -> None:
         _NEG.clear()
         _RECENT_VARS.clear()
         _RECENT_READS.clear()
+        if _native_batch():
+            from . import native_terms
+
+            native_terms.recent_clear()
 
 
 def _neg_key(key: tuple, cfg: GpuConfig) -> tuple:
@@ -123,10 +129,20 @@ def note_values(vals: Dict[str, int], cfg: Optional[GpuConfig] = None) -> None:
             _RECENT_VARS.move_to_end(k)
         while len(_RECENT_VARS) > cfg.recent_size:
             _RECENT_VARS.popitem(last=False)
+        if _native_batch():
+            from . import native_terms
+
+            native_terms.note_vars(vals, cfg.recent_size)
 
 
 def _note_witness(lo: Lowered, values: List[int], cfg: GpuConfig) -> None:
     """Record an accepted bucket witness's variable values (caller holds _lock)."""
+    if getattr(lo, "res", None) is not None:
+        # a native witness: the store's recent tables (pflt_note_result, the same updates)
+        from . import native_terms
+
+        native_terms.note_result(lo, values, cfg.recent_size)
+        return
     for term, val in zip(lo.var_terms, values):
         if term.op in ("var", "bvar"):
             _RECENT_VARS[term.val] = val
@@ -153,6 +169,17 @@ def _recent_parent(bucket: List[T.Term]) -> Optional[dict]:
     query is the same key)."""
     from .independence import dependence_keys
 
+    if _native_batch():
+        from . import native_terms
+
+        h = native_terms.recent_parent_handle(bucket)
+        if h is None:
+            return None
+        try:
+            return native_terms.parent_dict(h)
+        finally:
+            native_terms.free_parent(h)
+
     keys = set()
     for c in bucket:
         keys |= dependence_keys(c)
@@ -170,6 +197,19 @@ def _recent_parent(bucket: List[T.Term]) -> Optional[dict]:
     return out or None
 
 
+def _values(v) -> List[int]:
+    """A witness's values as ints (the native pipeline keeps them as limb rows)."""
+    if isinstance(v, np.ndarray):
+        from . import native_terms
+
+        return native_terms.ints_of(v)
+    return v
+
+
+def _union_thunk(parts, reg: UFRegistry):
+    return lambda: Witness.union([Witness(lo, _values(v), reg) for lo, v in parts], reg)
+
+
 def _set_seed(constraints: Sequence[T.Term]) -> int:
     h = 0
     for c in constraints:
@@ -178,6 +218,16 @@ def _set_seed(constraints: Sequence[T.Term]) -> int:
 
 
 _NATIVE_TERMS = os.environ.get("PF_NATIVE_TERMS", "1") != "0"
+
+
+def _native_batch() -> bool:
+    """check_sets' native pipeline (libpflower.so batch entry points): buckets lowered on
+    host threads, packed, re-checked and recorded in C++ — no Python term decoding."""
+    if not _NATIVE_TERMS:
+        return False
+    from . import native_terms
+
+    return native_terms.batch_api() is not None
 
 
 def _lower_bucket(bucket: List[T.Term], reg: UFRegistry, parent: Optional[dict], hints: bool):
@@ -255,7 +305,7 @@ def warm_pool(cfg: Optional[GpuConfig] = None) -> int:
     latency-sensitive caller can do it up front).  Returns the worker count."""
     cfg = cfg or CONFIG
     n = max(1, cfg.workers)
-    if n > 1:
+    if n > 1 and not _native_batch():   # the native pipeline lowers on host threads instead
         _pool(n).map(_warm, range(n), chunksize=1)
     return n
 
@@ -302,6 +352,9 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
     # cached witness is only valid for the registry state it was found under
     reg_sig = tuple(sorted((n, s.lo, len(s.concrete)) for n, s in reg.keccak.items()))
     jobs, job_keys, pending = [], [], set()
+    nat = _native_batch()
+    if nat:
+        from . import native_terms
     phases: Dict[str, float] = {}
     tp = [t0]
 
@@ -343,15 +396,37 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
                 hits += 1
                 continue
             pending.add(key)
-            bp = parent if parent is not None else (_recent_parent(b) if cfg.parents else None)
+            if nat:
+                # parent handles: the caller's model, or the store's recent values now (cache
+                # hits above recorded theirs first, as _note_witness does)
+                if parent is not None:
+                    with native_terms.store().lock:
+                        bp = (native_terms._parent_handle(native_terms.store(), parent), bool(parent))
+                elif cfg.parents:
+                    h = native_terms.recent_parent_handle(b)
+                    bp = (h, h is not None)
+                else:
+                    bp = (None, False)
+            else:
+                bp = parent if parent is not None else (_recent_parent(b) if cfg.parents else None)
             jobs.append((b, bp))
             job_keys.append(key)
         set_buckets.append(ks)
     lap("bucket")
     failed = set()
     parented: List[bool] = []
-    job_parent = {k: bool(j[1]) for k, j in zip(job_keys, jobs)}
-    lowered_all = _lower_all(jobs, reg, cfg)
+    if nat:
+        job_parent = {k: j[1][1] for k, j in zip(job_keys, jobs)}
+        try:
+            lowered_all = native_terms.lower_many(
+                [(b, h) for b, (h, _) in jobs], reg, cfg.hints, [_set_seed(b) for b, _ in jobs],
+                cfg.workers if len(jobs) >= 8 else 1)
+        finally:
+            for _, (h, _) in jobs:
+                native_terms.free_parent(h)
+    else:
+        job_parent = {k: bool(j[1]) for k, j in zip(job_keys, jobs)}
+        lowered_all = _lower_all(jobs, reg, cfg)
     lap("lower")
     for key, (lo, prog, err) in zip(job_keys, lowered_all):
         if err is not None:
@@ -386,16 +461,35 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
         sat = [k for k in range(len(progs)) if res.found[k] != 0xFFFFFFFF]
         vals_of = {}
         base = 0
+        limb_rows = []   # native: the witnesses' variables as limbs, in `sat` order
         for db in dbs:
             mine = [k for k in sat if base <= k < base + len(db)]
             if mine:
-                got = eng.materialize(db, [k - base for k in mine], [int(res.found[k]) for k in mine],
-                                      seed=cfg.seed)
-                vals_of.update(zip(mine, got))
+                sids, cids = [k - base for k in mine], [int(res.found[k]) for k in mine]
+                if nat:
+                    if hasattr(eng, "materialize_limbs"):
+                        rows = eng.materialize_limbs(db, sids, cids, seed=cfg.seed)
+                    else:
+                        rows = ir.limbs_array([x for vs in eng.materialize(db, sids, cids, seed=cfg.seed)
+                                               for x in vs])
+                    limb_rows.append(rows)
+                    o = 0
+                    for k in mine:
+                        nv = int(db.batch.descs[k - base][5])
+                        vals_of[k] = rows[o:o + nv]
+                        o += nv
+                else:
+                    got = eng.materialize(db, sids, cids, seed=cfg.seed)
+                    vals_of.update(zip(mine, got))
             base += len(db)
             db.free()
         vals = [vals_of[k] for k in sat]
         lap("materialize")
+        status = None
+        if nat and sat:
+            # the host re-check of every witness at once, on host threads (pflt_recheck_many)
+            status = native_terms.recheck_many([lows[k] for k in sat], np.concatenate(limb_rows), reg,
+                                               cfg.workers if len(sat) >= 8 else 1)
         for k in range(len(progs)):
             found[keys[k]] = None
         if not res.timed_out:  # a deadline-cut search is not a complete answer
@@ -406,7 +500,7 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
                         _NEG[_neg_key(keys[k], cfg)] = None
                 while len(_NEG) > cfg.cache_size:
                     _NEG.popitem(last=False)
-        for k, v in zip(sat, vals):
+        for j, (k, v) in enumerate(zip(sat, vals)):
             key = keys[k]
             # provenance of the witness: candidate 0 of a hinted program is the host's
             # constraint-directed hint model itself; any other index was found by the search
@@ -415,7 +509,12 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
             # re-check on the host under the same interpretation before trusting it:
             # natively (pflt_recheck, the Witness interpretation bit for bit) when built
             ok = None
-            if _NATIVE_TERMS:
+            if status is not None:
+                st_j = int(status[j])
+                ok = None if st_j < 0 else bool(st_j)
+                if ok is None:
+                    v = native_terms.ints_of(v)
+            elif _NATIVE_TERMS:
                 from . import native_terms
 
                 ok = native_terms.recheck(list(key[0]), lows[k], v, reg)
@@ -427,7 +526,8 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
                 # or interpretation bug — sound (the bucket stays unanswered), but counted
                 with _lock:
                     STATS.recheck_failures += 1
-                    _RECHECK_DEBUG.append((key[0], lows[k], v, progs[k], int(res.found[k])))
+                    prog = progs[k].decode() if hasattr(progs[k], "decode") else progs[k]
+                    _RECHECK_DEBUG.append((key[0], lows[k], v, prog, int(res.found[k])))
                     del _RECHECK_DEBUG[:-8]
             else:
                 found[key] = (lows[k], v)
@@ -436,6 +536,9 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
                     while len(_CACHE) > cfg.cache_size:
                         _CACHE.popitem(last=False)
                     _note_witness(lows[k], v, cfg)
+        if nat:
+            for lo in lows:   # programs are uploaded: keep only the witness metadata
+                native_terms.shrink(lo)
         lap("recheck")
 
     n_sat = 0
@@ -447,10 +550,12 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
             continue
         cs = [c for c in sets[i] if c is not T.TRUE]
         # buckets() partitions every conjunct of the set: each bucket's witness was
-        # re-checked on exactly its conjuncts above (or when it entered the cache)
-        w = Witness.union([Witness(lo, v, reg) for lo, v in parts], reg)
+        # re-checked on exactly its conjuncts above (or when it entered the cache), so the
+        # model's interpretation is only built when it is first read
+        w = _union_thunk(parts, reg)
         ok = True
         if cfg.recheck_union and len(parts) > 1:
+            w = w()
             ok = all(w.ev(c) for c in cs)
         if ok:
             out[i] = WitnessModel(w, list(sets[i]))

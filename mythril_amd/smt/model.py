@@ -101,10 +101,18 @@ def _as_value(t: T.Term, v):
 class WitnessModel:
     """Internal model of a GPU witness (one per satisfied set)."""
 
-    def __init__(self, witness: Witness, constraints: List[T.Term]):
-        self.w = witness
+    def __init__(self, witness, constraints: List[T.Term]):
+        # a Witness, or a function building it: check_sets defers decoding the native
+        # lowering's metadata until a model is first read
+        self._w = witness
         self.constraints = constraints
         self.origin = "search"   # set by check_sets: "hint" / "first" / "search" / "cache"
+
+    @property
+    def w(self) -> Witness:
+        if not hasattr(self._w, "ev"):
+            self._w = self._w()
+        return self._w
 
     def decls(self) -> List[Decl]:
         out: List[Decl] = []

@@ -36,7 +36,7 @@ _OPS = {
 OTHER = 99
 HINTS, PROGRAM = 1, 2
 GET_VARS, GET_VAR_TERMS, GET_UF_APPS, GET_READS, GET_CODE, GET_CONSTS, GET_NODES, GET_POOL, \
-    GET_ROOTS, GET_FORCED = range(10)
+    GET_ROOTS, GET_FORCED, GET_IN_ROOTS = range(11)
 VT_TERM, VT_SELECT, VT_EXTRACT = 0, 1, 2
 
 _u32p = ctypes.POINTER(ctypes.c_uint32)
@@ -84,6 +84,27 @@ def _bind(L):
     L.pflt_result_free.argtypes = [ctypes.c_void_p]
     L.pflt_result_info.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]
     L.pflt_result_get.argtypes = [ctypes.c_void_p, ctypes.c_uint32, _u32p, ctypes.c_char_p]
+    if hasattr(L, "pflt_lower_many"):
+        vp, sz, u32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32
+        L.pflt_parent_new.restype = vp
+        L.pflt_parent_new.argtypes = [ctypes.c_char_p, _u32p, sz, _u32p, _u32p, sz]
+        L.pflt_parent_free.argtypes = [vp]
+        L.pflt_parent_info.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
+        L.pflt_parent_get.argtypes = [vp, ctypes.c_char_p, _u32p, _u32p, _u32p]
+        L.pflt_recent_clear.argtypes = [vp]
+        L.pflt_note_vars.argtypes = [vp, ctypes.c_char_p, _u32p, sz, sz]
+        L.pflt_note_result.argtypes = [vp, vp, _u32p, sz]
+        L.pflt_recent_parent.restype = vp
+        L.pflt_recent_parent.argtypes = [vp, _u32p, sz]
+        L.pflt_lower_many.argtypes = [vp, vp, sz, _u32p, sz, u32, ctypes.POINTER(vp)]
+        L.pflt_result_status.argtypes = [vp]
+        L.pflt_result_error.restype = ctypes.c_char_p
+        L.pflt_result_error.argtypes = [vp]
+        L.pflt_result_shrink.argtypes = [vp]
+        L.pflt_pack_sizes.argtypes = [ctypes.POINTER(vp), sz, ctypes.POINTER(ctypes.c_uint64)]
+        L.pflt_pack_batch.argtypes = [ctypes.POINTER(vp), sz, _u32p, _u32p, u32, _u32p, _u32p, _u32p, _u32p, _u32p]
+        L.pflt_recheck_many.argtypes = [vp, ctypes.POINTER(vp), sz, _u32p, _u32p, sz, u32,
+                                        ctypes.POINTER(ctypes.c_int8)]
     _SIGNED = True
 
 
@@ -205,7 +226,7 @@ class _Result:
 
     def __init__(self, st: TermStore, h):
         self.st, self.h = st, h
-        info = (ctypes.c_uint64 * 14)()
+        info = (ctypes.c_uint64 * 17)()
         st.L.pflt_result_info(h, info)
         self.info = [int(x) for x in info]
 
@@ -397,3 +418,245 @@ def buckets(constraints: List[T.Term]) -> Optional[List[List[T.Term]]]:
             out.append([terms[i] for i in idl[o:o + n]])
             o += n
         return out
+
+
+# ---- batches: parent models, concurrent lowering, native batch packing and re-check ---------
+# (include/pf_lower.h "batches"; gpu_check.check_sets' native pipeline)
+
+def batch_api() -> Optional[TermStore]:
+    """The store when libpflower.so has the batch entry points, else None."""
+    st = store()
+    return st if st is not None and hasattr(st.L, "pflt_lower_many") else None
+
+
+class NativeLowered:
+    """to_dag.Lowered of a native result (the witness metadata), decoded on first use:
+    check_sets re-checks and records witnesses natively, so most buckets never need it."""
+
+    dag = None
+
+    def __init__(self, res: "_Result"):
+        self.res = res
+        self._lo: Optional[Lowered] = None
+
+    def _get(self) -> Lowered:
+        if self._lo is None:
+            self._lo = self.res.lowered()
+        return self._lo
+
+    var_terms = property(lambda self: self._get().var_terms)
+    uf_apps = property(lambda self: self._get().uf_apps)
+    array_reads = property(lambda self: self._get().array_reads)
+
+
+class NativeProgram(ir.PackedProgram):
+    """ir.PackedProgram of a native result: the batch is packed natively from the result
+    (pack_batch); instructions, constants and variables are decoded only when read."""
+
+    def __init__(self, res: "_Result", seed: int):
+        self.native_result = res
+        self.seed = seed
+        self.name = ""
+        self._code = None
+        self._words = self._consts = self._vars = None
+
+    @property
+    def words(self):
+        if self._words is None:
+            self._words = self.native_result.get(GET_CODE, self.native_result.info[6], 4).copy()
+        return self._words
+
+    @property
+    def consts(self):
+        if self._consts is None:
+            nc = self.native_result.info[7]
+            raw = self.native_result.get(GET_CONSTS, nc, 8).astype("<u4").tobytes()
+            self._consts = [int.from_bytes(raw[32 * i:32 * i + 32], "little") for i in range(nc)]
+        return self._consts
+
+    @property
+    def vars(self):
+        if self._vars is None:
+            self._vars = self.native_result.variables()
+        return self._vars
+
+    @property
+    def has_parent(self) -> bool:
+        return bool(self.native_result.info[16])
+
+    def decode(self) -> "NativeProgram":
+        """Read everything now (before pflt_result_shrink frees the tables)."""
+        self.words, self.consts, self.vars  # noqa: B018
+        return self
+
+
+def _parent_handle(st: TermStore, parent: dict):
+    pn, pnv, npn, pr, prv, npr = _parent_args(st, parent)
+    return st.L.pflt_parent_new(pn, pnv.ctypes.data_as(_u32p), npn, pr.ctypes.data_as(_u32p),
+                                prv.ctypes.data_as(_u32p), npr)
+
+
+def recent_parent_handle(bucket: List[T.Term]):
+    """The bucket's parent model from the store's recent values (pflt_recent_parent), as a
+    handle for lower_many, or None when no value is known (gpu_check._recent_parent)."""
+    st = batch_api()
+    with st.lock:
+        roots = np.array([st.export(c) for c in bucket] or [0], dtype=np.uint32)
+        return st.L.pflt_recent_parent(st.h, roots.ctypes.data_as(_u32p), len(bucket)) or None
+
+
+def parent_dict(h) -> dict:
+    """A parent handle as gpu_check's parent dict (names -> value, select term -> value)."""
+    st = batch_api()
+    info = (ctypes.c_uint64 * 4)()
+    st.L.pflt_parent_info(h, info)
+    nn, nb, nw, nr = (int(x) for x in info)
+    names = ctypes.create_string_buffer(max(nb, 1))
+    nv = np.zeros(max(nw, 1), dtype=np.uint32)
+    rd = np.zeros(max(2 * nr, 1), dtype=np.uint32)
+    rv = np.zeros(max(8 * nr, 1), dtype=np.uint32)
+    st.L.pflt_parent_get(h, names, nv.ctypes.data_as(_u32p), rd.ctypes.data_as(_u32p), rv.ctypes.data_as(_u32p))
+    out: dict = {}
+    labels = names.raw[:nb].split(b"\0")[:nn]
+    o = 0
+    for lab in labels:
+        k = int(nv[o])
+        out[lab.decode()] = _int_of(nv[o + 1:o + 1 + k])
+        o += 1 + k
+    for i in range(nr):
+        out[T.select(st.terms[int(rd[2 * i])], st.terms[int(rd[2 * i + 1])])] = _int_of(rv[8 * i:8 * i + 8])
+    return out
+
+
+def free_parent(h) -> None:
+    if h:
+        batch_api().L.pflt_parent_free(h)
+
+
+def note_vars(vals: Dict[str, int], recent_size: int) -> None:
+    st = batch_api()
+    if st is None:
+        return
+    names, words = [], []
+    for k, v in vals.items():
+        if v is None:
+            continue
+        names.append(k.encode())
+        ls = _limbs_of(int(v))
+        words += [len(ls)] + ls
+    if names:
+        w = np.array(words, dtype=np.uint32)
+        st.L.pflt_note_vars(st.h, b"\0".join(names) + b"\0", w.ctypes.data_as(_u32p), len(names), recent_size)
+
+
+def note_result(lo: NativeLowered, limbs: np.ndarray, recent_size: int) -> None:
+    st = batch_api()
+    if not isinstance(limbs, np.ndarray):
+        limbs = ir.limbs_array([int(x or 0) for x in limbs])
+    v = np.ascontiguousarray(limbs, dtype=np.uint32)
+    if v.size == 0:
+        v = np.zeros(8, dtype=np.uint32)
+    st.L.pflt_note_result(st.h, lo.res.h, v.ctypes.data_as(_u32p), recent_size)
+
+
+def recent_clear() -> None:
+    st = batch_api()
+    if st is not None:
+        st.L.pflt_recent_clear(st.h)
+
+
+# pflt_job (include/pf_lower.h): roots pointer, n_roots, parents handle, flags, seed
+_JOB = np.dtype([("roots", "<u8"), ("n", "<u8"), ("parents", "<u8"), ("flags", "<u4"), ("seed", "<u4")])
+
+
+def lower_many(jobs: List[Tuple[List[T.Term], object]], reg: UFRegistry, hints: bool, seeds: List[int],
+               threads: int) -> list:
+    """[(bucket, parent handle or None)] -> [(NativeLowered, NativeProgram, None) or
+    (None, None, error)], lowered concurrently on ``threads`` host threads."""
+    st = batch_api()
+    n = len(jobs)
+    if n == 0:
+        return []
+    with st.lock:
+        ex = st.export
+        flat: List[int] = []
+        offs = np.zeros(n, dtype=np.uint64)
+        lens = np.zeros(n, dtype=np.uint64)
+        for j, (b, _) in enumerate(jobs):
+            offs[j] = len(flat)
+            lens[j] = len(b)
+            flat += [ex(c) for c in b]
+        roots = np.array(flat or [0], dtype=np.uint32)
+        arr = np.zeros(n, dtype=_JOB)
+        arr["roots"] = roots.ctypes.data + 4 * offs
+        arr["n"] = lens
+        arr["parents"] = [h or 0 for _, h in jobs]
+        arr["flags"] = PROGRAM | (HINTS if hints else 0)
+        arr["seed"] = np.array(seeds, dtype=np.uint64) & 0xFFFFFFFF
+        regb = _registry_blob(reg)
+        res = (ctypes.c_void_p * n)()
+        st.L.pflt_lower_many(st.h, arr.ctypes.data, n, regb.ctypes.data_as(_u32p), len(regb),
+                             max(1, threads), res)
+    out = []
+    for j in range(n):
+        h = res[j]
+        rc = st.L.pflt_result_status(h)
+        if rc != 0:
+            msg = st.L.pflt_result_error(h).decode(errors="replace")
+            st.L.pflt_result_free(h)
+            out.append((None, None, msg if rc == -2 else f"ValueError: pflt_lower failed ({rc}): {msg}"))
+            continue
+        r = _Result(st, h)
+        out.append((NativeLowered(r), NativeProgram(r, seeds[j]), None))
+    return out
+
+
+def pack_batch(programs: List[NativeProgram]):
+    """ir.Batch's arrays (code, consts, schema, parents, descs) packed natively."""
+    st = batch_api()
+    n = len(programs)
+    hs = (ctypes.c_void_p * n)(*[p.native_result.h for p in programs])
+    sz = (ctypes.c_uint64 * 4)()
+    st.L.pflt_pack_sizes(hs, n, sz)
+    ni, nc, nv, np_ = (int(x) for x in sz)
+    code = np.zeros((max(ni, 1), 4), dtype=np.uint32)
+    consts = np.zeros((max(nc, 1), 8), dtype=np.uint32)
+    schema = np.zeros((max(nv, 1), 4), dtype=np.uint32)
+    parents = np.zeros((max(np_, 1), 8), dtype=np.uint32)
+    descs = np.zeros((max(n, 1), 8), dtype=np.uint32)
+    seeds = np.array([p.seed & 0xFFFFFFFF for p in programs] or [0], dtype=np.uint32)
+    lut = ir.reach_lut()
+    st.L.pflt_pack_batch(hs, n, seeds.ctypes.data_as(_u32p), lut.ctypes.data_as(_u32p), lut.shape[1],
+                         code.ctypes.data_as(_u32p), consts.ctypes.data_as(_u32p), schema.ctypes.data_as(_u32p),
+                         parents.ctypes.data_as(_u32p), descs.ctypes.data_as(_u32p))
+    return code[:ni], consts[:nc], schema[:nv], parents[:np_], descs[:n]
+
+
+def recheck_many(los: List[NativeLowered], limbs: np.ndarray, reg: UFRegistry, threads: int) -> np.ndarray:
+    """Status per bucket witness: 1 every conjunct true, 0 some false, -1 not evaluable
+    natively (re-check in Python).  limbs = the witnesses' variables back to back."""
+    st = batch_api()
+    n = len(los)
+    if n == 0:
+        return np.zeros(0, dtype=np.int8)
+    hs = (ctypes.c_void_p * n)(*[lo.res.h for lo in los])
+    v = np.ascontiguousarray(limbs, dtype=np.uint32).reshape(-1)
+    if v.size == 0:
+        v = np.zeros(8, dtype=np.uint32)
+    regb = _registry_blob(reg)
+    status = np.zeros(n, dtype=np.int8)
+    st.L.pflt_recheck_many(st.h, hs, n, v.ctypes.data_as(_u32p), regb.ctypes.data_as(_u32p), len(regb),
+                           max(1, threads), status.ctypes.data_as(ctypes.POINTER(ctypes.c_int8)))
+    return status
+
+
+def shrink(lo: NativeLowered) -> None:
+    """Free the program tables of a result whose program was uploaded (the cache keeps it)."""
+    st = batch_api()
+    st.L.pflt_result_shrink(lo.res.h)
+
+
+def ints_of(limbs: np.ndarray) -> List[int]:
+    """Rows of 8 u32 limbs -> ints."""
+    raw = np.ascontiguousarray(limbs, dtype="<u4").tobytes()
+    return [int.from_bytes(raw[32 * i:32 * i + 32], "little") for i in range(len(raw) // 32)]
