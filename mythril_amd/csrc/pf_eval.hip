@@ -87,10 +87,28 @@ namespace {
 // Narrow kernels: the register file is PF_NW_NARROW x 8 plain scalars, every access a
 // static index under a uniform switch over the register number, so each limb is its own
 // VGPR (no 16-dword vector tuples, no write sink): 56 VGPRs for 7 registers.
+// The operand copy is one asm block per case: as plain assignments, the phi copies of a
+// case were placed before the compare that leaves it (critical edges are not split), so a
+// read of register 2 executed the copies of registers 0, 1 and 2 (24 v_mov, ~14 on average
+// over the register mix instead of 8).  Early-clobber outputs: the moves run in order.
+#ifndef PF_RD_PLAIN
+#define PF_MOV8(d, s)                                                                        \
+    asm("v_mov_b32 %0, %8\n\tv_mov_b32 %1, %9\n\tv_mov_b32 %2, %10\n\tv_mov_b32 %3, %11\n\t"     \
+        "v_mov_b32 %4, %12\n\tv_mov_b32 %5, %13\n\tv_mov_b32 %6, %14\n\tv_mov_b32 %7, %15"          \
+        : "=&v"((d).l[0]), "=&v"((d).l[1]), "=&v"((d).l[2]), "=&v"((d).l[3]), "=&v"((d).l[4]),     \
+          "=&v"((d).l[5]), "=&v"((d).l[6]), "=&v"((d).l[7])                                      \
+        : "v"((s)[0]), "v"((s)[1]), "v"((s)[2]), "v"((s)[3]), "v"((s)[4]), "v"((s)[5]),           \
+          "v"((s)[6]), "v"((s)[7]))
+#define RDN_CASE(dst, W, R)                                                                \
+    case R:                                                                               \
+        PF_MOV8(dst, (W)[R]);                                                             \
+        break;
+#else
 #define RDN_CASE(dst, W, R)                                                                \
     case R:                                                                               \
         _Pragma("unroll") for (int k_ = 0; k_ < 8; k_++)(dst).l[k_] = (W)[R][k_];          \
         break;
+#endif
 #define WRN_CASE(W, R, src)                                                                \
     case R:                                                                               \
         _Pragma("unroll") for (int k_ = 0; k_ < 8; k_++)(W)[R][k_] = (src).l[k_];          \
