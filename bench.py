@@ -156,11 +156,16 @@ def discharge(args):
     sample = [q for q in c.queries if q.label == "sat"][:96]
     lat = []
     gpu_check.STATS.phase_s.clear()
+    slowest = (0.0, {})
     for q in sample:
         gpu_check.reset_cache()
+        before = dict(gpu_check.STATS.phase_s)
         ts = time.perf_counter()
         gpu_check.check_sets([q.constraints], registry=c.kfm.registry)
         lat.append(1e3 * (time.perf_counter() - ts))
+        if lat[-1] > slowest[0]:
+            slowest = (lat[-1], {k: round(1e3 * (v - before.get(k, 0.0)), 3)
+                                 for k, v in gpu_check.STATS.phase_s.items()})
     sq_phase = {k: round(1e3 * v / max(len(lat), 1), 3) for k, v in gpu_check.STATS.phase_s.items()}
     gpu_check.reset_cache()
     return {"population": "builder corpus (mythril_amd/corpus.py), not BASELINE's "
@@ -189,7 +194,7 @@ def discharge(args):
                                 "mean": float(np.mean(lat)) if lat else None,
                                 "p95": float(np.percentile(lat, 95)) if lat else None,
                                 "max": float(np.max(lat)) if lat else None, "queries": len(lat),
-                                "phase_mean_ms": sq_phase},
+                                "phase_mean_ms": sq_phase, "max_phase_ms": slowest[1]},
             "buckets_searched": stats_batch[0], "kernel_ms": stats_batch[1], "host_s": stats_batch[2],
             "phase_s": phase_s, "lowering_workers": n_workers, "pool_start_s": round(t_pool, 3),
             "wall_s": t2 - t1, "corpus_build_s": t1 - t0,

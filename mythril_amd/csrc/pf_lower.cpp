@@ -90,14 +90,28 @@ class Lowerer {
 
     void run(const uint32_t* roots, size_t n_roots) {
         order(roots, n_roots);
-        uses.assign(nn, {});
-        for (size_t t = 0; t < events.size(); ++t) {
-            const auto& e = events[t];
+        // use times per node, ascending (CSR: counted, then filled in event order)
+        use_off.assign(nn + 1, 0);
+        for (const auto& e : events) {
             if (!e.first) {
                 const Node& n = N[e.second];
-                for (uint32_t k = 0; k < n.nargs; ++k) uses[n.args[k]].push_back((int)t);
+                for (uint32_t k = 0; k < n.nargs; ++k) use_off[n.args[k] + 1]++;
             } else {
-                uses[e.second].push_back((int)t);
+                use_off[e.second + 1]++;
+            }
+        }
+        for (size_t i = 0; i < nn; ++i) use_off[i + 1] += use_off[i];
+        use_at.assign(use_off[nn], 0);
+        {
+            std::vector<int> fill(use_off.begin(), use_off.end() - 1);
+            for (size_t t = 0; t < events.size(); ++t) {
+                const auto& e = events[t];
+                if (!e.first) {
+                    const Node& n = N[e.second];
+                    for (uint32_t k = 0; k < n.nargs; ++k) use_at[fill[n.args[k]]++] = (int)t;
+                } else {
+                    use_at[fill[e.second]++] = (int)t;
+                }
             }
         }
         for (size_t t = 0; t < events.size(); ++t) {
@@ -121,7 +135,7 @@ class Lowerer {
     const Const8* pool;
     size_t n_pool;
     std::vector<std::pair<bool, int>> events;  // (is_assert, node)
-    std::vector<std::vector<int>> uses;
+    std::vector<int> use_off, use_at;  // uses of node i: use_at[use_off[i] .. use_off[i + 1])
     std::vector<int> where, slot_of, remat, cost, free_slots;
     RegFile W, B;
 
@@ -151,19 +165,32 @@ class Lowerer {
                 }
                 if (seen[i]) continue;
                 stack.push_back({i, true});
-                std::vector<int> args(n.args, n.args + n.nargs);
-                std::stable_sort(args.begin(), args.end(), [&](int a, int b) { return size[a] < size[b]; });
-                for (int a : args)
+                // operands by subtree size, stable (insertion sort over <= 3)
+                int args[3];
+                const uint32_t na = n.nargs;
+                for (uint32_t k = 0; k < na; ++k) {
+                    const int a = (int)n.args[k];
+                    uint32_t j = k;
+                    while (j > 0 && size[args[j - 1]] > size[a]) {
+                        args[j] = args[j - 1];
+                        --j;
+                    }
+                    args[j] = a;
+                }
+                for (uint32_t k = 0; k < na; ++k) {
+                    const int a = args[k];
                     if (!is_leaf(N[a].kind) && !seen[a]) stack.push_back({a, false});
+                }
             }
             events.push_back({true, (int)roots[ri]});
         }
     }
 
     int next_use(int nd, int now) const {
-        const auto& l = uses[nd];
-        auto it = std::upper_bound(l.begin(), l.end(), now);
-        return it == l.end() ? INF : *it;
+        const int* b = use_at.data() + use_off[nd];
+        const int* e = use_at.data() + use_off[nd + 1];
+        const int* it = std::upper_bound(b, e, now);
+        return it == e ? INF : *it;
     }
 
     int remat_size(int nd) {  // NONE = must stay resident
