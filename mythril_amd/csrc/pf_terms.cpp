@@ -973,13 +973,56 @@ struct Lowering {
     }
 
     // ---- arrays -----------------------------------------------------------------------
+    // (base, c) with t = base + c mod 2^w, constant additions / subtractions peeled off
+    // (base NO_BASE for a constant): TermLowering._offset_form — indices with one base and
+    // different offsets never alias
+    static constexpr uint32_t NO_BASE = 0xffffffffu;
+    std::pair<uint32_t, C8> offset_form(uint32_t t) const {
+        const uint32_t w = width(t);
+        uint32_t c[8] = {0};
+        auto addsub = [&](const Big& v, bool sub) {
+            const C8 x = c8_of(v, 256);
+            uint64_t carry = sub ? 1 : 0;
+            for (int i = 0; i < 8; i++) {
+                const uint64_t s = (uint64_t)c[i] + (sub ? (uint32_t)~x.l[i] : x.l[i]) + carry;
+                c[i] = (uint32_t)s;
+                carry = s >> 32;
+            }
+        };
+        for (;;) {
+            const TermRec& r = T(t);
+            if (r.op == T_BV) {
+                addsub(r.val, false);
+                return {NO_BASE, c8_of(Big(c, c + 8), w)};
+            }
+            if (r.op == PFLT_BVADD && r.args.size() == 2) {
+                if (T(r.args[1]).op == T_BV) {
+                    addsub(T(r.args[1]).val, false);
+                    t = r.args[0];
+                    continue;
+                }
+                if (T(r.args[0]).op == T_BV) {
+                    addsub(T(r.args[0]).val, false);
+                    t = r.args[1];
+                    continue;
+                }
+            } else if (r.op == PFLT_BVSUB && r.args.size() == 2 && T(r.args[1]).op == T_BV) {
+                addsub(T(r.args[1]).val, true);
+                t = r.args[0];
+                continue;
+            }
+            return {t, c8_of(Big(c, c + 8), w)};
+        }
+    }
+
     int32_t select(uint32_t arr, uint32_t idx) {
         const TermRec& A = T(arr);
         if (A.op == T_STORE) {
             const uint32_t base = A.args[0], k = A.args[1], v = A.args[2];
             if (k == idx) return node(v);
-            if (T(k).op == T_BV && T(idx).op == T_BV)
-                return big_eq(T(k).val, T(idx).val) ? node(v) : select(base, idx);
+            const auto kf = offset_form(k), xf = offset_form(idx);
+            if (kf.first == xf.first)  // the same base: the offsets decide
+                return kf.second == xf.second ? node(v) : select(base, idx);
             const int32_t rest = select(base, idx);
             const int32_t c = d.op(PF_B_EQ, width(idx), {node(idx), node(k)});
             return d.op(PF_W_ITE, A.w2, {c, node(v), rest});
@@ -1013,9 +1056,11 @@ struct Lowering {
         const std::pair<uint32_t, uint32_t> rd{arr, idx};
         int32_t val = mkvar(vname, rng, VarTerm{PFLT_VT_SELECT, arr, idx, 0}, nullptr, &rd);
         auto& entries = arrays[name];
+        const auto xf = offset_form(idx);
         for (size_t i = entries.size(); i-- > 0;) {
             const auto& e = entries[i];
-            if (T((uint32_t)e[0]).op == T_BV && T(idx).op == T_BV) continue;
+            const auto ef = offset_form((uint32_t)e[0]);
+            if (ef.first == xf.first && !(ef.second == xf.second)) continue;  // never aliases
             val = d.op(PF_W_ITE, rng, {d.op(PF_B_EQ, width(idx), {inode, e[2]}), e[3], val});
         }
         entries.push_back({(int32_t)idx, (int32_t)arr, inode, val});

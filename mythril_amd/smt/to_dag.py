@@ -429,14 +429,38 @@ class TermLowering:
         return node
 
     # ---- arrays ---------------------------------------------------------------------------
+    @staticmethod
+    def _offset_form(t: T.Term) -> Tuple[Optional[T.Term], int]:
+        """(base, c) with t = base + c mod 2^w — constant additions and subtractions peeled
+        off (base None for a constant).  Two indices with the same base and different c can
+        never be equal: LASER's dynamic-ABI reads ``calldata[off + 4 + k]`` (ABI words and
+        string bytes at one symbolic offset) then need no aliasing test among themselves."""
+        m = (1 << t.width) - 1
+        c = 0
+        while True:
+            if t.op == "bv":
+                return None, (c + t.val) & m
+            if t.op == "bvadd" and len(t.args) == 2:
+                if t.args[1].op == "bv":
+                    c, t = c + t.args[1].val, t.args[0]
+                    continue
+                if t.args[0].op == "bv":
+                    c, t = c + t.args[0].val, t.args[1]
+                    continue
+            elif t.op == "bvsub" and len(t.args) == 2 and t.args[1].op == "bv":
+                c, t = c - t.args[1].val, t.args[0]
+                continue
+            return t, c & m
+
     def _select(self, arr: T.Term, idx: T.Term, term: T.Term) -> int:
         d = self.dag
         if arr.op == "store":
             base, k, v = arr.args
             if k is idx:
                 return self.node(v)
-            if k.op == "bv" and idx.op == "bv":
-                return self._select(base, idx, term) if k.val != idx.val else self.node(v)
+            (kb, kc), (ib, ic) = self._offset_form(k), self._offset_form(idx)
+            if kb is ib:  # the same base: the offsets decide (both constants: their values)
+                return self._select(base, idx, term) if kc != ic else self.node(v)
             rest = self._select(base, idx, T.select(base, idx))
             c = d.op(ir.B_EQ, idx.width, self.node(idx), self.node(k))
             return d.op(ir.W_ITE, arr.sort[2], c, self.node(v), rest)
@@ -464,9 +488,11 @@ class TermLowering:
         sel_term = T.select(arr, idx)
         val = self._var(vname, rng, sel_term)
         # first earlier index with an equal value wins (consistent array interpretation)
+        ib, ic = self._offset_form(idx)
         for (it, _, inn, v) in reversed(entries):
-            if it.op == "bv" and idx.op == "bv":
-                continue  # distinct constants never alias
+            tb, tc = self._offset_form(it)
+            if tb is ib and tc != ic:
+                continue  # the same base at another offset (distinct constants) never aliases
             val = d.op(ir.W_ITE, rng, d.op(ir.B_EQ, idx.width, inode, inn), v, val)
         entries.append((idx, sel_term, inode, val))
         return val

@@ -217,3 +217,45 @@ def test_witness_reads_nested_calldata_offsets_like_the_program():
         agree += got == want
         sat += want
     assert agree == 400 and sat > 0
+
+
+def test_reads_at_one_base_and_distinct_offsets_need_no_alias_test():
+    """calldata[x + 4 + k] for k = 0..3 (one symbolic base, distinct constant offsets — a
+    dynamic-ABI word) can never alias each other, so the lowering emits no index comparison
+    between them (TermLowering._offset_form); against a constant index and across bases the
+    comparisons stay.  A store at base + c read back at (base + c - 1) + 1 is that store's
+    value without a test.  The program, the host Witness and the oracle still agree."""
+    from mythril_amd.smt import terms as T
+    from mythril_amd.smt.interp import Witness
+    from mythril_amd.smt.to_dag import TermLowering, UFRegistry
+
+    cd = T.array("1_calldata", 256, 8)
+    x = T.var("x", 256)
+    y = T.var("y", 256)
+    base = T.binop("bvadd", x, T.const(4, 256))
+    word = T.concat(*[T.select(cd, T.binop("bvadd", base, T.const(k, 256))) for k in range(4)])
+    lo = TermLowering(UFRegistry()).lower([T.cmp("bvult", T.const(5, 32), word)])
+    assert not any(n.kind == ir.B_EQ for n in lo.dag.nodes)
+    # a constant index and another base do get compared with the symbolic reads
+    cs = [T.cmp("bvult", T.const(5, 32), word),
+          T.eq(T.select(cd, T.const(6, 256)), T.const(7, 8)),
+          T.eq(T.select(cd, y), T.const(9, 8))]
+    lo2 = TermLowering(UFRegistry()).lower(cs)
+    # 4 reads x cd[6], 5 earlier reads x cd[y], and the two equalities of the constraints
+    assert sum(n.kind == ir.B_EQ for n in lo2.dag.nodes) == 4 + 5 + 2
+    st = T.store(T.array("s", 256, 256), T.binop("bvadd", x, T.const(3, 256)), T.const(11, 256))
+    idx = T.binop("bvadd", T.binop("bvsub", T.binop("bvadd", x, T.const(3, 256)), T.const(1, 256)),
+                  T.const(1, 256))
+    rd = TermLowering(UFRegistry())
+    assert rd.node(T.select(st, idx)) == rd.dag.const(11, 256)
+    prog = lower(lo2.dag)
+    sv = O.SetView.from_batch(ir.Batch([prog]), 0)
+    rng = random.Random(5)
+    agree = sat = 0
+    for _ in range(300):
+        vals = [rng.choice((0, 1, 2, 3, 6, 7, 9, rng.getrandbits(8))) & ir.mask(v.width) for v in lo2.dag.vars]
+        want = sv.evaluate(vals)
+        got = all(bool(Witness(lo2, vals, UFRegistry()).ev(c)) for c in cs)
+        agree += got == want
+        sat += want
+    assert agree == 300 and sat > 0
