@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--keccak-log2", type=int, default=24,
                     help="config 4: 2^k 64-byte key||slot messages per Keccak launch (0 = skip)")
     ap.add_argument("--lib", default=None, help="alternative build of libpathfeas.so (experiments)")
+    ap.add_argument("--serial-steps", action="store_true",
+                    help="one waited pf_check_batch call per step instead of all K enqueued at once")
     ap.add_argument("--corpus-scenarios", type=int, default=48,
                     help="LASER-shaped scenarios for the %% discharged half of the metric (0 = skip)")
     return ap.parse_args()
@@ -370,8 +372,17 @@ def main():
     evals = ops = 0
     kms = []
     founds = []
-    for k in range(args.warmup, n_steps):
-        r = eng.check(batches[k], budget=args.budget, seed=args.seed, flags=flags)
+    # the K steps are enqueued back to back on the device stream (pf_check_batches) and read
+    # afterwards — a stream of independent batches, as a batching caller would issue them —
+    # so no host round trip sits between two steps' kernels (--serial-steps: one
+    # pf_check_batch call per step, each waited for)
+    if args.serial_steps:
+        results = [eng.check(batches[k], budget=args.budget, seed=args.seed, flags=flags)
+                   for k in range(args.warmup, n_steps)]
+    else:
+        results = eng.check_each(batches[args.warmup:n_steps], budget=args.budget, seed=args.seed,
+                                 flags=flags)
+    for r in results:
         evals += r.evals_full if args.mode == "full" else r.cands_decided
         ops += r.ops
         kms.append(r.kernel_ms)

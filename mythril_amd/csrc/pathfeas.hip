@@ -189,6 +189,12 @@ void geometry(int num_cus, uint32_t n_sets, uint32_t budget, uint32_t flags, uin
         const uint64_t groups = (budget + 63u) / 64u;
         const uint64_t max_items = (uint64_t)num_cus * g_waves_per_cu_early * 64u;
         uint64_t cg = std::max<uint64_t>(g_early_chunk_groups, (n_sets * groups + max_items - 1) / max_items);
+        // small batches (the funnel's single queries, fork pairs): chunks small enough that
+        // every wave slot of the grid gets an item, so a set without a witness among its
+        // candidates takes one chunk's time per wave, not g_early_chunk_groups groups'
+        const uint64_t slots = (uint64_t)num_cus * g_waves_per_cu_early;
+        const uint64_t fill = (n_sets * groups + slots - 1) / slots;
+        if (fill < cg) cg = fill;
         cg = std::max<uint64_t>(1, std::min<uint64_t>(cg, groups));
         *per_wave = (uint32_t)(cg * 64u);
         *slices = std::max<uint32_t>(1u, (budget + *per_wave - 1) / *per_wave);

@@ -1455,10 +1455,15 @@ Result* lower_job(const Store& S, const std::vector<uint32_t>& rs, const Parents
                 if (rc == 0) {
                     R->code.resize(4 * ni);
                     R->consts.resize(8 * nc);
-                    bool spills = false;
-                    for (size_t i = 0; i < ni; i++) spills |= (R->code[4 * i] & 0xffu) == PF_W_SPILL;
+                    // narrow unless spill code exceeds an eighth of the program (lower.py
+                    // _spill_heavy: the same policy)
+                    size_t n_spill = 0;
+                    for (size_t i = 0; i < ni; i++) {
+                        const uint32_t op = R->code[4 * i] & 0xffu;
+                        n_spill += op == PF_W_SPILL || op == PF_W_FILL;
+                    }
                     R->n_wregs = tries[ti];
-                    if (ti == 0 && spills) continue;  // the wide register file instead
+                    if (ti == 0 && 8 * n_spill > ni) continue;  // the wide register file instead
                     break;
                 }
                 if (rc != -2) break;

@@ -134,6 +134,27 @@ class Engine:
                            sum(s.cands_decided for s in stats), sum(s.ops for s in stats),
                            max(s.kernel_ms for s in stats), any(s.timed_out for s in stats))
 
+    def check_each(self, dbs: Sequence[DeviceBatch], budget: int = 65536, seed: int = 0,
+                   flags: int = 2, timeout_ms: int = 0) -> List[CheckResult]:
+        """check() of every batch, all enqueued before any result is read (pf_check_batches):
+        batches on one device run back to back on its stream, with no host round trip
+        between them (a stream of independent batches, e.g. bench steps)."""
+        if not dbs:
+            return []
+        n = sum(len(db) for db in dbs)
+        found = np.full(max(n, 1), NOT_FOUND, dtype=np.uint32)
+        stats = (_lib.pf_stats * len(dbs))()
+        handles = np.array([db.handle for db in dbs], dtype=np.uint64)
+        _lib.check(_lib.lib().pf_check_batches(_lib.ptr_u64(handles), len(dbs), seed, budget, flags,
+                                              timeout_ms, _lib.ptr_u32(found), stats),
+                   "pf_check_batches")
+        out, off = [], 0
+        for db, s in zip(dbs, stats):
+            out.append(CheckResult(found[off:off + len(db)].copy(), s.evals_full, s.cands_decided,
+                                   s.ops, s.kernel_ms, bool(s.timed_out)))
+            off += len(db)
+        return out
+
     def materialize(self, db: DeviceBatch, set_ids: Sequence[int], cand_ids: Sequence[int],
                     seed: int = 0) -> List[List[int]]:
         """Concrete variable values of the given (set, candidate) pairs."""

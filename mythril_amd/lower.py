@@ -373,23 +373,32 @@ def pack_nodes(dag: Dag):
     return out
 
 
-def _spills(prog) -> bool:
+def _spill_heavy(prog) -> bool:
+    """More than an eighth of the program is W spill / fill code.  A program with a few
+    spills still runs faster in the 8-register kernels (4 waves/SIMD, the scratch round trips
+    of a spill cost about a cheap op) than in the 16-register ones at 2 waves/SIMD — and its
+    batch then needs no second launch (config 3: 0.4 % of the DAGs, 2-8 spill/fill
+    instructions each, were the whole 0.2 ms r16 launch per step).  pf_terms.cpp applies the
+    same policy."""
     if isinstance(prog, ir.PackedProgram):
-        return bool(((prog.words[:, 0] & 0xFF) == ir.W_SPILL).any())
-    return any(ins.op == ir.W_SPILL for ins in prog.code)
+        ops = prog.words[:, 0] & 0xFF
+        n, ns = len(ops), int(((ops == ir.W_SPILL) | (ops == ir.W_FILL)).sum())
+    else:
+        n, ns = len(prog.code), sum(1 for ins in prog.code if ins.op in (ir.W_SPILL, ir.W_FILL))
+    return 8 * ns > n
 
 
 def lower(dag: Dag, seed: int = 0, name: str = "", nw: Optional[int] = None) -> Program:
     """Register allocation + emission.  Without ``nw``: over ir.NW_NARROW registers first —
-    such a program runs the 8-register, 3-waves/SIMD search kernels — and over all ir.NW
-    when that would spill a W value or cannot fit (the 16-register kernels then run its
-    batch).  The native library when built (identical output, tests/test_native_lower.py),
+    such a program runs the 8-register, 4-waves/SIMD search kernels — and over all ir.NW
+    when that would make it spill-heavy (:func:`_spill_heavy`) or cannot fit (the
+    16-register kernels then run its batch).  The native library when built (identical output, tests/test_native_lower.py),
     else the Python reference :func:`lower_py`."""
     if nw is None:
         dag.finalize_word_hints()
         try:
             prog = lower(dag, seed, name, ir.NW_NARROW)
-            if not _spills(prog):
+            if not _spill_heavy(prog):
                 return prog
         except LoweringError:
             pass

@@ -117,6 +117,15 @@ def test_gpu_mask_engine_and_check_many(engine):
     r2 = eng.check_many([a, b], budget=4096, seed=0, flags=ir.FLAG_EARLY_EXIT | ir.FLAG_SHORTCIRCUIT)
     assert np.array_equal(r1.found, r2.found)
     assert r2.cands_decided > 0
+    # check_each (bench steps): the batches enqueued back to back on one stream, each with
+    # its own verdicts and counters — the full sweep too
+    for flags in (ir.FLAG_EARLY_EXIT | ir.FLAG_SHORTCIRCUIT, 0):
+        ra, rb = eng.check(a, budget=4096, seed=0, flags=flags), eng.check(b, budget=4096, seed=0, flags=flags)
+        each = eng.check_each([a, b], budget=4096, seed=0, flags=flags)
+        assert [len(r.found) for r in each] == [40, 56]
+        assert np.array_equal(each[0].found, ra.found) and np.array_equal(each[1].found, rb.found)
+        assert (each[0].evals_full, each[1].evals_full) == (ra.evals_full, rb.evals_full)
+        assert each[0].kernel_ms > 0 and each[1].kernel_ms > 0
     for db in (whole, a, b):
         db.free()
 
