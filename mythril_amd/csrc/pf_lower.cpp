@@ -247,8 +247,24 @@ class Lowerer {
         return (uint32_t)(consts.size() - 1);
     }
 
-    bool spill(int rg, int nd) {
-        if (free_slots.empty()) return false;
+    bool spill(int rg, int nd, int t, bool steal = true) {
+        if (free_slots.empty()) {
+            // a value that cannot be recomputed takes the slot of a spilled variable, the
+            // one used farthest in the future (lower.py spill: the same choice)
+            if (!steal) return false;
+            int far_v = NONE, far_nu = -1;
+            for (size_t v = 0; v < slot_of.size(); ++v) {
+                if (slot_of[v] == NONE || N[v].kind != PFL_K_VAR) continue;
+                const int nu = next_use((int)v, t);
+                if (far_v == NONE || nu >= far_nu) {
+                    far_v = (int)v;
+                    far_nu = nu;
+                }
+            }
+            if (far_v == NONE) return false;
+            free_slots.push_back(slot_of[far_v]);
+            slot_of[far_v] = NONE;
+        }
         const int s = free_slots.back();
         free_slots.pop_back();
         if (N[nd].is_bool)
@@ -274,7 +290,11 @@ class Lowerer {
                 const int nd = rf.holder[rg];
                 if (nd == NONE || ((pinned >> rg) & 1u)) continue;
                 if (slot_of[nd] == NONE && remat_size(nd) == NONE) continue;
-                const int sz = slot_of[nd] != NONE ? 1 : remat_cost(nd);
+                // a variable used again is spilled while a slot is free (lower.py
+                // _VAR_SPILL_COST): one spill now, fills later, no generator re-run
+                const int sz = slot_of[nd] != NONE ? 1
+                             : (N[nd].kind == PFL_K_VAR && !free_slots.empty()) ? 2
+                                                                                : remat_cost(nd);
                 const long long nu = -(long long)next_use(nd, t);
                 if (!have || sz < best_sz || (sz == best_sz && (nu < best_nu || (nu == best_nu && rg < best_r)))) {
                     have = true;
@@ -285,6 +305,10 @@ class Lowerer {
             }
             if (have) {
                 r = best_r;
+                const int old = rf.holder[r];
+                if (N[old].kind == PFL_K_VAR && slot_of[old] == NONE && !free_slots.empty() &&
+                    next_use(old, t) < INF)
+                    spill(r, old, t, false);
             } else {  // spill the value used farthest in the future
                 int vr = -1, vfar = -1;
                 for (int rg = 0; rg < rf.n; ++rg) {
@@ -296,7 +320,7 @@ class Lowerer {
                         vr = rg;
                     }
                 }
-                if (vr < 0 || !spill(vr, rf.holder[vr]))
+                if (vr < 0 || !spill(vr, rf.holder[vr], t))
                     throw LowerError{fail(-2, "more than %d live %s values", rf.n, &rf == &W ? "W" : "B")};
                 r = vr;
             }

@@ -1437,6 +1437,11 @@ Result* lower_job(const Store& S, const std::vector<uint32_t>& rs, const Parents
             if (roots2.empty()) roots2.push_back(0);
             const uint32_t tries[2] = {PF_NW_NARROW, PF_NW};
             int rc = -2;
+            // the narrow program unless its spill code exceeds an eighth of it and the wide
+            // register file at least halves that (lower.py lower(): the same policy)
+            bool have_narrow = false;
+            std::vector<uint32_t> n_code, n_consts;
+            size_t n_spill_narrow = 0;
             for (int ti = 0; ti < 2; ti++) {
                 size_t cap_i = 16 * d.nodes.size() + 64 + 4 * d.roots.size();
                 size_t cap_c = R->pool.size() / 8 + d.forced.size() + 1;
@@ -1455,15 +1460,31 @@ Result* lower_job(const Store& S, const std::vector<uint32_t>& rs, const Parents
                 if (rc == 0) {
                     R->code.resize(4 * ni);
                     R->consts.resize(8 * nc);
-                    // narrow unless spill code exceeds an eighth of the program (lower.py
-                    // _spill_heavy: the same policy)
                     size_t n_spill = 0;
                     for (size_t i = 0; i < ni; i++) {
                         const uint32_t op = R->code[4 * i] & 0xffu;
                         n_spill += op == PF_W_SPILL || op == PF_W_FILL;
                     }
                     R->n_wregs = tries[ti];
-                    if (ti == 0 && 8 * n_spill > ni) continue;  // the wide register file instead
+                    if (ti == 0 && 8 * n_spill > ni) {  // spill-heavy: try the wide register file
+                        have_narrow = true;
+                        n_code.swap(R->code);
+                        n_consts.swap(R->consts);
+                        n_spill_narrow = n_spill;
+                        continue;
+                    }
+                    if (ti == 1 && have_narrow && 2 * n_spill > n_spill_narrow) {
+                        R->code.swap(n_code);
+                        R->consts.swap(n_consts);
+                        R->n_wregs = tries[0];
+                    }
+                    break;
+                }
+                if (rc == -2 && ti == 1 && have_narrow) {  // the wide lowering failed: keep the narrow one
+                    R->code.swap(n_code);
+                    R->consts.swap(n_consts);
+                    R->n_wregs = tries[0];
+                    rc = 0;
                     break;
                 }
                 if (rc != -2) break;

@@ -270,9 +270,10 @@ class _RegFile:
         self.holder: Dict[int, int] = {}   # reg -> node
         self.where: Dict[int, int] = {}    # node -> reg
 
-    def alloc(self, node: int, evict_rank, pinned, spill=None, far=None) -> int:
-        """Take a free register, else evict the cheapest-to-restore value (evict_rank),
-        else spill the value used farthest in the future (spill(reg, node) emits it)."""
+    def alloc(self, node: int, evict_rank, pinned, spill=None, far=None, on_evict=None) -> int:
+        """Take a free register, else evict the cheapest-to-restore value (evict_rank;
+        on_evict(reg, node) may spill it first), else spill the value used farthest in the
+        future (spill(reg, node) emits it)."""
         if self.free:
             # the lowest free register: the narrow kernels keep their highest register out
             # of VGPRs when pressure demands (pf_eval.hip), so it should be the rarest one
@@ -283,6 +284,8 @@ class _RegFile:
             cands = [c for c in cands if c[0] is not None]
             if cands:
                 _, r = min(cands)
+                if on_evict is not None:
+                    on_evict(r, self.holder[r])
             else:
                 victims = [(far(nd), rg) for rg, nd in self.holder.items() if rg not in pinned]
                 if not victims or spill is None or not spill(max(victims)[1], self.holder[max(victims)[1]]):
@@ -307,6 +310,12 @@ _REMAT_OPCOST = 16  # only cheap ops (compare/ite/logic/extract/concat) are reco
 # Philox blocks + the strategy arms) measured ~6x a cheap op's time on the GPU, so under the
 # 7-register file a constant or a short recomputation is evicted before a variable
 _VAR_REMAT_COST = 6
+# ... but an evicted variable that is used again is spilled while a slot is free (one
+# W_SPILL now, one W_FILL per restore: scratch round trips, no generator run): storage-heavy
+# LASER buckets re-read their ~70 symbols across ~1,200 array-aliasing compares, which at 7
+# registers re-ran the generator for every read (1,186 W_VAR for 69 variables in the
+# heaviest corpus bucket — most of its search time)
+_VAR_SPILL_COST = 2
 
 
 # ---- native lowering (libpflower.so, include/pf_lower.h) ----------------------------------
@@ -373,6 +382,14 @@ def pack_nodes(dag: Dag):
     return out
 
 
+def _spill_code(prog) -> Tuple[int, int]:
+    """(instructions, W spill + fill instructions) of a program."""
+    if isinstance(prog, ir.PackedProgram):
+        ops = prog.words[:, 0] & 0xFF
+        return len(ops), int(((ops == ir.W_SPILL) | (ops == ir.W_FILL)).sum())
+    return len(prog.code), sum(1 for ins in prog.code if ins.op in (ir.W_SPILL, ir.W_FILL))
+
+
 def _spill_heavy(prog) -> bool:
     """More than an eighth of the program is W spill / fill code.  A program with a few
     spills still runs faster in the 8-register kernels (4 waves/SIMD, the scratch round trips
@@ -380,11 +397,7 @@ def _spill_heavy(prog) -> bool:
     batch then needs no second launch (config 3: 0.4 % of the DAGs, 2-8 spill/fill
     instructions each, were the whole 0.2 ms r16 launch per step).  pf_terms.cpp applies the
     same policy."""
-    if isinstance(prog, ir.PackedProgram):
-        ops = prog.words[:, 0] & 0xFF
-        n, ns = len(ops), int(((ops == ir.W_SPILL) | (ops == ir.W_FILL)).sum())
-    else:
-        n, ns = len(prog.code), sum(1 for ins in prog.code if ins.op in (ir.W_SPILL, ir.W_FILL))
+    n, ns = _spill_code(prog)
     return 8 * ns > n
 
 
@@ -396,13 +409,25 @@ def lower(dag: Dag, seed: int = 0, name: str = "", nw: Optional[int] = None) -> 
     else the Python reference :func:`lower_py`."""
     if nw is None:
         dag.finalize_word_hints()
+        narrow = None
         try:
-            prog = lower(dag, seed, name, ir.NW_NARROW)
-            if not _spill_heavy(prog):
-                return prog
+            narrow = lower(dag, seed, name, ir.NW_NARROW)
+            if not _spill_heavy(narrow):
+                return narrow
         except LoweringError:
             pass
-        return lower(dag, seed, name, ir.NW)
+        try:
+            wide = lower(dag, seed, name, ir.NW)
+        except LoweringError:
+            if narrow is None:
+                raise
+            return narrow
+        # a spill-heavy narrow program moves to the wide register file only when that at
+        # least halves its spill code (storage-heavy buckets whose evicted symbols spill
+        # under 15 registers too stay at 4 waves/SIMD)
+        if narrow is not None and 2 * _spill_code(wide)[1] > _spill_code(narrow)[1]:
+            return narrow
+        return wide
     L = _native()
     if not L:
         return lower_py(dag, seed, name, nw)
@@ -516,15 +541,26 @@ def lower_py(dag: Dag, seed: int = 0, name: str = "", nw: int = ir.NW) -> Progra
                 cost = 1
             elif remat_size(nd) is None:
                 return None
+            elif dag.nodes[nd].kind == K_VAR and free_slots:
+                cost = _VAR_SPILL_COST
             else:
                 cost = remat_cost(nd)
             # cheapest restore first, then farthest next use (Belady)
             return (cost, -next_use(nd, t))
         return f
 
-    def spill(rg: int, nd: int) -> bool:
+    def spill(rg: int, nd: int, t: int = 0, steal: bool = True) -> bool:
         if not free_slots:
-            return False
+            # a value that cannot be recomputed takes the slot of a spilled variable (the
+            # one used farthest in the future; its later restores re-run the generator)
+            vs = [v for v in sorted(slot_of) if dag.nodes[v].kind == K_VAR] if steal else []
+            if not vs:
+                return False
+            far_v = vs[0]
+            for v in vs[1:]:
+                if next_use(v, t) >= next_use(far_v, t):
+                    far_v = v
+            free_slots.append(slot_of.pop(far_v))
         s = free_slots.pop()
         n = dag.nodes[nd]
         if n.is_bool:
@@ -535,7 +571,12 @@ def lower_py(dag: Dag, seed: int = 0, name: str = "", nw: int = ir.NW) -> Progra
         return True
 
     def alloc(rf, nd, t, pinned):
-        return rf.alloc(nd, rank(t), pinned, spill, lambda x: next_use(x, t))
+        def on_evict(rg, old):
+            if dag.nodes[old].kind == K_VAR and old not in slot_of and free_slots \
+                    and next_use(old, t) < (1 << 30):
+                spill(rg, old, t, False)
+        return rf.alloc(nd, rank(t), pinned, lambda rg, x: spill(rg, x, t), lambda x: next_use(x, t),
+                        on_evict)
 
     def done(nd):
         regfile(nd).release(nd)

@@ -41,17 +41,20 @@ def _same1(dag, seed, nw):
 
 def _same(dag, seed=0):
     """Native == Python at both register counts the engine uses, and the default policy:
-    the narrow program unless it is spill-heavy or does not fit, then the 15-register one."""
+    the narrow program unless it does not fit, or is spill-heavy and the 15-register one at
+    least halves its spill code."""
     e_narrow = _same1(dag, seed, ir.NW_NARROW)
     e_wide = _same1(dag, seed, ir.NW)
     if e_wide is not None:
         return e_wide
     got = LW.lower(dag, seed=seed)
     narrow = None if e_narrow is not None else LW.lower_py(dag, seed=seed, nw=ir.NW_NARROW)
-    if narrow is not None and not LW._spill_heavy(narrow):
+    wide = LW.lower_py(dag, seed=seed, nw=ir.NW)
+    if narrow is not None and (not LW._spill_heavy(narrow)
+                               or 2 * LW._spill_code(wide)[1] > LW._spill_code(narrow)[1]):
         assert np.array_equal(_words(got), _words(narrow))
     else:
-        assert np.array_equal(_words(got), _words(LW.lower_py(dag, seed=seed, nw=ir.NW)))
+        assert np.array_equal(_words(got), _words(wide))
     return None
 
 
