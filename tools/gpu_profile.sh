@@ -15,5 +15,6 @@ timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- $P > $OUT/write.log 2>&1 || { echo "write failed"; exit 1; }
 timeout -k 10 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_WAVE_CYCLES --output-format csv -d $OUT/sq -o run -- $P > $OUT/sq.log 2>&1 || { echo "sq failed"; exit 1; }
 timeout -k 10 400 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU --output-format csv -d $OUT/clk -o run -- $P > $OUT/clk.log 2>&1 || { echo "clk failed"; exit 1; }
+timeout -k 10 400 rocprofv3 --pmc SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_CVT --output-format csv -d $OUT/f64 -o run -- $P > $OUT/f64.log 2>&1 || { echo "f64 failed"; exit 1; }
 echo PROFILE-DONE
 tail -1 $OUT/trace.log | cut -c1-300

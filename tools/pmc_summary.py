@@ -15,6 +15,8 @@ import os
 import sys
 
 KERNEL = "pf_check_kernel"
+F64_KEYS = ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
+            "SQ_INSTS_VALU_TRANS_F64", "SQ_INSTS_VALU_CVT")
 KECCAK = "pf_keccak_fixed_kernel"
 # pf_check_kernel is the full sweep only (the early-exit legs launch pf_check_early_kernel):
 # every one of its dispatches is the workload the roofline line is quoted on
@@ -55,6 +57,20 @@ def main():
     if clk:
         out["clk"] = {k: mean(clk, k) for k in ("GRBM_GUI_ACTIVE", "SQ_BUSY_CYCLES",
                                                  "SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU")}
+    f64 = per_dispatch(csvp("f64"))
+    if f64:
+        out["f64"] = {k: mean(f64, k) for k in F64_KEYS if k in f64[0]}
+        # VALU pipeline cycles per launch, cycle-weighted (not issue-counted): a wave64 op
+        # takes 2 SIMD cycles on SIMD-32 (MI355X_MICROARCH.md), v_mad_u64_u32 5.5 (measured,
+        # tools/mulbench.hip), f64 ops 4 (FP64 vector = half the FP32 rate), so the share of
+        # the SIMDs' cycles the VALU is busy is this over (1024 SIMDs x effective cycles)
+        n64 = sum(out["f64"].get(k, 0.0) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
+                                                    "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64",
+                                                    "SQ_INSTS_VALU_CVT"))
+        ni64 = sqm["SQ_INSTS_VALU_INT64"]
+        rest = sqm["SQ_INSTS_VALU"] - ni64 - n64
+        out["valu_cycles"] = {"cycles": 2.0 * rest + 5.5 * ni64 + 4.0 * n64, "int64": ni64, "fp64": n64,
+                              "other": rest, "weights": "other 2, int64 (v_mad_u64_u32) 5.5, f64 and conversions 4 SIMD cycles"}
     kf, kw = per_dispatch(csvp("fetch"), KECCAK), per_dispatch(csvp("write"), KECCAK)
     if kf and kw:
         k = {"kernel": KECCAK, "fetch_bytes": 2 * mean(kf, "FETCH_SIZE") * 1024,
@@ -73,6 +89,14 @@ def main():
     if "clk" in out:
         for key, v in out["clk"].items():
             lines.append(f"| {key} (clock pass) | {v:.4g} |")
+    for key, v in out.get("f64", {}).items():
+        lines.append(f"| {key} (f64 pass) | {v:.4g} |")
+    if "valu_cycles" in out:
+        vc = out["valu_cycles"]
+        lines.append(f"| VALU pipeline cycles (other x2 + int64 x5.5 + f64 x4) | {vc['cycles']:.4g} |")
+        if "clk" in out:
+            eff = out["clk"]["GRBM_GUI_ACTIVE"] / 8.0  # per-XCD cycles of the launch
+            lines.append(f"| VALU pipeline busy (over 1024 SIMDs x {eff:.4g} cycles) | {vc['cycles'] / (1024 * eff):.3f} |")
     w = sqm["SQ_WAVES"]
     lines += ["", f"per wave: {sqm['SQ_INSTS_VALU'] / w:.4g} VALU ({sqm['SQ_INSTS_VALU_INT64'] / w:.4g} int64), "
               f"{sqm['SQ_INSTS_SALU'] / w:.4g} SALU, {sqm['SQ_INSTS_BRANCH'] / w:.4g} branches, "
