@@ -36,8 +36,8 @@ INT32_PEAK_OPS = 256 * 4 * 32 * 2.4e9
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--sets", type=int, default=1024, help="DAGs per step per GPU")
     ap.add_argument("--budget", type=int, default=65536, help="candidates per DAG")
     ap.add_argument("--mode", choices=["full", "early"], default="full")
@@ -324,6 +324,12 @@ def valu_view(pmc, kernel_s):
         cyc = clk["GRBM_GUI_ACTIVE"] / 8.0
         # both counts from the same PMC run: independent of this run's kernel time
         out["issue_frac_eff_clock"] = 2.0 * clk["SQ_INSTS_VALU"] / (1024 * cyc)
+        vc = pmc.get("valu_cycles")
+        if vc:
+            # cycle-weighted: v_mad_u64_u32 holds the SIMD 5.5 cycles and f64 ops and
+            # conversions 4, not 2 (tools/pmc_summary.py) — the VALU pipeline's occupancy
+            out["valu_busy_eff_clock"] = vc["cycles"] / (1024 * cyc)
+            out["valu_busy_weights"] = vc["weights"]
     return out
 
 
