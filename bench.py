@@ -326,8 +326,9 @@ def valu_view(pmc, kernel_s):
         out["issue_frac_eff_clock"] = 2.0 * clk["SQ_INSTS_VALU"] / (1024 * cyc)
         vc = pmc.get("valu_cycles")
         if vc:
-            # cycle-weighted: v_mad_u64_u32 holds the SIMD 5.5 cycles and f64 ops and
-            # conversions 4, not 2 (tools/pmc_summary.py) — the VALU pipeline's occupancy
+            # cycle-weighted at the issue costs measured at 4 waves/SIMD (tools/movbench.hip:
+            # a simple op 2.9 cycles, v_mad_u64_u32 4.95, f64 4.9; tools/pmc_summary.py) —
+            # the VALU pipeline's occupancy
             out["valu_busy_eff_clock"] = vc["cycles"] / (1024 * cyc)
             out["valu_busy_weights"] = vc["weights"]
     return out

@@ -60,17 +60,21 @@ def main():
     f64 = per_dispatch(csvp("f64"))
     if f64:
         out["f64"] = {k: mean(f64, k) for k in F64_KEYS if k in f64[0]}
-        # VALU pipeline cycles per launch, cycle-weighted (not issue-counted): a wave64 op
-        # takes 2 SIMD cycles on SIMD-32 (MI355X_MICROARCH.md), v_mad_u64_u32 5.5 (measured,
-        # tools/mulbench.hip), f64 ops 4 (FP64 vector = half the FP32 rate), so the share of
-        # the SIMDs' cycles the VALU is busy is this over (1024 SIMDs x effective cycles)
+        # VALU pipeline cycles per launch, cycle-weighted (not issue-counted) at the issue
+        # costs tools/movbench.hip measures at the search kernel's 4 waves/SIMD
+        # (profiles/r03_movbench.log, shader cycles): a simple wave64 op 2.9 (not the 2 of the
+        # SIMD-32 datasheet), v_mad_u64_u32 4.95, f64 ops and conversions 4.9 — three-source
+        # integer ops (4.8) are not separable in the PMC and count as simple, so this is a
+        # lower bound; over (1024 SIMDs x effective cycles) it is the VALU's occupancy
         n64 = sum(out["f64"].get(k, 0.0) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
                                                     "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64",
                                                     "SQ_INSTS_VALU_CVT"))
         ni64 = sqm["SQ_INSTS_VALU_INT64"]
         rest = sqm["SQ_INSTS_VALU"] - ni64 - n64
-        out["valu_cycles"] = {"cycles": 2.0 * rest + 5.5 * ni64 + 4.0 * n64, "int64": ni64, "fp64": n64,
-                              "other": rest, "weights": "other 2, int64 (v_mad_u64_u32) 5.5, f64 and conversions 4 SIMD cycles"}
+        out["valu_cycles"] = {"cycles": 2.9 * rest + 4.95 * ni64 + 4.9 * n64, "int64": ni64, "fp64": n64,
+                              "other": rest,
+                              "weights": "measured issue costs at 4 waves/SIMD (tools/movbench.hip): other 2.9, "
+                                         "int64 (v_mad_u64_u32) 4.95, f64 and conversions 4.9 SIMD cycles"}
     kf, kw = per_dispatch(csvp("fetch"), KECCAK), per_dispatch(csvp("write"), KECCAK)
     if kf and kw:
         k = {"kernel": KECCAK, "fetch_bytes": 2 * mean(kf, "FETCH_SIZE") * 1024,
@@ -93,7 +97,7 @@ def main():
         lines.append(f"| {key} (f64 pass) | {v:.4g} |")
     if "valu_cycles" in out:
         vc = out["valu_cycles"]
-        lines.append(f"| VALU pipeline cycles (other x2 + int64 x5.5 + f64 x4) | {vc['cycles']:.4g} |")
+        lines.append(f"| VALU pipeline cycles (other x2.9 + int64 x4.95 + f64 x4.9, measured issue costs) | {vc['cycles']:.4g} |")
         if "clk" in out:
             eff = out["clk"]["GRBM_GUI_ACTIVE"] / 8.0  # per-XCD cycles of the launch
             lines.append(f"| VALU pipeline busy (over 1024 SIMDs x {eff:.4g} cycles) | {vc['cycles'] / (1024 * eff):.3f} |")
