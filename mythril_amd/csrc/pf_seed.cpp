@@ -9,7 +9,7 @@
 // two's-complement.  Host code, no HIP.
 #include <cstdint>
 #include <cstring>
-#include <functional>
+
 #include <string>
 #include <vector>
 
@@ -106,9 +106,19 @@ U shr(const U& a, unsigned k) {
     }
     return r;
 }
-U mask(unsigned w) {  // 2^w - 1
+U mask_slow(unsigned w) {
     if (w >= 256) return unot(U());
     return sub(shl(U::of(1), w), U::of(1));
+}
+struct MaskTable {
+    U m[257];
+    MaskTable() {
+        for (unsigned w = 0; w <= 256; w++) m[w] = mask_slow(w);
+    }
+};
+const U& mask(unsigned w) {  // 2^w - 1
+    static const MaskTable t;
+    return t.m[w >= 256 ? 256 : w];
 }
 U mw(const U& a, unsigned w) { return uand(a, mask(w)); }
 unsigned bitlen(const U& a) {
@@ -238,7 +248,7 @@ class Seeder {
            const U* soft)
         : N(nodes), nn(nn), pool(pool), vw(widths, widths + nv), soft(soft, soft + nv), nv(nv),
           has_bits(nv, 0), bits_v(nv), bits_m(nv), has_rng(nv, 0), rng_lo(nv), rng_hi(nv),
-          memo(nn), have(nn, 0), users(nn), leaf(nv) {
+          memo(nn), have(nn, 0), users(nn), leaf(nv), hv(nn, -1) {
         for (size_t i = 0; i < nn; i++) {
             const Node& n = N[i];
             for (uint32_t k = 0; k < n.nargs; k++) {
@@ -306,6 +316,9 @@ class Seeder {
     std::vector<U> memo;
     std::vector<char> have;
     std::vector<std::vector<int>> users, leaf;
+    std::vector<signed char> hv;                      // has_var memo: -1 unknown
+    std::vector<int> ev_stack, ch_stack, hv_stack;    // scratch (none of these recurse)
+    std::vector<int> rs_leaves, rs_stack;
 
     // ---- evaluation under the current hint model -------------------------------------
     U value_of_var(int v) {
@@ -332,7 +345,8 @@ class Seeder {
 
     const U& ev(int n) {
         if (have[n]) return memo[n];
-        std::vector<int> stack{n};
+        std::vector<int>& stack = ev_stack;
+        stack.assign(1, n);
         while (!stack.empty()) {
             const int i = stack.back();
             if (have[i]) {
@@ -457,7 +471,8 @@ class Seeder {
     }
 
     void changed(int v) {
-        std::vector<int> stack;
+        std::vector<int>& stack = ch_stack;
+        stack.clear();
         for (int i : leaf[v])
             if (have[i]) stack.push_back(i);
         while (!stack.empty()) {
@@ -635,19 +650,36 @@ class Seeder {
         }
     }
 
-    bool has_var(int n) const {
-        std::vector<int> stack{n};
-        std::vector<char> seen(nn, 0);
+    // does the sub-DAG under n reach a variable leaf?  (memoised: the DAG is immutable)
+    bool has_var(int n) {
+        if (hv[n] >= 0) return hv[n] != 0;
+        std::vector<int>& stack = hv_stack;
+        stack.assign(1, n);
         while (!stack.empty()) {
             const int i = stack.back();
-            stack.pop_back();
-            if (seen[i]) continue;
-            seen[i] = 1;
+            if (hv[i] >= 0) {
+                stack.pop_back();
+                continue;
+            }
             const Node& nd = N[i];
-            if (nd.kind == PFL_K_VAR || nd.kind == PFL_K_BVAR) return true;
-            for (uint32_t k = 0; k < nd.nargs; k++) stack.push_back((int)nd.args[k]);
+            if (nd.kind == PFL_K_VAR || nd.kind == PFL_K_BVAR) {
+                hv[i] = 1;
+                stack.pop_back();
+                continue;
+            }
+            bool pend = false;
+            for (uint32_t k = 0; k < nd.nargs; k++)
+                if (hv[nd.args[k]] < 0) {
+                    stack.push_back((int)nd.args[k]);
+                    pend = true;
+                }
+            if (pend) continue;
+            stack.pop_back();
+            char r = 0;
+            for (uint32_t k = 0; k < nd.nargs; k++) r |= hv[nd.args[k]];
+            hv[i] = r;
         }
-        return false;
+        return hv[n] != 0;
     }
 
     // ---- W interval desires -------------------------------------------------------------
@@ -672,8 +704,8 @@ class Seeder {
         }
         if (nd.kind == PF_W_ITE) {
             const int c = (int)nd.args[0], a = (int)nd.args[1], b = (int)nd.args[2];
-            alternatives({[&] { want_bool(c, true); want_range(a, lo, hi); },
-                          [&] { want_bool(c, false); want_range(b, lo, hi); }});
+            alternatives([&] { want_bool(c, true); want_range(a, lo, hi); },
+                         [&] { want_bool(c, false); want_range(b, lo, hi); });
             return;
         }
         if (nd.kind == PF_W_ADD || nd.kind == PF_W_SUB) {
@@ -700,8 +732,8 @@ class Seeder {
         } else if (scmp(shi, S()) < 0) {
             want_range(n, sadd(slo, S::pow2(w)), sadd(shi, S::pow2(w)));
         } else {
-            alternatives({[&] { want_range(n, S(), shi); },
-                          [&] { want_range(n, sadd(slo, S::pow2(w)), S::of(mask(w))); }});
+            alternatives([&] { want_range(n, S(), shi); },
+                         [&] { want_range(n, sadd(slo, S::pow2(w)), S::of(mask(w))); });
         }
     }
 
@@ -821,18 +853,21 @@ class Seeder {
         const int c = (int)nd.args[0], a = (int)nd.args[1], b = (int)nd.args[2];
         U ca, cb;
         const bool ha = cst(a, &ca), hb = cst(b, &cb);
-        std::function<void()> alt_a = [&] { want_bool(c, true); want_val(a, val, msk); };
-        std::function<void()> alt_b = [&] { want_bool(c, false); want_val(b, val, msk); };
+        auto alt_a = [&] { want_bool(c, true); want_val(a, val, msk); };
+        auto alt_b = [&] { want_bool(c, false); want_val(b, val, msk); };
         const bool cur = truth(c);
+        bool a_first;
         if (uand(uxor(ev(n), val), msk).zero()) {
-            cur ? alternatives({alt_a, alt_b}) : alternatives({alt_b, alt_a});
+            a_first = cur;
         } else if (hb && uand(uxor(cb, val), msk).zero() && !(ha && uand(uxor(ca, val), msk).zero())) {
-            alternatives({alt_b, alt_a});
+            a_first = false;
         } else if (ha && uand(uxor(ca, val), msk).zero()) {
-            alternatives({alt_a, alt_b});
+            a_first = true;
         } else {
-            cur ? alternatives({alt_a, alt_b}) : alternatives({alt_b, alt_a});
+            a_first = cur;
         }
+        if (a_first) alternatives(alt_a, alt_b);
+        else alternatives(alt_b, alt_a);
     }
 
     struct Snap {
@@ -870,11 +905,14 @@ class Seeder {
         }
     }
 
-    void alternatives(const std::vector<std::function<void()>>& alts) {
-        for (const auto& alt : alts)
-            if (try_(alt)) return;
-        if (force && !alts.empty()) {
-            alts[0]();
+    // First alternative that applies without a conflict wins; under `force` the first one is
+    // applied regardless.  Variadic (no std::function / vector allocation per choice).
+    template <typename F0, typename... Fs>
+    void alternatives(F0&& f0, Fs&&... fs) {
+        if (try_(f0)) return;
+        if ((try_(fs) || ...)) return;
+        if (force) {
+            f0();
             return;
         }
         throw Conflict{};
@@ -887,7 +925,9 @@ class Seeder {
         const uint32_t* a = nd.args;
         if (k == PF_B_AND || k == PF_B_OR) {
             // one conjunct / disjunct over the flattened tree, in left-to-right order
-            std::vector<int> leaves, stack{n};
+            std::vector<int>&leaves = rs_leaves, &stack = rs_stack;  // resolve() does not nest
+            leaves.clear();
+            stack.assign(1, n);
             while (!stack.empty()) {
                 const int i = stack.back();
                 stack.pop_back();
@@ -897,16 +937,20 @@ class Seeder {
                     leaves.push_back(i);
                 }
             }
-            std::vector<std::function<void()>> alts;
-            for (int x : leaves) alts.push_back([this, x, v] { want_bool(x, v); });
-            alternatives(alts);
+            for (int x : leaves)
+                if (try_([&] { want_bool(x, v); })) return;
+            if (force && !leaves.empty()) {
+                want_bool(leaves[0], v);
+                return;
+            }
+            throw Conflict{};
         } else if (k == PF_B_XOR) {
-            alternatives({[&] { want_bool((int)a[0], v); want_bool((int)a[1], false); },
-                          [&] { want_bool((int)a[0], !v); want_bool((int)a[1], true); }});
+            alternatives([&] { want_bool((int)a[0], v); want_bool((int)a[1], false); },
+                         [&] { want_bool((int)a[0], !v); want_bool((int)a[1], true); });
         } else if (k == PF_B_ITE) {
             const int c = (int)a[0], p = (int)a[1], q = (int)a[2];
-            alternatives({[&] { want_bool(c, true); want_bool(p, v); },
-                          [&] { want_bool(c, false); want_bool(q, v); }});
+            alternatives([&] { want_bool(c, true); want_bool(p, v); },
+                         [&] { want_bool(c, false); want_bool(q, v); });
         } else if (k == PF_B_EQ) {
             const int x = (int)a[0], y = (int)a[1];
             const unsigned w = nd.width;
@@ -914,9 +958,9 @@ class Seeder {
                 want_eqw(x, y, 0);
             } else {
                 const U vx = ev(x), vy = ev(y);
-                alternatives({[&] { want_val(x, uxor(vx, U::of(1)), mask(w)); },
-                              [&] { want_val(y, uxor(vy, U::of(1)), mask(w)); },
-                              [&] { want_val(x, uxor(vx, shl(U::of(1), w - 1)), mask(w)); }});
+                alternatives([&] { want_val(x, uxor(vx, U::of(1)), mask(w)); },
+                             [&] { want_val(y, uxor(vy, U::of(1)), mask(w)); },
+                             [&] { want_val(x, uxor(vx, shl(U::of(1), w - 1)), mask(w)); });
             }
         } else if (k == PF_B_ULT || k == PF_B_ULE || k == PF_B_SLT || k == PF_B_SLE) {
             int x = (int)a[0], y = (int)a[1];
@@ -929,12 +973,12 @@ class Seeder {
             }
             const int strict = (k == PF_B_ULT || k == PF_B_SLT) ? 1 : 0;
             if (k == PF_B_ULT || k == PF_B_ULE) {
-                alternatives({[&] { want_range(x, S(), ssub(S::of(vy), ssmall(strict))); },
-                              [&] { want_range(y, sadd(S::of(vx), ssmall(strict)), S::of(mask(w))); }});
+                alternatives([&] { want_range(x, S(), ssub(S::of(vy), ssmall(strict))); },
+                             [&] { want_range(y, sadd(S::of(vx), ssmall(strict)), S::of(mask(w))); });
             } else {
-                alternatives({[&] { want_srange(x, sneg(S::pow2(w - 1)), ssub(sgn(vy, w), ssmall(strict))); },
-                              [&] { want_srange(y, sadd(sgn(vx, w), ssmall(strict)),
-                                                ssub(S::pow2(w - 1), ssmall(1))); }});
+                alternatives([&] { want_srange(x, sneg(S::pow2(w - 1)), ssub(sgn(vy, w), ssmall(strict))); },
+                             [&] { want_srange(y, sadd(sgn(vx, w), ssmall(strict)),
+                                               ssub(S::pow2(w - 1), ssmall(1))); });
             }
         } else {
             want_bool(n, v);
@@ -955,26 +999,26 @@ class Seeder {
             return;
         }
         const Node &nx = N[x], &ny = N[y];
-        std::vector<std::function<void()>> alts;
-        if (depth < 8 && nx.kind == ny.kind && nx.aux == ny.aux && nx.width == ny.width &&
-            nx.nargs == ny.nargs && nx.kind != PFL_K_VAR && nx.kind != PFL_K_CONST) {
-            alts.push_back([&, depth] {
-                for (uint32_t i = 0; i < nx.nargs; i++) {
-                    const int a = (int)nx.args[i], b = (int)ny.args[i];
-                    if (a == b) continue;
-                    if (N[a].is_bool) {
-                        U dummy;
-                        if (!cst(b, &dummy)) want_bool(a, truth(b));
-                    } else {
-                        want_eqw(a, b, depth + 1);
-                    }
+        const bool structural = depth < 8 && nx.kind == ny.kind && nx.aux == ny.aux &&
+                                nx.width == ny.width && nx.nargs == ny.nargs &&
+                                nx.kind != PFL_K_VAR && nx.kind != PFL_K_CONST;
+        auto by_args = [&] {
+            for (uint32_t i = 0; i < nx.nargs; i++) {
+                const int a = (int)nx.args[i], b = (int)ny.args[i];
+                if (a == b) continue;
+                if (N[a].is_bool) {
+                    U dummy;
+                    if (!cst(b, &dummy)) want_bool(a, truth(b));
+                } else {
+                    want_eqw(a, b, depth + 1);
                 }
-            });
-        }
+            }
+        };
         const U vx = ev(x), vy = ev(y);
-        alts.push_back([&, vy] { want_val(x, vy, mask(w)); });
-        alts.push_back([&, vx] { want_val(y, vx, mask(w)); });
-        alternatives(alts);
+        auto x_to_y = [&] { want_val(x, vy, mask(w)); };
+        auto y_to_x = [&] { want_val(y, vx, mask(w)); };
+        if (structural) alternatives(by_args, x_to_y, y_to_x);
+        else alternatives(x_to_y, y_to_x);
     }
 
     void drain() {
