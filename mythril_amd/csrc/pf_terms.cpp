@@ -1057,14 +1057,91 @@ struct Lowering {
         int32_t val = mkvar(vname, rng, VarTerm{PFLT_VT_SELECT, arr, idx, 0}, nullptr, &rd);
         auto& entries = arrays[name];
         const auto xf = offset_form(idx);
+        // runs: entries next to each other in lookup order with one base other than idx's
+        // (constants: NO_BASE) — distinct offsets, so at most one of them can match
+        std::vector<RunEntry> run;
+        uint32_t run_base = 0;
         for (size_t i = entries.size(); i-- > 0;) {
             const auto& e = entries[i];
             const auto ef = offset_form((uint32_t)e[0]);
             if (ef.first == xf.first && !(ef.second == xf.second)) continue;  // never aliases
-            val = d.op(PF_W_ITE, rng, {d.op(PF_B_EQ, width(idx), {inode, e[2]}), e[3], val});
+            if (ef.first == xf.first) {
+                val = index_run(run, run_base, idx, inode, rng, val);
+                run.clear();
+                val = d.op(PF_W_ITE, rng, {d.op(PF_B_EQ, width(idx), {inode, e[2]}), e[3], val});
+                continue;
+            }
+            if (!run.empty() && ef.first != run_base) {
+                val = index_run(run, run_base, idx, inode, rng, val);
+                run.clear();
+            }
+            run_base = ef.first;
+            run.push_back({ef.second, e[2], e[3]});
         }
+        val = index_run(run, run_base, idx, inode, rng, val);
         entries.push_back({(int32_t)idx, (int32_t)arr, inode, val});
         return val;
+    }
+
+    // TermLowering._run / _window: a run of indices base + c of a byte array, contiguous in
+    // 8..32-long pieces, read through one window lookup per piece; short runs and pieces
+    // stay ite(idx == base + c, v_c, ...) chains in lookup order
+    struct RunEntry {
+        C8 c;
+        int32_t inn, v;
+    };
+    static constexpr size_t WINDOW_MIN = 8;
+    static bool c8_less(const C8& a, const C8& b) {
+        for (int i = 7; i >= 0; i--)
+            if (a.l[i] != b.l[i]) return a.l[i] < b.l[i];
+        return false;
+    }
+    static bool c8_succ(const C8& a, const C8& b) {  // b == a + 1 (no wrap: b > a)
+        C8 x = a;
+        for (int i = 0; i < 8; i++)
+            if (++x.l[i] != 0) break;
+        return x == b && c8_less(a, b);
+    }
+    int32_t index_run(const std::vector<RunEntry>& run, uint32_t base, uint32_t idx, int32_t inode, uint32_t rng,
+                      int32_t val) {
+        bool dup = false;
+        std::vector<RunEntry> items(run);
+        std::stable_sort(items.begin(), items.end(),
+                         [](const RunEntry& a, const RunEntry& b) { return c8_less(a.c, b.c); });
+        for (size_t i = 1; i < items.size(); i++) dup |= items[i].c == items[i - 1].c;
+        if (run.size() < WINDOW_MIN || rng != 8 || width(idx) != 256 || dup) {
+            for (const RunEntry& e : run)
+                val = d.op(PF_W_ITE, rng, {d.op(PF_B_EQ, width(idx), {inode, e.inn}), e.v, val});
+            return val;
+        }
+        size_t i = 0;
+        while (i < items.size()) {
+            size_t j = i + 1;
+            while (j < items.size() && c8_succ(items[j - 1].c, items[j].c) && j - i < 32) j++;
+            if (j - i < WINDOW_MIN) {
+                for (size_t k = i; k < j; k++)
+                    val = d.op(PF_W_ITE, rng, {d.op(PF_B_EQ, width(idx), {inode, items[k].inn}), items[k].v, val});
+            } else {
+                val = window(items, i, j, base == NO_BASE, inode, val);
+            }
+            i = j;
+        }
+        return val;
+    }
+    int32_t window(const std::vector<RunEntry>& items, size_t i, size_t j, bool const_base, int32_t inode,
+                   int32_t val) {
+        const uint32_t n = (uint32_t)(j - i);
+        int32_t acc = items[i].v;
+        for (uint32_t k = 1; k < n; k++) acc = d.op(PF_W_CONCAT, 8 * (k + 1), {items[i + k].v, acc}, 8 * k);
+        const C8& lo = items[i].c;
+        bool lo_zero = true;
+        for (int k = 0; k < 8; k++) lo_zero &= lo.l[k] == 0;
+        // idx - (base + lo): the piece's lowest index node
+        const int32_t t = const_base && lo_zero ? inode : d.op(PF_W_SUB, 256, {inode, items[i].inn});
+        const int32_t hit = d.op(PF_B_ULT, 256, {t, d.cnst(n, 256)});
+        const int32_t amt = d.op(PF_W_EXTRACT, 8 * n, {d.op(PF_W_SHL, 256, {t, d.cnst(3, 256)})}, 0);
+        const int32_t byte = d.op(PF_W_EXTRACT, 8, {d.op(PF_W_LSHR, 8 * n, {acc, amt})}, 0);
+        return d.op(PF_W_ITE, 8, {hit, byte, val});
     }
 
     static std::string big_decimal(const Big& v) {

@@ -50,6 +50,8 @@ ACTORS = (
     0xAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAA,  # SOMEGUY
 )
 KECCAK_MASK_BITS = 117
+_WINDOW_MIN = 8   # runs of a byte array's indices this long become window lookups
+_NO_RUN = object()
 
 
 @dataclass
@@ -489,13 +491,71 @@ class TermLowering:
         val = self._var(vname, rng, sel_term)
         # first earlier index with an equal value wins (consistent array interpretation)
         ib, ic = self._offset_form(idx)
+        # runs: entries next to each other in lookup order with one base other than idx's
+        # (constants: base None) — distinct offsets, so at most one of them can match
+        run: List[Tuple[int, int, object]] = []
+        run_base: object = _NO_RUN
         for (it, _, inn, v) in reversed(entries):
             tb, tc = self._offset_form(it)
             if tb is ib and tc != ic:
                 continue  # the same base at another offset (distinct constants) never aliases
-            val = d.op(ir.W_ITE, rng, d.op(ir.B_EQ, idx.width, inode, inn), v, val)
+            if tb is ib:
+                val = self._run(run, run_base, idx, inode, rng, val)
+                run, run_base = [], _NO_RUN
+                val = d.op(ir.W_ITE, rng, d.op(ir.B_EQ, idx.width, inode, inn), v, val)
+                continue
+            if run and tb is not run_base:
+                val = self._run(run, run_base, idx, inode, rng, val)
+                run = []
+            run_base = tb
+            run.append((tc, inn, v))
+        val = self._run(run, run_base, idx, inode, rng, val)
         entries.append((idx, sel_term, inode, val))
         return val
+
+    def _run(self, run, base, idx: T.Term, inode: int, rng: int, val):
+        """The part of a read's ``ite`` chain that tests a run of indices base + c (entries
+        next to each other in lookup order, so at most one of them can match and their order
+        is free).  Short runs stay ``ite(idx == base + c, v_c, ...)`` in lookup order.  A byte
+        array's contiguous offsets c .. c + n - 1 (8 <= n <= 32: LASER's calldata header and
+        ABI words at a constant or a symbolic offset, calldata.py:233-246) become one window
+        lookup per read: the n bytes concatenated (v_c lowest), shifted right by
+        8 * (idx - (base + c)) and cut to a byte, selected when that difference is < n — a
+        dozen nodes instead of 4 * n, the same value for every assignment (the single
+        query's longest programs are these chains: DESIGN.md §6)."""
+        d = self.dag
+        if (len(run) < _WINDOW_MIN or rng != 8 or idx.width != 256
+                or len({e[0] for e in run}) != len(run)):
+            for (_, inn, v) in run:
+                val = d.op(ir.W_ITE, rng, d.op(ir.B_EQ, idx.width, inode, inn), v, val)
+            return val
+        items = sorted(run, key=lambda e: e[0])
+        i = 0
+        while i < len(items):
+            j = i + 1
+            while j < len(items) and items[j][0] == items[j - 1][0] + 1 and j - i < 32:
+                j += 1
+            piece = items[i:j]
+            if len(piece) < _WINDOW_MIN:
+                for (_, inn, v) in piece:
+                    val = d.op(ir.W_ITE, rng, d.op(ir.B_EQ, idx.width, inode, inn), v, val)
+            else:
+                val = self._window(piece, base is None, inode, val)
+            i = j
+        return val
+
+    def _window(self, piece, const_base: bool, inode: int, val) -> int:
+        d = self.dag
+        lo, n = piece[0][0], len(piece)
+        acc = piece[0][2]
+        for j in range(1, n):
+            acc = d.op(ir.W_CONCAT, 8 * (j + 1), piece[j][2], acc, aux=8 * j)
+        # idx - (base + lo): the piece's lowest index node
+        t = inode if const_base and lo == 0 else d.op(ir.W_SUB, 256, inode, piece[0][1])
+        hit = d.op(ir.B_ULT, 256, t, d.const(n, 256))
+        amt = d.op(ir.W_EXTRACT, 8 * n, d.op(ir.W_SHL, 256, t, d.const(3, 256)), aux=0)
+        byte = d.op(ir.W_EXTRACT, 8, d.op(ir.W_LSHR, 8 * n, acc, amt), aux=0)
+        return d.op(ir.W_ITE, 8, hit, byte, val)
 
     # ---- uninterpreted functions --------------------------------------------------------
     def _hash_args(self, args, salt) -> int:

@@ -259,3 +259,80 @@ def test_reads_at_one_base_and_distinct_offsets_need_no_alias_test():
         agree += got == want
         sat += want
     assert agree == 300 and sat > 0
+
+
+def _window_terms():
+    """A dynamic-ABI shape with long index runs: calldata bytes 0..39 read at constant
+    indices (a 40-byte run: a 32-byte window piece and an 8-byte one), a word read at
+    x + 4 + k (k = 0..31), a word at another symbolic base y + k compared against both, and a
+    constant index read after the symbolic ones (a run of one base: a window too)."""
+    from mythril_amd.smt import terms as T
+
+    cd = T.array("1_calldata", 256, 8)
+    hdr = [T.select(cd, T.const(i, 256)) for i in range(40)]
+    x = T.var("x", 256)
+    y = T.var("y", 256)
+    wx = T.concat(*[T.select(cd, T.binop("bvadd", T.binop("bvadd", x, T.const(4, 256)), T.const(k, 256)))
+                    for k in range(32)])
+    wy = T.concat(*[T.select(cd, T.binop("bvadd", y, T.const(k, 256))) for k in range(32)])
+    late = T.select(cd, T.const(70, 256))
+    cs = [T.cmp("bvult", T.const(3, 256), T.concat(*hdr[4:36])),
+          T.eq(hdr[0], T.const(0xA9, 8)),
+          T.cmp("bvult", T.const(5, 256), wx),
+          T.cmp("bvule", wy, wx),
+          T.eq(late, T.const(7, 8))]
+    return cs, wx, wy, late
+
+
+_WINDOW_X = [0, 1, 3, 4, 8, 31, 32, 33, 35, 36, 39, 40, 66, 70, 100, (1 << 256) - 1, (1 << 256) - 4,
+             (1 << 256) - 5, (1 << 256) - 31, (1 << 256) - 32, (1 << 256) - 40]
+
+
+def test_index_runs_become_window_lookups_with_the_same_values(monkeypatch):
+    """Runs of >= 8 contiguous indices of a byte array with one base (constants, or one
+    symbolic base) are read through a window lookup — concat, shift by 8 * (idx - lo), byte
+    — instead of an ite(idx == lo + j) chain: every read and every constraint takes the
+    chain's value on every assignment, including indices that hit a run partially, wrap
+    around 2^256, or fall between the pieces; the program, the host Witness and the oracle
+    agree; and the DAG has a fraction of the chain's comparisons."""
+    from dag_eval import eval_dag_values
+    from mythril_amd.smt import to_dag
+    from mythril_amd.smt.interp import Witness
+    from mythril_amd.smt.to_dag import TermLowering, UFRegistry
+
+    cs, wx, wy, late = _window_terms()
+    win = TermLowering(UFRegistry())
+    lw = win.lower(cs)
+    monkeypatch.setattr(to_dag, "_WINDOW_MIN", 1 << 30)
+    chain = TermLowering(UFRegistry())
+    lc = chain.lower(cs)
+    monkeypatch.undo()
+    n_eq = [sum(n.kind == ir.B_EQ for n in lo.dag.nodes) for lo in (lw, lc)]
+    assert sum(n.kind == ir.W_LSHR for n in lw.dag.nodes) >= 64 + 1
+    assert n_eq[0] * 10 < n_eq[1], n_eq
+    assert [v.name for v in lw.dag.vars] == [v.name for v in lc.dag.vars]
+    reads = [win.memo.get(t) for t in (wx, wy, late)]
+    reads_c = [chain.memo.get(t) for t in (wx, wy, late)]
+    prog = lower(lw.dag)
+    sv = O.SetView.from_batch(ir.Batch([prog]), 0)
+    rng = random.Random(17)
+    sat = 0
+    for trial in range(400):
+        vals = []
+        for v in lw.dag.vars:
+            if v.width == 256:
+                vals.append(rng.choice(_WINDOW_X + [rng.getrandbits(256)]))
+            else:
+                vals.append(rng.choice((0, 5, 7, 0xA9, rng.getrandbits(8))))
+        if trial % 4 == 0:   # y at x + 4 + d: the two symbolic runs overlap
+            vals[[v.name for v in lw.dag.vars].index("y")] = (vals[[v.name for v in lw.dag.vars].index("x")]
+                                                             + 4 + rng.randrange(-33, 34)) % (1 << 256)
+        vw, vc = eval_dag_values(lw.dag, vals), eval_dag_values(lc.dag, vals)
+        for a, b in zip(reads, reads_c):
+            assert vw[a] == vc[b], trial
+        for a, b in zip(lw.dag.roots, lc.dag.roots):
+            assert vw[a] == vc[b], trial
+        want = sv.evaluate(vals)
+        assert all(bool(Witness(lw, vals, UFRegistry()).ev(c)) for c in cs) == want
+        sat += want
+    assert sat > 0

@@ -118,6 +118,19 @@ def test_corpus_programs_match(corpus_buckets):
         _compare_program(b, reg, hints=False)
 
 
+def test_window_lookups_match():
+    """Index runs read through window lookups (to_dag.TermLowering._run): constant and
+    symbolic-base runs, pieces of 32 and of 8, a constant read after symbolic ones — the
+    native lowering builds the same nodes, hints and program."""
+    from test_lowering import _window_terms
+
+    cs = _window_terms()[0]
+    lo = _compare_dag(cs, UFRegistry())
+    assert lo is not None and sum(n.kind == ir.W_LSHR for n in lo.dag.nodes) > 64
+    _compare_program(cs, UFRegistry(), hints=True)
+    _compare_program(cs, UFRegistry(), hints=False)
+
+
 def test_parent_models_match(corpus_buckets):
     """Parents by symbol name and by array read (gpu_check._recent_parent's two key kinds)."""
     reg, bks = corpus_buckets
