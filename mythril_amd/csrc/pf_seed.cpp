@@ -566,7 +566,12 @@ class Seeder {
             want_val(a[0], neg(val), msk);
         } else if (k == PF_W_LSHR || k == PF_W_SHL || k == PF_W_UDIV) {
             U c;
-            if (!cst(a[1], &c)) return;
+            if (!cst(a[1], &c)) {
+                if (k == PF_W_UDIV) return;
+                // a shift by a computed amount (a window lookup's byte, to_dag._window):
+                // propagate through the amount's current value
+                c = ev((int)a[1]);
+            }
             unsigned cs;
             if (k == PF_W_UDIV) {
                 if (c.zero()) return;

@@ -252,7 +252,11 @@ class Seeder:
         elif k in (ir.W_LSHR, ir.W_SHL, ir.W_UDIV):
             c = self._const(a[1])
             if c is None:
-                return
+                if k == ir.W_UDIV:
+                    return
+                # a shift by a computed amount (a window lookup's byte, to_dag._window):
+                # propagate through the amount's current value
+                c = self.ev(a[1])
             if k == ir.W_UDIV:
                 if c == 0:
                     return
