@@ -150,8 +150,29 @@ U mul(const U& a, const U& b) {
     return lo;
 }
 void divmod(const U& a, const U& b, U* q, U* r) {  // b != 0
-    U Q, R;
-    for (int k = (int)bitlen(a) - 1; k >= 0; k--) {
+    if (lt(a, b)) {
+        *q = U();
+        *r = a;
+        return;
+    }
+    if (!(b.w[1] | b.w[2] | b.w[3])) {  // one-limb divisor: 128/64 steps
+        const uint64_t d = b.w[0];
+        U Q;
+        unsigned __int128 rem = 0;
+        for (int i = 3; i >= 0; i--) {
+            const unsigned __int128 cur = (rem << 64) | a.w[i];
+            Q.w[i] = (uint64_t)(cur / d);
+            rem = cur % d;
+        }
+        *q = Q;
+        *r = U::of((uint64_t)rem);
+        return;
+    }
+    // restoring division from the first quotient bit that can be set (the bits of a above
+    // it are below b)
+    const int k0 = (int)bitlen(a) - (int)bitlen(b);
+    U Q, R = shr(a, (unsigned)k0 + 1u);
+    for (int k = k0; k >= 0; k--) {
         R = shl(R, 1);
         if (bit(a, (unsigned)k)) R.w[0] |= 1;
         if (!lt(R, b)) {

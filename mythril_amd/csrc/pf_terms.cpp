@@ -977,7 +977,14 @@ struct Lowering {
     // (base NO_BASE for a constant): TermLowering._offset_form — indices with one base and
     // different offsets never alias
     static constexpr uint32_t NO_BASE = 0xffffffffu;
+    // memoised per term: select() asks for every earlier entry's form on every read
+    mutable std::unordered_map<uint32_t, std::pair<uint32_t, C8>> of_memo;
     std::pair<uint32_t, C8> offset_form(uint32_t t) const {
+        auto it = of_memo.find(t);
+        if (it != of_memo.end()) return it->second;
+        return of_memo.emplace(t, offset_form_of(t)).first->second;
+    }
+    std::pair<uint32_t, C8> offset_form_of(uint32_t t) const {
         const uint32_t w = width(t);
         uint32_t c[8] = {0};
         auto addsub = [&](const Big& v, bool sub) {
@@ -1104,16 +1111,18 @@ struct Lowering {
     }
     int32_t index_run(const std::vector<RunEntry>& run, uint32_t base, uint32_t idx, int32_t inode, uint32_t rng,
                       int32_t val) {
+        auto chain = [&]() {
+            for (const RunEntry& e : run)
+                val = d.op(PF_W_ITE, rng, {d.op(PF_B_EQ, width(idx), {inode, e.inn}), e.v, val});
+            return val;
+        };
+        if (run.size() < WINDOW_MIN || rng != 8 || width(idx) != 256) return chain();
         bool dup = false;
         std::vector<RunEntry> items(run);
         std::stable_sort(items.begin(), items.end(),
                          [](const RunEntry& a, const RunEntry& b) { return c8_less(a.c, b.c); });
         for (size_t i = 1; i < items.size(); i++) dup |= items[i].c == items[i - 1].c;
-        if (run.size() < WINDOW_MIN || rng != 8 || width(idx) != 256 || dup) {
-            for (const RunEntry& e : run)
-                val = d.op(PF_W_ITE, rng, {d.op(PF_B_EQ, width(idx), {inode, e.inn}), e.v, val});
-            return val;
-        }
+        if (dup) return chain();
         size_t i = 0;
         while (i < items.size()) {
             size_t j = i + 1;
@@ -1519,24 +1528,27 @@ Result* lower_job(const Store& S, const std::vector<uint32_t>& rs, const Parents
             bool have_narrow = false;
             std::vector<uint32_t> n_code, n_consts;
             size_t n_spill_narrow = 0;
+            // output scratch per thread, grown but never cleared (pfl_lower writes what it
+            // reports); the result keeps only the words written
+            thread_local std::vector<uint32_t> code_buf, const_buf;
             for (int ti = 0; ti < 2; ti++) {
                 size_t cap_i = 16 * d.nodes.size() + 64 + 4 * d.roots.size();
                 size_t cap_c = R->pool.size() / 8 + d.forced.size() + 1;
                 size_t ni = 0, nc = 0;
                 for (int attempt = 0; attempt < 4; attempt++) {
-                    R->code.assign(4 * cap_i, 0u);
-                    R->consts.assign(8 * cap_c, 0u);
+                    if (code_buf.size() < 4 * cap_i) code_buf.resize(4 * cap_i);
+                    if (const_buf.size() < 8 * cap_c) const_buf.resize(8 * cap_c);
                     rc = pfl_lower(R->packed_nodes.data(), d.nodes.size(), R->pool.data(), R->pool.size() / 8,
                                    roots2.data(), d.roots.size(), forced.empty() ? nullptr : forced.data(),
-                                   d.forced.size(), tries[ti], R->code.data(), cap_i, &ni, R->consts.data(),
+                                   d.forced.size(), tries[ti], code_buf.data(), cap_i, &ni, const_buf.data(),
                                    cap_c, &nc);
                     if (rc != -3) break;
                     cap_i *= 4;
                     cap_c *= 4;
                 }
                 if (rc == 0) {
-                    R->code.resize(4 * ni);
-                    R->consts.resize(8 * nc);
+                    R->code.assign(code_buf.begin(), code_buf.begin() + 4 * ni);
+                    R->consts.assign(const_buf.begin(), const_buf.begin() + 8 * nc);
                     size_t n_spill = 0;
                     for (size_t i = 0; i < ni; i++) {
                         const uint32_t op = R->code[4 * i] & 0xffu;
