@@ -129,6 +129,15 @@ def discharge(args):
                    gpu_check.STATS.host_s - s0[2])
     bucket_origin = dict(gpu_check.STATS.bucket_origin)
     phase_s = {k: round(v, 4) for k, v in gpu_check.STATS.phase_s.items()}
+    # the same corpus again with the answer caches cleared: its terms are now in the native
+    # store with their bucket keys memoised — a live analysis's steady state, where each new
+    # query shares all but its newest conjunct with earlier ones (the figure above is cold)
+    gpu_check.reset_cache()
+    gpu_check.STATS.phase_s.clear()
+    t3 = time.perf_counter()
+    gpu_check.check_sets([q.constraints for q in c.queries], registry=c.kfm.registry)
+    t_rep = time.perf_counter() - t3
+    phase_rep = {k: round(v, 4) for k, v in gpu_check.STATS.phase_s.items()}
     # soundness slice: UNSAT by construction, never answered sat
     unsat = corpus.labelled_unsat(c, n=256)
     fps = []
@@ -201,6 +210,7 @@ def discharge(args):
             "phase_s": phase_s, "lowering_workers": n_workers, "pool_start_s": round(t_pool, 3),
             "wall_s": t2 - t1, "corpus_build_s": t1 - t0,
             "queries_per_s": n / max(t2 - t1, 1e-9),
+            "queries_per_s_terms_known": n / max(t_rep, 1e-9), "phase_s_terms_known": phase_rep,
             "corpus": f"mythril_amd/corpus.py, {args.corpus_scenarios} planted 2-tx scenarios "
                       f"(config-2 substitute: no z3/solc for --solver-log dumps)"}
 
