@@ -220,6 +220,34 @@ def _set_seed(constraints: Sequence[T.Term]) -> int:
 _NATIVE_TERMS = os.environ.get("PF_NATIVE_TERMS", "1") != "0"
 
 
+def _witness_limbs(eng, db, mine: List[int], base: int, progs, found, seed_: int) -> np.ndarray:
+    """The witnesses' variables as limb rows, in ``mine`` order.  A witness at candidate 0 of
+    a program whose variables all carry parent values is those values (the generator keeps
+    them at candidate 0: native_terms.candidate0_limbs), so only the other witnesses are
+    materialised on the device — for a single query whose hint model holds, no second
+    launch."""
+    from . import native_terms
+
+    parts: List[Optional[np.ndarray]] = []
+    need = []
+    for k in mine:
+        rows = native_terms.candidate0_limbs(progs[k]) if int(found[k]) == 0 else None
+        parts.append(rows)
+        if rows is None:
+            need.append(k)
+    if need:
+        got = eng.materialize_limbs(db, [k - base for k in need], [int(found[k]) for k in need], seed=seed_)
+        o = 0
+        it = iter(need)
+        for j, rows in enumerate(parts):
+            if rows is None:
+                k = next(it)
+                nv = int(db.batch.descs[k - base][5])
+                parts[j] = got[o:o + nv]
+                o += nv
+    return np.concatenate(parts) if parts else np.zeros((0, 8), dtype=np.uint32)
+
+
 def _native_batch() -> bool:
     """check_sets' native pipeline (libpflower.so batch entry points): buckets lowered on
     host threads, packed, re-checked and recorded in C++ — no Python term decoding."""
@@ -468,7 +496,7 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
                 sids, cids = [k - base for k in mine], [int(res.found[k]) for k in mine]
                 if nat:
                     if hasattr(eng, "materialize_limbs"):
-                        rows = eng.materialize_limbs(db, sids, cids, seed=cfg.seed)
+                        rows = _witness_limbs(eng, db, mine, base, progs, res.found, cfg.seed)
                     else:
                         rows = ir.limbs_array([x for vs in eng.materialize(db, sids, cids, seed=cfg.seed)
                                                for x in vs])

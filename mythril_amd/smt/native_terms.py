@@ -449,6 +449,26 @@ class NativeLowered:
     array_reads = property(lambda self: self._get().array_reads)
 
 
+def candidate0_limbs(prog) -> Optional[np.ndarray]:
+    """Candidate 0 of a native program whose every variable has a parent value (the host
+    hint model or a parent state's model), as materialize_limbs rows: the generator keeps
+    every parented variable's parent at candidate 0, masked to its width
+    (include/pf_bytecode.h; ``pf::gen_var``).  None when some variable has no parent (the
+    generator then draws it): such witnesses are materialised on the device."""
+    r = getattr(prog, "native_result", None)
+    if r is None:
+        return None
+    nv = int(r.info[0])
+    if nv == 0:
+        return np.zeros((0, 8), dtype=np.uint32)
+    rows = r.get(GET_VARS, nv, 13)
+    if not rows[:, 4].all():
+        return None
+    bits = np.clip(rows[:, :1].astype(np.int64) - 32 * np.arange(8, dtype=np.int64), 0, 32)
+    masks = ((np.int64(1) << bits) - 1).astype(np.uint32)   # 32 bits: 2^32 - 1
+    return rows[:, 5:13] & masks
+
+
 class NativeProgram(ir.PackedProgram):
     """ir.PackedProgram of a native result: the batch is packed natively from the result
     (pack_batch); instructions, constants and variables are decoded only when read."""

@@ -50,6 +50,12 @@ class OracleEngine:
     def keccak256(self, messages):
         return [O.keccak256(bytes(m)) for m in messages]
 
+    def materialize_limbs(self, db, set_ids, cand_ids, seed=0):
+        """Engine.materialize_limbs: the (set, candidate) pairs' variables as limb rows."""
+        self.materialized = getattr(self, "materialized", 0) + len(set_ids)
+        vals = [x for vs in self.materialize(db, set_ids, cand_ids, seed) for x in vs]
+        return ir.limbs_array(vals) if vals else np.zeros((0, 8), dtype=np.uint32)
+
     def materialize(self, db, set_ids, cand_ids, seed=0):
         out = []
         for s, c in zip(set_ids, cand_ids):

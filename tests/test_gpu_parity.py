@@ -400,3 +400,27 @@ def test_window_lookup_programs(engine):
             w = _oracle_first(p, budget, seed)
             g = None if res.found[i] == 0xFFFFFFFF else int(res.found[i])
             assert g == w, (flags, i, g, w)
+
+
+def test_candidate0_limbs_match_device_materialize(engine):
+    """The host rows gpu_check reads for a witness at candidate 0 of a fully parented program
+    (native_terms.candidate0_limbs) are what pf_materialize returns for candidate 0, under
+    several seeds (the candidate-0 rule does not depend on the seed)."""
+    from test_lowering import _window_terms
+
+    from mythril_amd.smt import native_terms as NT
+    from mythril_amd.smt.to_dag import UFRegistry
+
+    if NT.batch_api() is None:
+        pytest.skip("libpflower.so without the batch API")
+    cs, wx, wy, late = _window_terms()
+    buckets_ = [cs, cs[:3], [cs[4]]]
+    res = NT.lower_many([(b, None) for b in buckets_], UFRegistry(), True, [1, 2, 3], 1)
+    progs = [r[1] for r in res if r[2] is None]
+    assert len(progs) == len(buckets_)
+    rows = [NT.candidate0_limbs(p) for p in progs]
+    assert all(r is not None for r in rows)
+    db = engine.upload(progs)
+    for seed in (0, 7, 0xDEAD_BEEF):
+        got = engine.materialize_limbs(db, list(range(len(progs))), [0] * len(progs), seed=seed)
+        assert np.array_equal(got, np.concatenate(rows)), seed

@@ -344,3 +344,30 @@ def test_native_buckets_match(corpus_buckets):
     ]
     for cs in cases:
         assert NT.buckets(cs) == buckets(cs)
+
+
+def test_candidate0_limbs_are_the_generators_candidate_0(corpus_buckets):
+    """native_terms.candidate0_limbs (the host rows gpu_check uses instead of a materialise
+    launch for a witness at candidate 0) equals the generator's candidate 0 (the C oracle's
+    restatement of pf::gen_var) for every hinted program whose variables all carry parents;
+    None when one has no parent."""
+    reg, bks = corpus_buckets
+    n_full = n_none = 0
+    for b in bks[:150]:
+        try:
+            res = NT.lower_many([(b, None)], reg, True, [5], 1)[0]
+        except LoweringError:
+            continue
+        if res[2] is not None:
+            continue
+        prog = res[1]
+        rows = NT.candidate0_limbs(prog)
+        if rows is None:
+            assert not all(v.parent is not None for v in prog.vars)
+            n_none += 1
+            continue
+        sv = O.SetView.from_batch(ir.Batch([prog]), 0)
+        want = sv.gen_assignments(np.array([0], dtype=np.uint64), 0x5EED)[0]
+        assert [ir.from_limbs(r) for r in rows.tolist()] == [int(x) for x in want]
+        n_full += 1
+    assert n_full > 50
