@@ -148,6 +148,11 @@ const char* pflt_last_error(void);
 void pflt_result_free(void* result);
 void pflt_result_info(void* result, uint64_t* info);  /* 17 sizes, see pf_terms.cpp */
 void pflt_result_get(void* result, uint32_t which, uint32_t* out, char* names_out);
+/* Candidate 0 of the result's program when every variable carries a parent value: the
+ * parents masked to their widths, 8 u32 per variable, into out (the generator keeps every
+ * parented variable's parent at candidate 0, pf_bytecode.h).  Returns 1, or 0 (out untouched)
+ * when some variable has no parent.  Replaces a pf_materialize launch for such witnesses. */
+int pflt_result_candidate0(const void* result, uint32_t* out);
 
 /* A stored term, read-only (pointers valid until the next pflt_add). */
 typedef struct pflt_term_view {

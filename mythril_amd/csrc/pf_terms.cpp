@@ -1874,6 +1874,18 @@ void pflt_result_info(void* res, uint64_t* info) {
 /* vars: n_vars x 12 u32 = width, kind, hint0, hint1, has_parent, parent x 8 ... (13 words)
  * var_terms: n x 4; uf_apps: n; reads: n x 2 (array id, index id) + counts per array;
  * code n_ins x 4; consts n_const x 8; nodes n_nodes x 8; pool n_pool x 8; roots; forced x 8 */
+int pflt_result_candidate0(const void* res, uint32_t* out) {
+    const Result* R = (const Result*)res;
+    for (const DVar& v : R->dag.vars)
+        if (!v.has_parent) return 0;
+    for (const DVar& v : R->dag.vars) {
+        const C8 c = c8_of(big_of(v.parent), v.width);
+        memcpy(out, c.l, 32);
+        out += 8;
+    }
+    return 1;
+}
+
 void pflt_result_get(void* res, uint32_t which, uint32_t* out, char* names_out) {
     const Result* R = (const Result*)res;
     switch (which) {

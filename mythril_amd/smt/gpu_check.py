@@ -221,31 +221,23 @@ _NATIVE_TERMS = os.environ.get("PF_NATIVE_TERMS", "1") != "0"
 
 
 def _witness_limbs(eng, db, mine: List[int], base: int, progs, found, seed_: int) -> np.ndarray:
-    """The witnesses' variables as limb rows, in ``mine`` order.  A witness at candidate 0 of
-    a program whose variables all carry parent values is those values (the generator keeps
-    them at candidate 0: native_terms.candidate0_limbs), so only the other witnesses are
-    materialised on the device — for a single query whose hint model holds, no second
-    launch."""
+    """The witnesses' variables as limb rows, in ``mine`` order.  When every witness of the
+    batch is candidate 0 of a program whose variables all carry parent values (a single
+    query whose hint model holds), those values are the rows (the generator keeps them at
+    candidate 0: native_terms.candidate0_limbs) and no materialise launch is made; otherwise
+    one launch materialises them all."""
     from . import native_terms
 
-    parts: List[Optional[np.ndarray]] = []
-    need = []
-    for k in mine:
-        rows = native_terms.candidate0_limbs(progs[k]) if int(found[k]) == 0 else None
-        parts.append(rows)
-        if rows is None:
-            need.append(k)
-    if need:
-        got = eng.materialize_limbs(db, [k - base for k in need], [int(found[k]) for k in need], seed=seed_)
-        o = 0
-        it = iter(need)
-        for j, rows in enumerate(parts):
+    if all(int(found[k]) == 0 for k in mine):
+        parts = []
+        for k in mine:
+            rows = native_terms.candidate0_limbs(progs[k])
             if rows is None:
-                k = next(it)
-                nv = int(db.batch.descs[k - base][5])
-                parts[j] = got[o:o + nv]
-                o += nv
-    return np.concatenate(parts) if parts else np.zeros((0, 8), dtype=np.uint32)
+                break
+            parts.append(rows)
+        else:
+            return np.concatenate(parts) if parts else np.zeros((0, 8), dtype=np.uint32)
+    return eng.materialize_limbs(db, [k - base for k in mine], [int(found[k]) for k in mine], seed=seed_)
 
 
 def _native_batch() -> bool:

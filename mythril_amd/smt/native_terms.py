@@ -84,6 +84,9 @@ def _bind(L):
     L.pflt_result_free.argtypes = [ctypes.c_void_p]
     L.pflt_result_info.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]
     L.pflt_result_get.argtypes = [ctypes.c_void_p, ctypes.c_uint32, _u32p, ctypes.c_char_p]
+    if hasattr(L, "pflt_result_candidate0"):
+        L.pflt_result_candidate0.argtypes = [ctypes.c_void_p, _u32p]
+        L.pflt_result_candidate0.restype = ctypes.c_int
     if hasattr(L, "pflt_lower_many"):
         vp, sz, u32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32
         L.pflt_parent_new.restype = vp
@@ -453,20 +456,16 @@ def candidate0_limbs(prog) -> Optional[np.ndarray]:
     """Candidate 0 of a native program whose every variable has a parent value (the host
     hint model or a parent state's model), as materialize_limbs rows: the generator keeps
     every parented variable's parent at candidate 0, masked to its width
-    (include/pf_bytecode.h; ``pf::gen_var``).  None when some variable has no parent (the
-    generator then draws it): such witnesses are materialised on the device."""
+    (include/pf_bytecode.h; ``pf::gen_var``) — pflt_result_candidate0.  None when some
+    variable has no parent (the generator then draws it)."""
     r = getattr(prog, "native_result", None)
     if r is None:
         return None
     nv = int(r.info[0])
-    if nv == 0:
-        return np.zeros((0, 8), dtype=np.uint32)
-    rows = r.get(GET_VARS, nv, 13)
-    if not rows[:, 4].all():
+    out = np.empty((max(nv, 1), 8), dtype=np.uint32)
+    if not r.st.L.pflt_result_candidate0(r.h, out.ctypes.data_as(_u32p)):
         return None
-    bits = np.clip(rows[:, :1].astype(np.int64) - 32 * np.arange(8, dtype=np.int64), 0, 32)
-    masks = ((np.int64(1) << bits) - 1).astype(np.uint32)   # 32 bits: 2^32 - 1
-    return rows[:, 5:13] & masks
+    return out[:nv]
 
 
 class NativeProgram(ir.PackedProgram):
