@@ -10,6 +10,7 @@
 // witness before trusting it (soundness: a GPU "sat" must satisfy the terms, not only the
 // program); tests/test_native_terms.py checks it against Witness.ev.  Host code, no HIP.
 #include <algorithm>
+#include <initializer_list>
 #include <cstdint>
 #include <cstring>
 #include <map>
@@ -24,7 +25,100 @@
 namespace {
 
 // ---- values of any width: little-endian u32 limbs, exactly ceil(w / 32) of them ----------
-typedef std::vector<uint32_t> V;
+// A small vector: up to 512 bits in place (every value of a <= 256-bit bucket and the
+// 257..512-bit chunks), wider on the heap — the evaluator makes a value per node and op, and
+// a heap allocation each was most of a re-check's time.
+class V {
+   public:
+    V() = default;
+    explicit V(size_t n) : V(n, 0u) {}
+    V(size_t n, uint32_t x) {
+        set_size(n);
+        std::fill(p_, p_ + n, x);
+    }
+    V(std::initializer_list<uint32_t> il) {
+        set_size(il.size());
+        std::copy(il.begin(), il.end(), p_);
+    }
+    V(const uint32_t* b, const uint32_t* e) { assign(b, e); }
+    V(const V& o) { assign(o.p_, o.p_ + o.n_); }
+    V(V&& o) noexcept { take(o); }
+    V& operator=(const V& o) {
+        if (this != &o) assign(o.p_, o.p_ + o.n_);
+        return *this;
+    }
+    V& operator=(V&& o) noexcept {
+        if (this != &o) {
+            release();
+            take(o);
+        }
+        return *this;
+    }
+    ~V() { release(); }
+    size_t size() const { return n_; }
+    bool empty() const { return n_ == 0; }
+    uint32_t& operator[](size_t i) { return p_[i]; }
+    const uint32_t& operator[](size_t i) const { return p_[i]; }
+    uint32_t& back() { return p_[n_ - 1]; }
+    const uint32_t& back() const { return p_[n_ - 1]; }
+    uint32_t* data() { return p_; }
+    const uint32_t* data() const { return p_; }
+    uint32_t* begin() { return p_; }
+    uint32_t* end() { return p_ + n_; }
+    const uint32_t* begin() const { return p_; }
+    const uint32_t* end() const { return p_ + n_; }
+    void push_back(uint32_t x) {
+        if (n_ == cap_) grow(2 * cap_);
+        p_[n_++] = x;
+    }
+    void assign(const uint32_t* b, const uint32_t* e) {
+        const size_t n = (size_t)(e - b);
+        set_size(n);
+        std::copy(b, e, p_);
+    }
+    bool operator==(const V& o) const { return n_ == o.n_ && std::equal(p_, p_ + n_, o.p_); }
+    bool operator!=(const V& o) const { return !(*this == o); }
+
+   private:
+    static constexpr size_t N = 16;
+    uint32_t buf_[N];
+    uint32_t* p_ = buf_;
+    size_t n_ = 0, cap_ = N;
+    void set_size(size_t n) {  // contents not kept
+        if (n > cap_) {
+            release();
+            p_ = new uint32_t[n];
+            cap_ = n;
+        }
+        n_ = n;
+    }
+    void grow(size_t c) {
+        uint32_t* q = new uint32_t[c];
+        std::copy(p_, p_ + n_, q);
+        release();
+        p_ = q;
+        cap_ = c;
+    }
+    void release() {
+        if (p_ != buf_) delete[] p_;
+        p_ = buf_;
+        cap_ = N;
+    }
+    void take(V& o) {
+        n_ = o.n_;
+        if (o.p_ == o.buf_) {
+            p_ = buf_;
+            cap_ = N;
+            std::copy(o.buf_, o.buf_ + o.n_, buf_);
+        } else {
+            p_ = o.p_;
+            cap_ = o.cap_;
+            o.p_ = o.buf_;
+            o.cap_ = N;
+        }
+        o.n_ = 0;
+    }
+};
 
 size_t nl_of(uint32_t w) { return (w + 31) / 32; }
 
@@ -131,17 +225,49 @@ V vashr(const V& a, uint64_t s, uint32_t w) {
 }
 
 void vdivmod(const V& a, const V& b, uint32_t w, V* q, V* r) {  // unsigned, b != 0
+    const V A = vmask(a, w);
     *q = vzero(w);
-    *r = vzero(w + 1);
-    for (uint32_t i = w; i-- > 0;) {
-        *r = vshl(*r, 1, w + 1);
-        if (vbit(a, i)) (*r)[0] |= 1u;
-        if (vcmp(*r, b) >= 0) {
-            *r = vsub(*r, b, w + 1);
+    if (vcmp(A, b) < 0) {  // quotient 0
+        *r = A;
+        return;
+    }
+    bool wide_b = false;
+    for (size_t i = 1; i < b.size(); i++) wide_b |= b[i] != 0u;
+    if (!wide_b) {  // one-limb divisor: 64/32 steps from the top limb
+        const uint64_t d = b[0];
+        uint64_t rem = 0;
+        for (size_t i = A.size(); i-- > 0;) {
+            const uint64_t cur = (rem << 32) | A[i];
+            (*q)[i] = (uint32_t)(cur / d);
+            rem = cur % d;
+        }
+        *r = vzero(w);
+        if (!r->empty()) (*r)[0] = (uint32_t)rem;
+        return;
+    }
+    // restoring division in place, from A's top bit (the remainder stays below 2b)
+    const size_t n = A.size() + 1;
+    V R(n, 0u);
+    uint32_t top = 0;
+    for (size_t i = A.size(); i-- > 0;)
+        if (A[i]) {
+            top = 32u * (uint32_t)i + 32u - (uint32_t)__builtin_clz(A[i]);
+            break;
+        }
+    for (uint32_t i = top; i-- > 0;) {
+        for (size_t k = n; k-- > 1;) R[k] = (R[k] << 1) | (R[k - 1] >> 31);
+        R[0] = (R[0] << 1) | ((A[i / 32] >> (i % 32)) & 1u);
+        if (vcmp(R, b) >= 0) {
+            uint64_t br = 0;
+            for (size_t k = 0; k < n; k++) {
+                const uint64_t x = (uint64_t)R[k] - (k < b.size() ? b[k] : 0u) - br;
+                R[k] = (uint32_t)x;
+                br = (x >> 63) & 1u;
+            }
             (*q)[i / 32] |= 1u << (i % 32);
         }
     }
-    *r = vmask(*r, w);
+    *r = vmask(R, w);
 }
 
 uint64_t vsmall(const V& a, bool* big) {  // value if it fits 64 bits

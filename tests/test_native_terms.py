@@ -371,3 +371,33 @@ def test_candidate0_limbs_are_the_generators_candidate_0(corpus_buckets):
         assert [ir.from_limbs(r) for r in rows.tolist()] == [int(x) for x in want]
         n_full += 1
     assert n_full > 50
+
+
+@pytest.mark.parametrize("w", [8, 64, 160, 256])
+def test_native_recheck_division_paths(w):
+    """pflt_recheck's division (quotient 0, one-limb divisor, restoring steps from the
+    dividend's top bit) against Witness.ev on bvudiv / bvurem / bvsdiv / bvsrem / bvsmod,
+    with the expected results right or off by one, over divisors of every length."""
+    from mythril_amd.smt.interp import Witness
+
+    x, y, z = T.var("x", w), T.var("y", w), T.var("z", w)
+    rng = random.Random(w)
+    ops = ["bvudiv", "bvurem", "bvsdiv", "bvsrem", "bvsmod"]
+    checked = 0
+    for op in ops:
+        cs = [T.eq(T.binop(op, x, y), z)]
+        lo = TermLowering(UFRegistry()).lower(cs)
+        names = [t.val for t in lo.var_terms]
+        for _ in range(60):
+            xv = rng.choice([0, 1, rng.getrandbits(w), (1 << w) - 1, 1 << (w - 1)])
+            yb = rng.choice([1, 2, 7, 31, 32, 33, 63, 64, w - 1, w])
+            yv = rng.getrandbits(min(yb, w)) | (1 << (min(yb, w) - 1))
+            vals = {"x": xv, "y": yv & ((1 << w) - 1)}
+            w0 = Witness(lo, [vals.get(n, 0) for n in names], UFRegistry())
+            zv = w0.ev(T.binop(op, x, y))
+            vals["z"] = zv ^ rng.choice([0, 0, 1])
+            vs = [vals[n] for n in names]
+            want = all(bool(Witness(lo, vs, UFRegistry()).ev(c)) for c in cs)
+            assert NT.recheck(cs, lo, vs, UFRegistry()) == want, (op, w, xv, yv, vals["z"])
+            checked += 1
+    assert checked == 5 * 60
