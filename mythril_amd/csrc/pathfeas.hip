@@ -217,18 +217,17 @@ int check_enqueue(Batch* B, uint64_t gseed, uint32_t budget, uint32_t flags, uin
     Dev* D = find_dev(B->device);
     unsigned long long* d_counters = reinterpret_cast<unsigned long long*>(B->d_scratch);
     uint64_t* d_t0 = reinterpret_cast<uint64_t*>(B->d_scratch + 8);
-#ifdef PF_PROFILE_UNITS
-    HIPCHK(hipMemsetAsync(B->d_scratch, 0, 512, st));
-#else
-    HIPCHK(hipMemsetAsync(B->d_scratch, 0, 64, st));
-#endif
-    HIPCHK(hipMemsetAsync(d_found, 0xff, std::max<size_t>(B->n_sets, 1) * sizeof(uint32_t), st));
 #ifndef PF_FULL_QUEUE
 #define PF_FULL_QUEUE 1
 #endif
-    if ((flags & PF_FLAG_EARLY_EXIT) || PF_FULL_QUEUE)  // the work-queue heads of both launch parts
-        HIPCHK(hipMemsetAsync(B->d_scratch + PF_EARLY_QUEUE_OFF / 4, 0,
-                              2 * PF_EARLY_QUEUES * PF_EARLY_QUEUE_STRIDE * 4, st));
+    // counters (and the profiling slots) at the front, the work-queue heads of both launch
+    // parts from PF_EARLY_QUEUE_OFF: one fill for both when the queues are used
+    if ((flags & PF_FLAG_EARLY_EXIT) || PF_FULL_QUEUE)
+        HIPCHK(hipMemsetAsync(B->d_scratch, 0, PF_EARLY_QUEUE_OFF + 2 * PF_EARLY_QUEUES * PF_EARLY_QUEUE_STRIDE * 4,
+                              st));
+    else
+        HIPCHK(hipMemsetAsync(B->d_scratch, 0, PF_EARLY_QUEUE_OFF, st));
+    HIPCHK(hipMemsetAsync(d_found, 0xff, std::max<size_t>(B->n_sets, 1) * sizeof(uint32_t), st));
     HIPCHK(hipEventRecord(B->ev0, st));
     const uint64_t deadline = timeout_ms ? (uint64_t)timeout_ms * 100000ull : 0ull;  // 100 MHz
     const bool early = flags & PF_FLAG_EARLY_EXIT;
@@ -262,9 +261,15 @@ int check_enqueue(Batch* B, uint64_t gseed, uint32_t budget, uint32_t flags, uin
 }
 
 // Wait for B's last search on stream st and read its counters.
-int check_collect(Batch* B, hipStream_t st, pf_stats* stats) {
+// counters and kernel time of the last launch; with `found`, the verdicts too, copied before
+// the one stream synchronisation (a second round trip was ~4 % of a single query's search)
+int check_collect(Batch* B, hipStream_t st, pf_stats* stats, std::vector<uint32_t>* found = nullptr) {
     unsigned long long h[4];
     HIPCHK(hipMemcpyAsync(h, B->d_scratch, sizeof(h), hipMemcpyDeviceToHost, st));
+    if (found) {
+        found->assign(std::max<size_t>(B->n_sets, 1), 0u);
+        HIPCHK(hipMemcpyAsync(found->data(), B->d_found, found->size() * 4, hipMemcpyDeviceToHost, st));
+    }
     HIPCHK(hipStreamSynchronize(st));
     float ms = 0.f;
     HIPCHK(hipEventElapsedTime(&ms, B->ev0, B->ev1));
@@ -579,11 +584,8 @@ int pf_batch_free(uint64_t handle) {
     return 0;
 }
 
-static int found_to_host(Batch* B, hipStream_t st, uint32_t* found_out, uint8_t* sat_bitmap_out,
-                         pf_stats* stats) {
-    std::vector<uint32_t> found(std::max<size_t>(B->n_sets, 1));
-    HIPCHK(hipMemcpyAsync(found.data(), B->d_found, found.size() * 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+static int found_to_host(Batch* B, const std::vector<uint32_t>& found, uint32_t* found_out,
+                         uint8_t* sat_bitmap_out, pf_stats* stats) {
     uint64_t nsat = 0;
     if (sat_bitmap_out) memset(sat_bitmap_out, 0, (B->n_sets + 7) / 8);
     for (size_t s = 0; s < B->n_sets; s++) {
@@ -606,8 +608,9 @@ int pf_check_batch(uint64_t handle, uint64_t global_seed, uint32_t budget, uint3
     Dev* D = use_dev(B->device);
     if (!D || switch_stream(D, D->stream)) return -1;
     if (check_enqueue(B, global_seed, budget, flags, timeout_ms, B->d_found, D->stream)) return -1;
-    if (check_collect(B, D->stream, stats)) return -1;
-    return found_to_host(B, D->stream, found_out, sat_bitmap_out, stats);
+    std::vector<uint32_t> found;
+    if (check_collect(B, D->stream, stats, &found)) return -1;
+    return found_to_host(B, found, found_out, sat_bitmap_out, stats);
 }
 
 int pf_check_batches(const uint64_t* handles, size_t n, uint64_t global_seed, uint32_t budget,
@@ -628,8 +631,9 @@ int pf_check_batches(const uint64_t* handles, size_t n, uint64_t global_seed, ui
         Dev* D = use_dev(B->device);
         if (!D) return -1;
         pf_stats* st = stats ? stats + i : nullptr;
-        if (check_collect(B, D->stream, st)) return -1;
-        if (found_to_host(B, D->stream, found_out ? found_out + off : nullptr, nullptr, st)) return -1;
+        std::vector<uint32_t> found;
+        if (check_collect(B, D->stream, st, &found)) return -1;
+        if (found_to_host(B, found, found_out ? found_out + off : nullptr, nullptr, st)) return -1;
         off += B->n_sets;
     }
     return 0;
