@@ -459,7 +459,7 @@ def candidate0_limbs(prog) -> Optional[np.ndarray]:
     (include/pf_bytecode.h; ``pf::gen_var``) — pflt_result_candidate0.  None when some
     variable has no parent (the generator then draws it)."""
     r = getattr(prog, "native_result", None)
-    if r is None:
+    if r is None or not hasattr(r.st.L, "pflt_result_candidate0"):
         return None
     nv = int(r.info[0])
     out = np.empty((max(nv, 1), 8), dtype=np.uint32)
