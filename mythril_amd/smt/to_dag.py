@@ -522,7 +522,7 @@ class TermLowering:
         lookup per read: the n bytes concatenated (v_c lowest), shifted right by
         8 * (idx - (base + c)) and cut to a byte, selected when that difference is < n — a
         dozen nodes instead of 4 * n, the same value for every assignment (the single
-        query's longest programs are these chains: DESIGN.md §6)."""
+        query's longest programs were these chains: DESIGN.md §4)."""
         d = self.dag
         if (len(run) < _WINDOW_MIN or rng != 8 or idx.width != 256
                 or len({e[0] for e in run}) != len(run)):
