@@ -17,9 +17,11 @@ Seams:
   ``check()`` unchanged.
 * ``MythrilAmdPluginBuilder`` — a ``MythrilLaserPlugin`` (mythril/plugin/interface.py:40-46,
   ``plugin_default_enabled = True`` read at discovery.py:71) whose LASER plugin batches every
-  open state's constraints at ``stop_sym_trans`` (svm.py:307-308) — right before the
-  tx-boundary ``is_possible`` pass of the next iteration (svm.py:266-286) — in ONE GPU
-  launch, so that pass is answered from the batch.
+  open state's constraints in ONE GPU launch right before each tx-boundary ``is_possible``
+  pass (svm.py:279-283): at ``start_execute_transactions`` (svm.py:227-228) for the first
+  prune and at ``stop_sym_trans`` (svm.py:306-307) for the next one — never after the last
+  transaction, which no prune follows (svm.py:259) — so every prune is answered from the
+  batch.
 """
 
 from __future__ import annotations
@@ -419,6 +421,32 @@ def batch_open_states(open_states, kfm=None, registry: UFRegistry = DEFAULT_REGI
     return n
 
 
+def prune_follows(svm, tx_index: int) -> bool:
+    """Whether LASER runs a tx-boundary prune (svm.py:266-283) next, given ``tx_index``
+    transactions started since ``start_execute_transactions`` — i.e. whether a batch now
+    would be read.
+
+    * no prune at all without ``use_reachability_check`` (svm.py:266; off e.g. for concolic
+      runs, concolic_execution.py:33), and none over zero open states (the loop breaks,
+      svm.py:260);
+    * the ordered loop (``tx_strategy is None``, svm.py:229-234) runs only if no plugin has
+      executed the transactions already, and prunes at iterations 0 … ``transaction_count``-1
+      (svm.py:259): after the last transaction's ``stop_sym_trans`` nothing prunes;
+    * with a tx prioritiser (svm.py:235-237) every sequence re-enters the loop at i = 0
+      (svm.py:248-250), so a batch after any transaction may feed the next sequence's first
+      prune: always batch.
+    A stand-in without these attributes counts as the default ordered loop of unknown
+    length (batch)."""
+    if not getattr(svm, "use_reachability_check", True) or not svm.open_states:
+        return False
+    if getattr(svm, "tx_strategy", None) is not None:
+        return True
+    if tx_index == 0 and getattr(svm, "executed_transactions", False):
+        return False
+    n = getattr(svm, "transaction_count", None)
+    return n is None or tx_index < n
+
+
 _PLUGIN_CLASSES = None
 
 
@@ -440,17 +468,43 @@ def _plugin_classes():
         return _PLUGIN_CLASSES
 
     class MythrilAmdLaserPlugin(LaserPlugin):
+        """Batches the open states right before each tx-boundary prune (svm.py:279-283).
+
+        The prune of iteration i runs at the top of the loop body, before that iteration's
+        ``start_sym_trans`` (svm.py:301) — so the hook that precedes it is the previous
+        iteration's ``stop_sym_trans`` (svm.py:306), and for i = 0 ``start_execute_transactions``
+        (svm.py:227-228, fired after contract creation, :190-206).  The iteration count is
+        ``transaction_count`` (svm.py:259): the ``stop_sym_trans`` of the last transaction is
+        followed by no prune, so it launches nothing (its batch would be dropped unread)."""
+
         def initialize(self, symbolic_vm) -> None:
             install()
+            self.tx_index = 0          # start_sym_trans calls in the current transaction loop
+            self.batches = 0
 
-            @symbolic_vm.laser_hook("stop_sym_trans")
             def _batch():
+                if not prune_follows(symbolic_vm, self.tx_index):
+                    return
                 try:
                     n = batch_open_states(symbolic_vm.open_states)
-                    log.info("GPU batch: %d/%d open states have a witness", n,
-                             len(symbolic_vm.open_states))
+                    self.batches += 1
+                    log.info("GPU batch before prune %d: %d/%d open states have a witness",
+                             self.tx_index, n, len(symbolic_vm.open_states))
                 except Exception as e:  # noqa: BLE001 - the batch is only an optimisation
                     log.warning("GPU batch failed: %s", e)
+
+            @symbolic_vm.laser_hook("start_execute_transactions")
+            def _before_first_prune():
+                self.tx_index = 0
+                _batch()
+
+            @symbolic_vm.laser_hook("start_sym_trans")
+            def _count():
+                self.tx_index += 1
+
+            @symbolic_vm.laser_hook("stop_sym_trans")
+            def _before_next_prune():
+                _batch()
 
     class MythrilAmdPluginBuilder(MythrilLaserPlugin):
         name = "mythril-amd-path-feasibility"

@@ -1,0 +1,222 @@
+"""The tx-boundary batch placed where LASER prunes.
+
+``LaserEVM._execute_transactions_incremental`` (svm.py:252-309) prunes the open states at
+the TOP of iteration i (svm.py:279-283), before that iteration's ``start_sym_trans``
+(:301) and ``stop_sym_trans`` (:306).  So the batch serving prune 0 must come from
+``start_execute_transactions`` (svm.py:227-228, after contract creation :190-206), the one
+serving prune i > 0 from the ``stop_sym_trans`` of transaction i - 1, and the
+``stop_sym_trans`` of the last transaction (i = ``transaction_count`` - 1, :259) must launch
+nothing: no prune reads it.
+
+``LoopSVM`` below is the control flow of ``execute_transactions`` + the incremental loop
+(svm.py:220-239, 252-309) over stand-in world states, with the hook registries of
+svm.py:113-145 — test infrastructure only.  The prune queries run through the restated
+funnel (``Constraints.is_possible`` -> ``get_model`` -> quick-sat -> ``Optimize.check``,
+tests/mythril_standin.py) on the C oracle engine.
+"""
+
+import pytest
+
+import fake_z3 as z3
+import mythril_standin
+import oracle_engine
+from mythril_amd import integration
+from mythril_amd.smt import gpu_check
+from mythril_amd.smt.solver import SolverStatistics
+
+
+class LoopSVM:
+    """svm.py:220-309: hooks, ``execute_transactions`` and the incremental loop.  ``step(i,
+    states)`` stands for ``execute_message_call`` (svm.py:304): it returns the open states
+    transaction i leaves behind."""
+
+    def __init__(self, creation_states, step, transaction_count=3, tx_strategy=None,
+                 use_reachability_check=True, sequences=1):
+        self.open_states = list(creation_states)
+        self.transaction_count = transaction_count
+        self.tx_strategy = tx_strategy
+        self.use_reachability_check = use_reachability_check
+        self.executed_transactions = False
+        self.step = step
+        self.sequences = sequences
+        self.events = []
+        self.hooks = {n: [] for n in ("start_execute_transactions", "stop_execute_transactions",
+                                      "start_sym_trans", "stop_sym_trans")}
+
+    def laser_hook(self, name):
+        def deco(fn):
+            self.hooks[name].append(fn)
+            return fn
+        return deco
+
+    def _fire(self, name):
+        for hook in self.hooks[name]:
+            hook()
+
+    def execute_transactions(self):
+        self._fire("start_execute_transactions")
+        if self.tx_strategy is None:
+            if self.executed_transactions is False:
+                self._incremental()
+        else:
+            for _ in range(self.sequences):            # svm.py:248-250
+                self._incremental()
+        self._fire("stop_execute_transactions")
+
+    def _incremental(self):
+        for i in range(self.transaction_count):
+            if len(self.open_states) == 0:
+                break
+            if self.use_reachability_check:
+                self.events.append(("prune", i, len(self.open_states)))
+                self.open_states = [s for s in self.open_states if s.constraints.is_possible()]
+            self._fire("start_sym_trans")
+            self.open_states = self.step(i, self.open_states)
+            self._fire("stop_sym_trans")
+        self.executed_transactions = True
+
+
+@pytest.fixture
+def standin(monkeypatch):
+    ns = mythril_standin.install(monkeypatch, z3)
+    ns.engine = oracle_engine.install(monkeypatch)
+    monkeypatch.setattr(gpu_check.CONFIG, "budget", 4096)
+    integration._BATCH_CACHE.clear()
+    st = SolverStatistics()
+    st.gpu_sat = st.gpu_attempts = 0
+    return ns
+
+
+def _forks(ns):
+    """Each transaction forks every open state three ways over a fresh symbol
+    ``call_value{i+1}``: two satisfiable children (``== k``: z3's completion default 0 fails
+    them, so no cached model answers them in quick-sat) and one contradiction."""
+    B = ns.Bool
+
+    def step(i, states):
+        cv = z3.BitVec("call_value%d" % (i + 1), 256)
+        out = []
+        for j, s in enumerate(states):
+            base = list(s.constraints)
+            k = 1000 * (i + 1) + 2 * j + 1
+            out.append(ns.WorldState(base + [B(cv == z3.BitVecVal(k, 256))]))
+            out.append(ns.WorldState(base + [B(cv == z3.BitVecVal(k + 1, 256))]))
+            out.append(ns.WorldState(base + [B(z3.ULT(cv, z3.BitVecVal(5, 256))),
+                                              B(z3.ULT(z3.BitVecVal(9, 256), cv))]))
+        return out
+
+    cv0 = z3.BitVec("call_value0", 256)
+    creation = [ns.WorldState([B(cv0 == z3.BitVecVal(7, 256))]),
+                ns.WorldState([B(cv0 == z3.BitVecVal(8, 256))])]
+    return creation, step
+
+
+def _instrument(monkeypatch, svm):
+    real_batch, real_lookup = integration.batch_open_states, integration._lookup_batch
+    hits = []
+
+    def batch(states, *a, **k):
+        svm.events.append(("batch", len(states)))
+        return real_batch(states, *a, **k)
+
+    def lookup(terms):
+        m = real_lookup(terms)
+        hits.append(m is not None)
+        return m
+
+    monkeypatch.setattr(integration, "batch_open_states", batch)
+    monkeypatch.setattr(integration, "_lookup_batch", lookup)
+    return hits
+
+
+def _run(ns, monkeypatch, **kw):
+    creation, step = _forks(ns)
+    svm = LoopSVM(creation, step, **kw)
+    hits = _instrument(monkeypatch, svm)
+    plugin = integration._plugin_classes()[1]()()
+    plugin.initialize(svm)
+    svm.execute_transactions()
+    return svm, plugin, hits
+
+
+def test_one_batch_before_every_prune_and_none_after_the_last(standin, monkeypatch):
+    """Reference loop order at -t 3: creation -> start_execute_transactions -> for i < 3:
+    prune, start_sym_trans, exec, stop_sym_trans.  One batch right before each of the three
+    prunes (i = 0 included), none after the third transaction, and every satisfiable state
+    of every prune is answered from the batch's parked witness — no search inside a prune."""
+    launches_in_prunes = []
+    orig_check = standin.engine.check
+
+    def check(*a, **k):
+        launches_in_prunes.append(svm_ref[0].events[-1][0] if svm_ref else None)
+        return orig_check(*a, **k)
+
+    svm_ref = []
+    standin.engine.check = check
+    creation, step = _forks(standin)
+    svm = LoopSVM(creation, step, transaction_count=3)
+    svm_ref.append(svm)
+    hits = _instrument(monkeypatch, svm)
+    plugin = integration._plugin_classes()[1]()()
+    plugin.initialize(svm)
+    svm.execute_transactions()
+
+    kinds = [e[0] for e in svm.events]
+    assert kinds == ["batch", "prune"] * 3, svm.events
+    # the batch covers exactly the states the prune then checks
+    for b, p in zip(svm.events[0::2], svm.events[1::2]):
+        assert b[1] == p[2]
+    assert plugin.batches == 3 and plugin.tx_index == 3
+    # states per prune: 2, 2*3, 4*3 -> satisfiable 2, 4, 8 -> 14 lookups hit
+    assert sum(hits) == 2 + 4 + 8
+    # every engine launch was a batch: none came from a prune's own query
+    assert launches_in_prunes and all(k == "batch" for k in launches_in_prunes)
+    assert len(svm.open_states) == 8 * 3        # the last transaction's output: unpruned
+
+
+def test_last_transaction_launches_nothing(standin, monkeypatch):
+    """-t 1: only the start_execute_transactions batch; the single stop_sym_trans is last."""
+    svm, plugin, _ = _run(standin, monkeypatch, transaction_count=1)
+    assert [e[0] for e in svm.events] == ["batch", "prune"]
+    assert plugin.batches == 1
+
+
+def test_no_prune_no_batch(standin, monkeypatch):
+    """use_reachability_check=False (svm.py:266; concolic_execution.py:33): nothing prunes,
+    so nothing is batched."""
+    svm, plugin, _ = _run(standin, monkeypatch, use_reachability_check=False)
+    assert [e[0] for e in svm.events] == []
+    assert plugin.batches == 0
+
+
+def test_transactions_already_executed(standin, monkeypatch):
+    """A plugin that ran the transactions itself (executed_transactions, svm.py:229-230): the
+    ordered loop does not run, so start_execute_transactions launches nothing."""
+    creation, step = _forks(standin)
+    svm = LoopSVM(creation, step)
+    svm.executed_transactions = True
+    _instrument(monkeypatch, svm)
+    plugin = integration._plugin_classes()[1]()()
+    plugin.initialize(svm)
+    svm.execute_transactions()
+    assert svm.events == [] and plugin.batches == 0
+
+
+def test_prioritised_sequences_feed_the_next_sequence(standin, monkeypatch):
+    """With a tx prioritiser every sequence re-enters the loop at i = 0 (svm.py:235-237,
+    248-250): the last stop_sym_trans of one sequence feeds the next sequence's first prune,
+    so it batches too."""
+    svm, plugin, _ = _run(standin, monkeypatch, transaction_count=1, tx_strategy=object(),
+                          sequences=2)
+    assert [e[0] for e in svm.events] == ["batch", "prune", "batch", "prune", "batch"]
+
+
+def test_prune_follows_rules():
+    class S:
+        open_states = [1]
+    s = S()
+    s.transaction_count = 2
+    assert integration.prune_follows(s, 0) and integration.prune_follows(s, 1)
+    assert not integration.prune_follows(s, 2)
+    s.open_states = []
+    assert not integration.prune_follows(s, 0)
