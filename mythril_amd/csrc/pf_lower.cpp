@@ -137,6 +137,7 @@ class Lowerer {
     std::vector<std::pair<bool, int>> events;  // (is_assert, node)
     std::vector<int> use_off, use_at;  // uses of node i: use_at[use_off[i] .. use_off[i + 1])
     std::vector<int> where, slot_of, remat, cost, free_slots;
+    int filling = NONE;  // the spilled node materialize() is restoring (not a steal candidate)
     RegFile W, B;
 
     void order(const uint32_t* roots, size_t n_roots) {
@@ -254,7 +255,9 @@ class Lowerer {
             if (!steal) return false;
             int far_v = NONE, far_nu = -1;
             for (size_t v = 0; v < slot_of.size(); ++v) {
-                if (slot_of[v] == NONE || N[v].kind != PFL_K_VAR) continue;
+                // never the variable materialize() is filling right now (its slot is read
+                // after the register is allocated)
+                if (slot_of[v] == NONE || N[v].kind != PFL_K_VAR || (int)v == filling) continue;
                 const int nu = next_use((int)v, t);
                 if (far_v == NONE || nu >= far_nu) {
                     far_v = (int)v;
@@ -403,11 +406,15 @@ class Lowerer {
         if (where[nd] != NONE) return where[nd];
         if (slot_of[nd] != NONE) {
             const Node& n = N[nd];
+            const int slot = slot_of[nd];
+            const int outer = filling;
+            filling = nd;
             const int r = alloc(rf, nd, t, n.is_bool ? pinned_b : pinned_w);
+            filling = outer;
             if (n.is_bool)
-                emit(PF_B_FILL, 1, r, 0, 0, 0, slot_of[nd]);
+                emit(PF_B_FILL, 1, r, 0, 0, 0, slot);
             else
-                emit(PF_W_FILL, n.width, r, 0, 0, 0, slot_of[nd]);
+                emit(PF_W_FILL, n.width, r, 0, 0, 0, slot);
             return r;
         }
         if (!is_leaf(N[nd].kind) && remat_size(nd) == NONE)

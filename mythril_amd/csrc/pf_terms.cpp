@@ -1569,7 +1569,7 @@ Result* lower_job(const Store& S, const std::vector<uint32_t>& rs, const Parents
                     }
                     break;
                 }
-                if (rc == -2 && ti == 1 && have_narrow) {  // the wide lowering failed: keep the narrow one
+                if (ti == 1 && have_narrow) {  // the wide lowering failed (any rc): keep the narrow one
                     R->code.swap(n_code);
                     R->consts.swap(n_consts);
                     R->n_wregs = tries[0];

@@ -418,7 +418,9 @@ def lower(dag: Dag, seed: int = 0, name: str = "", nw: Optional[int] = None) -> 
             pass
         try:
             wide = lower(dag, seed, name, ir.NW)
-        except LoweringError:
+        except (LoweringError, ValueError, OverflowError):
+            # any failure of the wide lowering keeps a valid narrow program (pf_terms.cpp
+            # does the same)
             if narrow is None:
                 raise
             return narrow
@@ -534,6 +536,7 @@ def lower_py(dag: Dag, seed: int = 0, name: str = "", nw: int = ir.NW) -> Progra
     # it again costs nothing and restoring it is one fill
     slot_of: Dict[int, int] = {}
     free_slots = list(range(ir.MAX_SPILL - 1, -1, -1))
+    filling: List[Optional[int]] = [None]   # the spilled node materialize() is restoring
 
     def rank(t):
         def f(nd):
@@ -553,7 +556,10 @@ def lower_py(dag: Dag, seed: int = 0, name: str = "", nw: int = ir.NW) -> Progra
         if not free_slots:
             # a value that cannot be recomputed takes the slot of a spilled variable (the
             # one used farthest in the future; its later restores re-run the generator)
-            vs = [v for v in sorted(slot_of) if dag.nodes[v].kind == K_VAR] if steal else []
+            # (never the variable materialize() is filling now: its slot is read after the
+            # register is allocated)
+            vs = [v for v in sorted(slot_of) if dag.nodes[v].kind == K_VAR and v != filling[0]] \
+                if steal else []
             if not vs:
                 return False
             far_v = vs[0]
@@ -633,11 +639,14 @@ def lower_py(dag: Dag, seed: int = 0, name: str = "", nw: int = ir.NW) -> Progra
             return rf.where[nd]
         if nd in slot_of:
             n = dag.nodes[nd]
+            slot, outer = slot_of[nd], filling[0]
+            filling[0] = nd
             r = alloc(rf, nd, t, pinned_b if n.is_bool else pinned_w)
+            filling[0] = outer
             if n.is_bool:
-                prog.emit(ir.B_FILL, 1, dst=r, aux0=slot_of[nd])
+                prog.emit(ir.B_FILL, 1, dst=r, aux0=slot)
             else:
-                prog.emit(ir.W_FILL, n.width, dst=r, aux0=slot_of[nd])
+                prog.emit(ir.W_FILL, n.width, dst=r, aux0=slot)
             return r
         if dag.nodes[nd].kind not in _LEAF_KINDS and remat_size(nd) is None:
             raise LoweringError("non-rematerialisable value was evicted")

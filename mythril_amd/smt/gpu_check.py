@@ -52,6 +52,9 @@ class GpuConfig:
     # neighbourhood candidates, include/pf_bytecode.h) for the one bucket the condition changes
     parents: bool = True
     recent_size: int = 1 << 14   # symbol values kept for parent models
+    # terms in the native store before it is retired for a fresh one (a long analysis would
+    # otherwise keep every term it ever posed): ~2M terms, a few hundred MB of host memory
+    store_limit: int = 1 << 21
     cache_size: int = 1 << 16    # bucket witnesses kept
     # re-evaluate every constraint of a multi-bucket set under the union of its bucket
     # witnesses.  Off by default: each bucket witness is re-checked on exactly its bucket's
@@ -375,6 +378,9 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
     nat = _native_batch()
     if nat:
         from . import native_terms
+
+        if native_terms.new_generation(cfg.store_limit):
+            reset_cache()   # cached witnesses hold results of the retired store
     phases: Dict[str, float] = {}
     tp = [t0]
 

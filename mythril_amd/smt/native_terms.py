@@ -120,7 +120,18 @@ class TermStore:
         self.h = lib.pflt_store_new()
         self.ids: Dict[T.Term, int] = {}
         self.terms: List[T.Term] = []
-        self.lock = threading.Lock()
+        # guards Store::t and the recent tables: pflt_add (export) may reallocate the term
+        # vector that a concurrent recheck / recent-parent / lowering reads through pointers
+        # (ctypes drops the GIL), so every call into the store holds it
+        self.lock = threading.RLock()
+
+    def __del__(self):
+        # the C++ store goes with the last reference: results keep their own TermStore
+        # (``_Result.st``), so a retired generation lives until its results are gone
+        try:
+            self.L.pflt_store_free(self.h)
+        except Exception:  # noqa: BLE001
+            pass
 
     def export(self, root: T.Term) -> int:
         """Store id of ``root``, adding it and every new subterm (children first)."""
@@ -192,6 +203,23 @@ def store() -> Optional[TermStore]:
 
 
 _BLOBS: Dict[tuple, np.ndarray] = {}
+
+
+def new_generation(limit: int) -> bool:
+    """Retire the process's store once it holds ``limit`` terms or more (over a
+    long ``myth analyze`` every term ever exported stays in it).  The next export starts a
+    fresh store; results lowered from the old one keep it alive through ``_Result.st`` and
+    are re-checked / recorded against it, never against the new one.  The caller drops its
+    caches of such results (gpu_check.check_sets: reset_cache).  True if retired."""
+    global _STORE
+    st = _STORE
+    if st is None or len(st.terms) < limit:
+        return False
+    with _STORE_LOCK:
+        if _STORE is not st:
+            return False
+        _STORE = TermStore(st.L)
+    return True
 
 
 def _registry_blob(reg: UFRegistry) -> np.ndarray:
@@ -565,23 +593,27 @@ def note_vars(vals: Dict[str, int], recent_size: int) -> None:
         words += [len(ls)] + ls
     if names:
         w = np.array(words, dtype=np.uint32)
-        st.L.pflt_note_vars(st.h, b"\0".join(names) + b"\0", w.ctypes.data_as(_u32p), len(names), recent_size)
+        with st.lock:
+            st.L.pflt_note_vars(st.h, b"\0".join(names) + b"\0", w.ctypes.data_as(_u32p), len(names),
+                                recent_size)
 
 
 def note_result(lo: NativeLowered, limbs: np.ndarray, recent_size: int) -> None:
-    st = batch_api()
+    st = lo.res.st          # the store the result's term ids belong to
     if not isinstance(limbs, np.ndarray):
         limbs = ir.limbs_array([int(x or 0) for x in limbs])
     v = np.ascontiguousarray(limbs, dtype=np.uint32)
     if v.size == 0:
         v = np.zeros(8, dtype=np.uint32)
-    st.L.pflt_note_result(st.h, lo.res.h, v.ctypes.data_as(_u32p), recent_size)
+    with st.lock:
+        st.L.pflt_note_result(st.h, lo.res.h, v.ctypes.data_as(_u32p), recent_size)
 
 
 def recent_clear() -> None:
     st = batch_api()
     if st is not None:
-        st.L.pflt_recent_clear(st.h)
+        with st.lock:
+            st.L.pflt_recent_clear(st.h)
 
 
 # pflt_job (include/pf_lower.h): roots pointer, n_roots, parents handle, flags, seed
@@ -654,25 +686,36 @@ def pack_batch(programs: List[NativeProgram]):
 def recheck_many(los: List[NativeLowered], limbs: np.ndarray, reg: UFRegistry, threads: int) -> np.ndarray:
     """Status per bucket witness: 1 every conjunct true, 0 some false, -1 not evaluable
     natively (re-check in Python).  limbs = the witnesses' variables back to back."""
-    st = batch_api()
     n = len(los)
     if n == 0:
         return np.zeros(0, dtype=np.int8)
+    st = los[0].res.st      # the store the results' term ids belong to
+    if any(lo.res.st is not st for lo in los):
+        # results of two store generations (a retirement between lowering and re-check):
+        # each group against its own store
+        v = np.ascontiguousarray(limbs, dtype=np.uint32).reshape(-1, 8)
+        offs = np.cumsum([0] + [int(lo.res.info[0]) for lo in los])
+        status = np.zeros(n, dtype=np.int8)
+        for g in {id(lo.res.st) for lo in los}:
+            idx = [k for k in range(n) if id(los[k].res.st) == g]
+            rows = np.concatenate([v[offs[k]:offs[k + 1]] for k in idx] or [v[:0]])
+            status[idx] = recheck_many([los[k] for k in idx], rows, reg, threads)
+        return status
     hs = (ctypes.c_void_p * n)(*[lo.res.h for lo in los])
     v = np.ascontiguousarray(limbs, dtype=np.uint32).reshape(-1)
     if v.size == 0:
         v = np.zeros(8, dtype=np.uint32)
     regb = _registry_blob(reg)
     status = np.zeros(n, dtype=np.int8)
-    st.L.pflt_recheck_many(st.h, hs, n, v.ctypes.data_as(_u32p), regb.ctypes.data_as(_u32p), len(regb),
-                           max(1, threads), status.ctypes.data_as(ctypes.POINTER(ctypes.c_int8)))
+    with st.lock:
+        st.L.pflt_recheck_many(st.h, hs, n, v.ctypes.data_as(_u32p), regb.ctypes.data_as(_u32p), len(regb),
+                               max(1, threads), status.ctypes.data_as(ctypes.POINTER(ctypes.c_int8)))
     return status
 
 
 def shrink(lo: NativeLowered) -> None:
     """Free the program tables of a result whose program was uploaded (the cache keeps it)."""
-    st = batch_api()
-    st.L.pflt_result_shrink(lo.res.h)
+    lo.res.st.L.pflt_result_shrink(lo.res.h)
 
 
 def ints_of(limbs: np.ndarray) -> List[int]:

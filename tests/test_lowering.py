@@ -336,3 +336,52 @@ def test_index_runs_become_window_lookups_with_the_same_values(monkeypatch):
         assert all(bool(Witness(lw, vals, UFRegistry()).ev(c)) for c in cs) == want
         sat += want
     assert sat > 0
+
+
+def _slot_steal_dag(n_vars, n_pairs):
+    """Every spill slot taken and every register held by a value that can be neither
+    recomputed nor evicted for free, at the moment a spilled variable is filled for its last
+    use (the steal must not take the slot being filled).  Phase 1 spills the
+    variables (each used again later); phase 2 computes two fresh products per root — each
+    live to the end, so two spills per root against the one slot the root's variable frees."""
+    dag = Dag()
+    xs = [dag.var(f"x{i}", 256) for i in range(n_vars)]
+    for i, x in enumerate(xs):
+        dag.assert_(dag.op(ir.B_ULT, 256, x, dag.const((i + 1) << 200, 256)))
+    live = []
+    for k in range(n_pairs):
+        y, z = dag.var(f"y{k}", 256), dag.var(f"z{k}", 256)
+        q, r = dag.op(ir.W_MUL, 256, y, y), dag.op(ir.W_MUL, 256, z, z)
+        live += [q, r]
+        dag.assert_(dag.op(ir.B_ULT, 256, dag.op(ir.W_ADD, 256, xs[k % n_vars], q), r))
+    acc = live[-1]
+    for v in reversed(live[:-1]):
+        acc = dag.op(ir.W_XOR, 256, acc, v)
+    dag.assert_(dag.op(ir.B_ULT, 256, acc, dag.const(1 << 255, 256)))
+    return dag
+
+
+@pytest.mark.parametrize("n_vars", [30, 40])
+def test_fill_never_loses_its_own_slot(n_vars):
+    """At 7 registers the steal would have taken the slot of the variable being filled (a
+    FILL from slot NONE / a KeyError that aborted check_sets); now that lowering is a clean
+    LoweringError, the default policy moves to 15 registers, and the program validates and
+    computes the DAG's value."""
+    from mythril_amd.lower import lower_py
+
+    dag = _slot_steal_dag(n_vars, 36)
+    with pytest.raises(LoweringError):
+        lower_py(dag, nw=ir.NW_NARROW)
+    with pytest.raises(LoweringError):
+        lower(dag, nw=ir.NW_NARROW)
+    prog = lower(dag)
+    b = ir.Batch([prog])           # validates: every FILL reads a slot a SPILL wrote
+    w = prog.words if isinstance(prog, ir.PackedProgram) else \
+        np.array([ins.words() for ins in prog.code], dtype=np.uint32).reshape(-1, 4)
+    fills = w[(w[:, 0] & 0xFF) == ir.W_FILL]
+    assert len(fills) and (fills[:, 2] < ir.MAX_SPILL).all()
+    sv = O.SetView.from_batch(b, 0)
+    rng = random.Random(11)
+    for _ in range(6):
+        vals = [rng.getrandbits(256) for _ in dag.vars]
+        assert sv.evaluate(vals) == bool(eval_dag(dag, vals))

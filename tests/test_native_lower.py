@@ -126,3 +126,12 @@ def test_native_program_runs_like_python_on_the_oracle():
     b = O.SetView.from_batch(ir.Batch([ref]), 0).check(512, 9)
     assert a == b
     assert np.array_equal(ir.Batch([prog]).code, ir.Batch([ref]).code)
+
+
+@pytest.mark.parametrize("n_vars,n_pairs", [(30, 36), (40, 36), (40, 30)])
+def test_slot_steal_edge_identical(n_vars, n_pairs):
+    """The fill-at-last-use slot steal: native and Python agree — the same
+    program, or the same LoweringError — at both register counts."""
+    from test_lowering import _slot_steal_dag
+
+    _same(_slot_steal_dag(n_vars, n_pairs))

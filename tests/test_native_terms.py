@@ -401,3 +401,32 @@ def test_native_recheck_division_paths(w):
             assert NT.recheck(cs, lo, vs, UFRegistry()) == want, (op, w, xv, yv, vals["z"])
             checked += 1
     assert checked == 5 * 60
+
+
+def test_store_generation_retires_and_results_keep_their_store(monkeypatch):
+    """the native store is retired past ``store_limit`` terms; results lowered
+    before keep (and re-check against) their own store, and the next query exports into a
+    fresh one."""
+    from dataclasses import replace
+
+    from mythril_amd.smt import native_terms
+
+    if native_terms.batch_api() is None:
+        pytest.skip("libpflower.so not built")
+    oracle_engine.install(monkeypatch)
+    from mythril_amd.smt import ULT, symbol_factory
+
+    q = [ULT(symbol_factory.BitVecSym("gen_x", 256), symbol_factory.BitVecVal(10, 256)).raw]
+    cfg = replace(gpu_check.CONFIG, budget=256)
+    m1 = gpu_check.check_sets([q], config=cfg)[0]
+    assert m1 is not None
+    old = native_terms.store()
+    assert len(old.terms) > 0
+    lo_old = next(iter(gpu_check._CACHE.values()))[0]
+    # a limit below the current size retires the store at the next call
+    m2 = gpu_check.check_sets([q], config=replace(cfg, store_limit=1))[0]
+    assert m2 is not None
+    new = native_terms.store()
+    assert new is not old and lo_old.res.st is old
+    assert native_terms.recheck_many([lo_old], np.asarray(ir.limbs_array([m1.w.vars["gen_x"]])),
+                                     gpu_check.DEFAULT_REGISTRY, 1).tolist() == [1]
