@@ -33,7 +33,7 @@ sys.path.insert(0, ROOT)
 INT32_PEAK_OPS = 256 * 4 * 32 * 2.4e9
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=8)
@@ -53,7 +53,7 @@ def parse():
                     help="one waited pf_check_batch call per step instead of all K enqueued at once")
     ap.add_argument("--corpus-scenarios", type=int, default=48,
                     help="LASER-shaped scenarios for the %% discharged half of the metric (0 = skip)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 def cpu_baseline(programs, budget, seed, target_s):
@@ -270,7 +270,7 @@ def keccak_leg(args, torch, rank, world):
                                  "slots (2 cycles per wave64 instruction at 2.4 GHz)"}}
 
 
-def early_leg(args, eng, batch, torch, dist, first_id):
+def early_leg(args, eng, batch, torch, dist, first_id, cdev="cuda"):
     """SURVEY §8(d) config 3 asks for both sweeps: the same DAGs searched with ballot early
     exit and per-assert short-circuit on (the engine's production flags,
     pf_check_early_kernel).  Two launches:
@@ -291,7 +291,7 @@ def early_leg(args, eng, batch, torch, dist, first_id):
         r = eng.check(db, budget=args.budget, seed=args.seed, flags=flags)
         vals = [float(r.cands_decided), r.kernel_ms / 1e3, float(int(r.sat.sum()))]
         if dist is not None:
-            t = torch.tensor(vals, dtype=torch.float64, device="cuda")
+            t = torch.tensor(vals, dtype=torch.float64, device=cdev)
             s_ = t[[0, 2]].clone()
             dist.all_reduce(s_, op=dist.ReduceOp.SUM)
             m_ = t[1:2].clone()
@@ -358,6 +358,24 @@ def main():
         dist = dist_mod
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    line = run(args, rank, world, local, dist)
+    if line is not None:
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        # rank 0 spends a few seconds on the host-side legs: leave together
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def run(args, rank, world, local, dist, engine=None, cdev="cuda"):
+    """The bench body for one rank; returns rank 0's JSON line (None on other ranks).
+
+    ``dist`` is torch.distributed with the process group already up (None at N = 1).  The
+    engine and the collectives' device are parameters so that the multi-rank branch — the
+    step-time max, the evals sum, the verdict all-gather, the early-exit reductions and
+    rank 0's line — also runs in a CPU test under gloo with the oracle as the engine
+    (tests/test_bench_dist.py), not first in the driver's SCALE run."""
+    import torch
 
     from mythril_amd import _lib, ir, synth
     from mythril_amd.engine import Engine
@@ -365,7 +383,7 @@ def main():
     if args.lib:
         _lib.load_library(args.lib)
 
-    eng = Engine(local)
+    eng = engine if engine is not None else Engine(local)
     flags = ir.FLAG_COUNT_OPS | (ir.FLAG_EARLY_EXIT | ir.FLAG_SHORTCIRCUIT if args.mode == "early" else 0)
     n_steps = args.warmup + args.steps
     batches, step_progs = [], []
@@ -378,7 +396,8 @@ def main():
     t_gen = time.perf_counter() - t_gen
 
     def barrier():
-        torch.cuda.synchronize()
+        if cdev == "cuda":
+            torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
 
@@ -409,7 +428,7 @@ def main():
 
     tot_evals, max_dt = float(evals), dt
     if dist is not None:
-        t = torch.tensor([float(evals), dt], dtype=torch.float64, device="cuda")
+        t = torch.tensor([float(evals), dt], dtype=torch.float64, device=cdev)
         ev = t[:1].clone()
         dist.all_reduce(ev, op=dist.ReduceOp.SUM)
         mx = t[1:].clone()
@@ -418,20 +437,20 @@ def main():
         # the path's one collective: all-gather the per-set SAT verdicts
         from mythril_amd.dist import gather_found
 
-        local = np.concatenate(founds)
-        gather_found(local, rank * len(local), world * len(local))
+        mine = np.concatenate(founds)
+        gathered = gather_found(mine, rank * len(mine), world * len(mine))
 
     # node evaluations of the timed steps: every instruction of every set runs for every
     # candidate in the full sweep (also report node-evals/s)
     nodes_per_step = [sum(len(p.code) for p in step_progs[k]) for k in range(args.warmup, n_steps)]
     tot_nodes = float(sum(nodes_per_step) * args.budget)
     if dist is not None:
-        x = torch.tensor([tot_nodes], dtype=torch.float64, device="cuda")
+        x = torch.tensor([tot_nodes], dtype=torch.float64, device=cdev)
         dist.all_reduce(x, op=dist.ReduceOp.SUM)
         tot_nodes = float(x.item())
 
-    early = (early_leg(args, eng, batches[args.warmup], torch, dist, (args.warmup * world + rank) * args.sets)
-             if args.mode == "full" else None)
+    early = (early_leg(args, eng, batches[args.warmup], torch, dist, (args.warmup * world + rank) * args.sets,
+                       cdev) if args.mode == "full" else None)
     kec = keccak_leg(args, torch, rank, world) if args.keccak_log2 > 0 else None
 
     # the SURVEY.md §8(d) op table's figure (prices EXP as 512 products and division as an
@@ -496,11 +515,11 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(step_progs[args.warmup], args.budget, args.seed,
                                                 args.cpu_sample_s)
-        print(json.dumps(line), flush=True)
-    if dist is not None:
-        # rank 0 spends a few seconds on the host-side legs above: leave together
-        dist.barrier()
-        dist.destroy_process_group()
+        if dist is not None:
+            line["verdicts_gathered"] = int(gathered.size)
+            line["sets_with_witness"] = int((gathered != 0xFFFFFFFF).sum())
+        return line
+    return None
 
 
 if __name__ == "__main__":

@@ -113,6 +113,16 @@ namespace {
     case R:                                                                               \
         _Pragma("unroll") for (int k_ = 0; k_ < 8; k_++)(W)[R][k_] = (src).l[k_];          \
         break;
+// An LDS operand read is waited for where it is issued, before the next instruction's
+// scalar fetch goes out (run_program): LDS reads and scalar loads share lgkmcnt and scalar
+// loads return out of order, so a wait at the join of the operand switch — where the compiler
+// put one for every later use of the operand, whichever register it came from — also waited
+// for the fetch in flight, exposing its latency on every instruction.
+#ifndef PF_FETCH_EARLY
+#define PF_WAIT_LDS() __builtin_amdgcn_s_waitcnt(0xC07F)  // lgkmcnt(0)
+#else
+#define PF_WAIT_LDS() ((void)0)
+#endif
 #if PF_NW_NARROW == 7
 // Registers 5 and 6 live in LDS, one 32-byte slot per lane each: entry 0 of EXP's window
 // table (which keeps base^0 = 1 out of it) and one entry past it (PF_LDS_WREG6).  40 VGPRs of
@@ -124,8 +134,8 @@ namespace {
         switch (r) {                                                                      \
             RDN_CASE(dst, W, 0) RDN_CASE(dst, W, 1) RDN_CASE(dst, W, 2) RDN_CASE(dst, W, 3) \
             RDN_CASE(dst, W, 4)                                                           \
-            case 5: (dst) = pf::tbl_get(LT, 64u, PF_LDS_WREG5); break;                      \
-            default: (dst) = pf::tbl_get(LT, 64u, PF_LDS_WREG6); break;                     \
+            case 5: (dst) = pf::tbl_get(LT, 64u, PF_LDS_WREG5); PF_WAIT_LDS(); break;       \
+            default: (dst) = pf::tbl_get(LT, 64u, PF_LDS_WREG6); PF_WAIT_LDS(); break;      \
         }                                                                                 \
     } while (0)
 #define WRN_SW(W, r, src, LT)                                                              \
@@ -593,9 +603,12 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
         if (__builtin_expect(unit == PF_U_END, 0)) break;
         // Issue the next fetch only after this instruction's words are decoded: scalar
         // loads return out of order, so a fetch issued before the decode would be waited
-        // for together with the one being consumed (lgkmcnt(0)).
+        // for together with the one being consumed (lgkmcnt(0)).  And after the operand
+        // reads (PF_WAIT_LDS): see there.
+#ifdef PF_FETCH_EARLY
         __builtin_amdgcn_sched_barrier(0);
         In = fetch_ins(++ip);
+#endif
         u256 x, y, z;
         // register indices are trusted: pf_batch_create checks every read and write
         // against the register file of the kernel that runs the set
@@ -606,6 +619,10 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
             if (__builtin_expect((tr & PF_TR_RA) != 0u, 1)) RD_W(x, W, a, LPB);
             if (__builtin_expect((tr & PF_TR_RB) != 0u, 1)) RD_W(y, W, b, LPB);
         }
+#ifndef PF_FETCH_EARLY
+        __builtin_amdgcn_sched_barrier(0);
+        In = fetch_ins(++ip);
+#endif
         // Dispatch on the datapath unit (w0 bits 21..23) first.  The heavy datapaths exist
         // once each (multiplier, divider, shifter, generator) and are shared by every
         // opcode that needs them: the kernel's code must stay small enough for the
