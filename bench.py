@@ -322,8 +322,10 @@ def pmc_traffic(args):
 def valu_view(pmc, kernel_s):
     """Hardware side of the roofline from the PMC summary: wave-level VALU instructions per
     launch (SQ_INSTS_VALU) over the SIMDs' VALU issue slots (a wave64 VALU instruction
-    occupies its SIMD for 2 cycles; 1024 SIMDs), at the effective clock of the PMC run
-    (GRBM_GUI_ACTIVE / 8 XCDs) and, for reference, at 2.4 GHz over the live kernel time."""
+    occupies its SIMD for 2 cycles; 1024 SIMDs, MI355X_MICROARCH.md "Wave scheduling"), at
+    the effective clock of the PMC run (GRBM_GUI_ACTIVE / 8 XCDs) and, for reference, at
+    2.4 GHz over the live kernel time.  The empty slots are latency the resident waves do not
+    hide (dependent chains, scalar dispatch, waits); no instruction is priced above 2 cycles."""
     if not pmc or "sq" not in pmc:
         return None
     v = pmc["sq"]["SQ_INSTS_VALU"]
@@ -334,13 +336,6 @@ def valu_view(pmc, kernel_s):
         cyc = clk["GRBM_GUI_ACTIVE"] / 8.0
         # both counts from the same PMC run: independent of this run's kernel time
         out["issue_frac_eff_clock"] = 2.0 * clk["SQ_INSTS_VALU"] / (1024 * cyc)
-        vc = pmc.get("valu_cycles")
-        if vc:
-            # cycle-weighted at the issue costs measured at 4 waves/SIMD (tools/movbench.hip:
-            # a simple op 2.9 cycles, v_mad_u64_u32 4.95, f64 4.9; tools/pmc_summary.py) —
-            # the VALU pipeline's occupancy
-            out["valu_busy_eff_clock"] = vc["cycles"] / (1024 * cyc)
-            out["valu_busy_weights"] = vc["weights"]
     return out
 
 

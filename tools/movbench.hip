@@ -4,7 +4,9 @@
 // EXP Horner chain's Hensel divisions) and the f64 ops of the division estimates.
 // Each lane runs `iters` rounds of 16 independent instructions (inline asm, so the compiler
 // cannot fold or reorder them); grid = 4 waves per SIMD, the search kernels' occupancy.
-// Prints SIMD cycles per wave-instruction.
+// Prints SIMD cycles per wave-instruction: latency-limited rates at the given occupancy (16
+// independent instructions per wave), not throughput — the VALU issues a wave64 instruction
+// every 2 cycles at best (MI355X_MICROARCH.md).
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdio>
@@ -269,12 +271,23 @@ int main(int argc, char** argv) {
         const double cyc = ms * 1e-3 * 2.4e9 / ((double)iters * 16.0 * waves_per_simd);
         printf("%-20s %8.3f ms  %6.2f SIMD cycles per wave-instruction (at 2.4 GHz)\n", k.name, ms, cyc);
     }
+    CHK(hipEventRecord(e0));
     hipLaunchKernelGGL(k_clock, dim3(grid), dim3(block), 0, 0, iters, out);
-    CHK(hipDeviceSynchronize());
+    CHK(hipEventRecord(e1));
+    CHK(hipEventSynchronize(e1));
+    float ms_clk; CHK(hipEventElapsedTime(&ms_clk, e0, e1));
     uint64_t h[2];
     CHK(hipMemcpy(h, out, 16, hipMemcpyDeviceToHost));
     const double ghz = (double)h[0] / ((double)h[1] * 10.0);  // cycles per 10 ns tick
-    printf("shader clock during the add loop: %.3f GHz; v_add_u32 at that clock: %.2f SIMD cycles per wave-instruction\n",
-           ghz, (double)h[0] / ((double)iters * 16.0 * waves_per_simd));
+    // SIMD cycles per wave-instruction = the kernel's event time at the measured clock over
+    // the instructions each SIMD issues.  (Round 3 divided ONE wave's s_memtime lifetime by
+    // waves_per_simd x its instructions: that assumes every wave of the SIMD is resident for
+    // the measured wave's whole life, which the dispatcher does not guarantee — at 8 waves it
+    // read 0.75 cycles, below the 2-cycle wave64 issue floor.)  With 16 independent
+    // instructions per wave these are latency-limited rates at that occupancy, not the VALU's
+    // throughput (2 cycles per wave64 instruction, MI355X_MICROARCH.md).
+    printf("shader clock during the add loop: %.3f GHz (one wave's s_memtime / s_memrealtime); "
+           "v_add_u32: %.2f SIMD cycles per wave-instruction (event time at that clock)\n",
+           ghz, ms_clk * 1e-3 * ghz * 1e9 / ((double)iters * 16.0 * waves_per_simd));
     return 0;
 }

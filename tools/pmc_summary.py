@@ -60,29 +60,16 @@ def main():
     f64 = per_dispatch(csvp("f64"))
     if f64:
         out["f64"] = {k: mean(f64, k) for k in F64_KEYS if k in f64[0]}
-        # VALU pipeline cycles per launch, cycle-weighted (not issue-counted) at the issue
-        # costs tools/movbench.hip measures at the search kernel's 4 waves/SIMD
-        # (profiles/r03_movbench.log, shader cycles): a simple wave64 op 2.9 (not the 2 of the
-        # SIMD-32 datasheet), v_mad_u64_u32 4.95, f64 ops and conversions 4.9 — three-source
-        # integer ops (4.8) are not separable in the PMC and count as simple, so this is a
-        # lower bound; over (1024 SIMDs x effective cycles) it is the VALU's occupancy
-        n64 = sum(out["f64"].get(k, 0.0) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
-                                                    "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64",
-                                                    "SQ_INSTS_VALU_CVT"))
-        ni64 = sqm["SQ_INSTS_VALU_INT64"]
-        rest = sqm["SQ_INSTS_VALU"] - ni64 - n64
-        out["valu_cycles"] = {"cycles": 2.9 * rest + 4.95 * ni64 + 4.9 * n64, "int64": ni64, "fp64": n64,
-                              "other": rest,
-                              "weights": "measured issue costs at 4 waves/SIMD (tools/movbench.hip): other 2.9, "
-                                         "int64 (v_mad_u64_u32) 4.95, f64 and conversions 4.9 SIMD cycles"}
+        # (round 3 also wrote a cycle-weighted "VALU pipeline busy" here, priced at
+        # tools/movbench.hip's 4-wave rates; those are latency-limited, not issue costs, so
+        # the summary now reports only the issue-slot fraction at the VALU's 2 cycles per
+        # wave64 instruction — MI355X_MICROARCH.md "Wave scheduling")
     kf, kw = per_dispatch(csvp("fetch"), KECCAK), per_dispatch(csvp("write"), KECCAK)
     if kf and kw:
         k = {"kernel": KECCAK, "fetch_bytes": 2 * mean(kf, "FETCH_SIZE") * 1024,
              "write_bytes": mean(kw, "WRITE_SIZE") * 1024}
         k["traffic_bytes"] = k["fetch_bytes"] + k["write_bytes"]
         out["keccak"] = k
-    with open(os.path.join(root, "profiles", f"{tag}_pmc.json"), "w") as f:
-        json.dump(out, f, indent=1)
     lines = [f"# {tag} — PMC passes of `bench.py --steps 2 --warmup 1` ({KERNEL})", "",
              "Each counter group is its own `rocprofv3 --pmc` run (tools/gpu_profile.sh).", "",
              "| quantity | per launch |", "|---|---|",
@@ -95,12 +82,16 @@ def main():
             lines.append(f"| {key} (clock pass) | {v:.4g} |")
     for key, v in out.get("f64", {}).items():
         lines.append(f"| {key} (f64 pass) | {v:.4g} |")
-    if "valu_cycles" in out:
-        vc = out["valu_cycles"]
-        lines.append(f"| VALU pipeline cycles (other x2.9 + int64 x4.95 + f64 x4.9, measured issue costs) | {vc['cycles']:.4g} |")
-        if "clk" in out:
-            eff = out["clk"]["GRBM_GUI_ACTIVE"] / 8.0  # per-XCD cycles of the launch
-            lines.append(f"| VALU pipeline busy (over 1024 SIMDs x {eff:.4g} cycles) | {vc['cycles'] / (1024 * eff):.3f} |")
+    if "clk" in out:
+        eff = out["clk"]["GRBM_GUI_ACTIVE"] / 8.0  # per-XCD cycles of the launch
+        out["valu_issue_frac"] = 2.0 * out["clk"]["SQ_INSTS_VALU"] / (1024 * eff)
+        lines.append(f"| VALU issue-slot fraction (2 cycles per wave64 instruction, 1024 SIMDs x {eff:.4g} "
+                     f"cycles) | {out['valu_issue_frac']:.3f} |")
+        if "f64" in out:
+            n64 = sum(out["f64"].values())
+            ni = sqm["SQ_INSTS_VALU_INT64"]
+            lines.append(f"| of which v_mad_u64_u32-class (INT64) / f64+cvt instructions | "
+                         f"{2.0 * ni / (1024 * eff):.3f} / {2.0 * n64 / (1024 * eff):.3f} |")
     w = sqm["SQ_WAVES"]
     lines += ["", f"per wave: {sqm['SQ_INSTS_VALU'] / w:.4g} VALU ({sqm['SQ_INSTS_VALU_INT64'] / w:.4g} int64), "
               f"{sqm['SQ_INSTS_SALU'] / w:.4g} SALU, {sqm['SQ_INSTS_BRANCH'] / w:.4g} branches, "
@@ -109,6 +100,8 @@ def main():
         k = out["keccak"]
         lines += [f"{KECCAK} per launch: FETCH_SIZE x2 {k['fetch_bytes'] / 1e6:.1f} MB + WRITE_SIZE "
                   f"{k['write_bytes'] / 1e6:.1f} MB (algorithmic: 96 B x 2^24 messages = 1610.6 MB)", ""]
+    with open(os.path.join(root, "profiles", f"{tag}_pmc.json"), "w") as f:
+        json.dump(out, f, indent=1)
     with open(os.path.join(root, "profiles", f"{tag}_pmc.md"), "w") as f:
         f.write("\n".join(lines) + "\n")
     print("\n".join(lines))
