@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -83,6 +84,10 @@ class Lowerer {
         : N(nodes), nn(n_nodes), pool(pool), n_pool(n_pool), where(n_nodes, NONE),
           slot_of(n_nodes, NONE), remat(n_nodes, -2), cost(n_nodes, -1), W(n_wregs, &where), B(PF_NB, &where) {
         for (int s = PF_MAX_SPILL - 1; s >= 0; --s) free_slots.push_back(s);
+        // a variable is spilled (not regenerated) only when this many uses remain after its
+        // eviction (lower.py _var_spill_uses: the same environment variable)
+        const char* e = getenv("PF_VAR_SPILL_USES");
+        spill_min_uses = e ? std::max(1, atoi(e)) : 1;
     }
 
     std::vector<uint32_t> code;    // 4 words per instruction
@@ -138,6 +143,7 @@ class Lowerer {
     std::vector<int> use_off, use_at;  // uses of node i: use_at[use_off[i] .. use_off[i + 1])
     std::vector<int> where, slot_of, remat, cost, free_slots;
     int filling = NONE;  // the spilled node materialize() is restoring (not a steal candidate)
+    int spill_min_uses = 1;
     RegFile W, B;
 
     void order(const uint32_t* roots, size_t n_roots) {
@@ -185,6 +191,12 @@ class Lowerer {
             }
             events.push_back({true, (int)roots[ri]});
         }
+    }
+
+    int uses_after(int nd, int now) const {
+        const int* b = use_at.data() + use_off[nd];
+        const int* e = use_at.data() + use_off[nd + 1];
+        return (int)(e - std::upper_bound(b, e, now));
     }
 
     int next_use(int nd, int now) const {
@@ -296,7 +308,8 @@ class Lowerer {
                 // a variable used again is spilled while a slot is free (lower.py
                 // _VAR_SPILL_COST): one spill now, fills later, no generator re-run
                 const int sz = slot_of[nd] != NONE ? 1
-                             : (N[nd].kind == PFL_K_VAR && !free_slots.empty()) ? 2
+                             : (N[nd].kind == PFL_K_VAR && !free_slots.empty() &&
+                                uses_after(nd, t) >= spill_min_uses) ? 2
                                                                                 : remat_cost(nd);
                 const long long nu = -(long long)next_use(nd, t);
                 if (!have || sz < best_sz || (sz == best_sz && (nu < best_nu || (nu == best_nu && rg < best_r)))) {
@@ -310,7 +323,7 @@ class Lowerer {
                 r = best_r;
                 const int old = rf.holder[r];
                 if (N[old].kind == PFL_K_VAR && slot_of[old] == NONE && !free_slots.empty() &&
-                    next_use(old, t) < INF)
+                    uses_after(old, t) >= spill_min_uses)
                     spill(r, old, t, false);
             } else {  // spill the value used farthest in the future
                 int vr = -1, vfar = -1;

@@ -16,6 +16,9 @@ and is left to z3 (the engine never guesses).
 
 from __future__ import annotations
 
+import bisect
+import os
+
 from dataclasses import dataclass, field
 from typing import Dict, List, NamedTuple, Optional, Sequence, Tuple  # noqa: F401
 
@@ -316,6 +319,10 @@ _VAR_REMAT_COST = 6
 # registers re-ran the generator for every read (1,186 W_VAR for 69 variables in the
 # heaviest corpus bucket — most of its search time)
 _VAR_SPILL_COST = 2
+# ... only when at least this many uses remain after the eviction (1 = any later use); the
+# native lowering reads the same environment variable (pf_lower.cpp)
+def _var_spill_uses() -> int:
+    return max(1, int(os.environ.get("PF_VAR_SPILL_USES", "1")))
 
 
 # ---- native lowering (libpflower.so, include/pf_lower.h) ----------------------------------
@@ -538,13 +545,19 @@ def lower_py(dag: Dag, seed: int = 0, name: str = "", nw: int = ir.NW) -> Progra
     free_slots = list(range(ir.MAX_SPILL - 1, -1, -1))
     filling: List[Optional[int]] = [None]   # the spilled node materialize() is restoring
 
+    min_uses = _var_spill_uses()
+
+    def uses_after(nd: int, now: int) -> int:
+        lst = uses.get(nd, [])
+        return len(lst) - bisect.bisect_right(lst, now)
+
     def rank(t):
         def f(nd):
             if nd in slot_of:
                 cost = 1
             elif remat_size(nd) is None:
                 return None
-            elif dag.nodes[nd].kind == K_VAR and free_slots:
+            elif dag.nodes[nd].kind == K_VAR and free_slots and uses_after(nd, t) >= min_uses:
                 cost = _VAR_SPILL_COST
             else:
                 cost = remat_cost(nd)
@@ -579,7 +592,7 @@ def lower_py(dag: Dag, seed: int = 0, name: str = "", nw: int = ir.NW) -> Progra
     def alloc(rf, nd, t, pinned):
         def on_evict(rg, old):
             if dag.nodes[old].kind == K_VAR and old not in slot_of and free_slots \
-                    and next_use(old, t) < (1 << 30):
+                    and uses_after(old, t) >= min_uses:
                 spill(rg, old, t, False)
         return rf.alloc(nd, rank(t), pinned, lambda rg, x: spill(rg, x, t), lambda x: next_use(x, t),
                         on_evict)

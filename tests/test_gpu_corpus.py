@@ -50,3 +50,64 @@ def test_bucket_cache_answers_repeated_queries(engine, monkeypatch):
         if not parents:
             assert [m is None for m in first] == [m is None for m in again]
     assert gpu_check.STATS.recheck_failures == 0
+
+
+def _run_pipeline(eng, c, cfg, live):
+    """check_sets over the corpus (one batch, or fork pairs one call at a time in live
+    order) on ``eng``; returns the verdicts, witness values, the bucket cache's witnesses and
+    every launch's per-bucket smallest witness indices."""
+    from mythril_amd.smt import native_terms
+
+    launches = []
+    orig = eng.check
+
+    def check(db, *a, **k):
+        r = orig(db, *a, **k)
+        launches.append(r.found.tolist())
+        return r
+
+    eng.check = check
+    try:
+        gpu_check.reset_cache()
+        groups = corpus.live_order_groups(c.queries) if live else [c.queries]
+        models = []
+        for g in groups:
+            models += gpu_check.check_sets([q.constraints for q in g], registry=c.kfm.registry, config=cfg)
+    finally:
+        eng.check = orig
+    verdicts = [m is not None for m in models]
+    values = [dict(m.w.vars) if m is not None else None for m in models]
+
+    def ints(v):
+        return native_terms.ints_of(v) if hasattr(v, "dtype") else [int(x or 0) for x in v]
+
+    cache = {k: ints(v) for k, (_, v) in gpu_check._CACHE.items()}
+    return verdicts, values, cache, launches
+
+
+@pytest.mark.parametrize("hints,parents,live", [(True, False, False), (False, False, False),
+                                                (False, True, True)])
+def test_gpu_pipeline_equals_oracle_pipeline(engine, monkeypatch, hints, parents, live):
+    """The same discharge pipeline (independence buckets, hint models, parent models, native
+    lowering, batch packing, witness materialisation and re-check) with only the engine
+    swapped — the MI355X kernel vs the C oracle (tests/oracle_engine.py) — gives identical
+    per-query verdicts and witness values, identical bucket witnesses, and identical
+    smallest witness indices in every launch: ref support_utils.py:57-71's predicate on
+    LASER shapes, end to end."""
+    from dataclasses import replace
+
+    import oracle_engine
+    import mythril_amd.engine as E
+
+    c = corpus.build(6, 2, seed=7)
+    cfg = replace(gpu_check.CONFIG, hints=hints, parents=parents, budget=2048, timeout_ms=0)
+    gpu = _run_pipeline(E.get_engine(), c, cfg, live)
+    ora_eng = oracle_engine.OracleEngine()
+    monkeypatch.setattr(E, "get_engine", lambda device=None: ora_eng)
+    ora = _run_pipeline(ora_eng, c, cfg, live)
+    gpu_check.reset_cache()
+    assert gpu[0] == ora[0]
+    assert gpu[1] == ora[1]
+    assert gpu[2] == ora[2]
+    assert gpu[3] == ora[3]
+    assert sum(gpu[0]) > 0 and len(gpu[3]) > 0

@@ -22,8 +22,11 @@ i=0
 for rep in 1 2; do
 for v in base "$@"; do
   i=$((i+1))
-  if [ "$v" = base ]; then L=""; else L="--lib build_var/lib_$v.so"; fi
-  timeout -k 10 200 $B $L > $O/ab$i.log 2>&1 || { echo "variant $v failed"; tail -5 $O/ab$i.log; exit 1; }
+  # a variant "env:NAME=VALUE" runs the product library with that environment variable
+  # (host-side policies, e.g. the lowering's PF_VAR_SPILL_USES); any other name is a library
+  E=""
+  if [ "$v" = base ]; then L=""; elif [ "${v#env:}" != "$v" ]; then L=""; E="${v#env:}"; else L="--lib build_var/lib_$v.so"; fi
+  timeout -k 10 200 env $E $B $L > $O/ab$i.log 2>&1 || { echo "variant $v failed"; tail -5 $O/ab$i.log; exit 1; }
   python -c "import json,sys; d=json.loads(open('$O/ab$i.log').read().strip().splitlines()[-1]); r=d['roofline']; print('$v', round(d['value']/1e9,4), 'Gevals/s', round(r['kernel_ms_avg'],3), 'ms frac', round(r['frac'],4), 'early', round(d['early_exit']['unplanted']['kernel_ms'],3), round(d['early_exit']['planted']['kernel_ms'],3))"
 done
 done

@@ -222,6 +222,26 @@ KERN3(k_bfi, uint32_t, "v_bfi_b32")
 KERN3(k_alignbit, uint32_t, "v_alignbit_b32")
 KERN3(k_add3, uint32_t, "v_add3_u32")
 KERN2(k_addf32, float, "v_add_f32")
+// v_bitop3_b32 carries an 8-bit truth table (0x96 = a ^ b ^ c, the Keccak/Philox xor3)
+#define BODY3B                                                                                 \
+    asm volatile("v_bitop3_b32 %0, %8, %9, %10 bitop3:0x96\n\tv_bitop3_b32 %1, %9, %10, %11 bitop3:0x96\n\t" \
+                 "v_bitop3_b32 %2, %10, %11, %12 bitop3:0x96\n\tv_bitop3_b32 %3, %11, %12, %13 bitop3:0x96\n\t" \
+                 "v_bitop3_b32 %4, %12, %13, %14 bitop3:0x96\n\tv_bitop3_b32 %5, %13, %14, %15 bitop3:0x96\n\t" \
+                 "v_bitop3_b32 %6, %14, %15, %8 bitop3:0x96\n\tv_bitop3_b32 %7, %15, %8, %9 bitop3:0x96"       \
+                 : "=v"(a0), "=v"(a1), "=v"(a2), "=v"(a3), "=v"(a4), "=v"(a5), "=v"(a6), "=v"(a7) \
+                 : "v"(b0), "v"(b1), "v"(b2), "v"(b3), "v"(b4), "v"(b5), "v"(b6), "v"(b7));     \
+    asm volatile("v_bitop3_b32 %0, %8, %9, %10 bitop3:0x96\n\tv_bitop3_b32 %1, %9, %10, %11 bitop3:0x96\n\t" \
+                 "v_bitop3_b32 %2, %10, %11, %12 bitop3:0x96\n\tv_bitop3_b32 %3, %11, %12, %13 bitop3:0x96\n\t" \
+                 "v_bitop3_b32 %4, %12, %13, %14 bitop3:0x96\n\tv_bitop3_b32 %5, %13, %14, %15 bitop3:0x96\n\t" \
+                 "v_bitop3_b32 %6, %14, %15, %8 bitop3:0x96\n\tv_bitop3_b32 %7, %15, %8, %9 bitop3:0x96"       \
+                 : "=v"(b0), "=v"(b1), "=v"(b2), "=v"(b3), "=v"(b4), "=v"(b5), "=v"(b6), "=v"(b7) \
+                 : "v"(a0), "v"(a1), "v"(a2), "v"(a3), "v"(a4), "v"(a5), "v"(a6), "v"(a7))
+extern "C" __global__ void __launch_bounds__(256) k_bitop3_d(uint32_t iters, uint64_t* out) {
+    R16(uint32_t, (uint32_t)threadIdx.x);
+    for (uint32_t i = 0; i < iters; i++) { BODY3B; }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = SINK16;
+}
+KERN3D(k_alignbit_d, uint32_t, "v_alignbit_b32")
 KERN2(k_xor, uint32_t, "v_xor_b32")
 // carry-out forms (the 256-bit add chain's instructions), carry into VCC
 
@@ -255,7 +275,9 @@ int main(int argc, char** argv) {
         {"v_bfi_b32 (3 regs)", k_bfi_d}, {"v_add3_u32 (3 regs)", k_add3_d}, {"v_fma_f32 (3 regs)", k_fma_d},
         {"v_cndmask_b32 vcc", k_cndmask}, {"v_cndmask_b32 s[]", k_cndmask_s},
         {"v_cndmask_b32_e64 vcc", k_cndmask_e64vcc}, {"v_cndmask vcc<-SALU", k_cndmask_svcc}, {"v_mad_u64_u32", k_mad64},
-        {"add256 chain e32/vcc", k_add256_e32}, {"add256 chain e64/sgpr", k_add256_e64}};
+        {"add256 chain e32/vcc", k_add256_e32}, {"add256 chain e64/sgpr", k_add256_e64},
+        {"v_bitop3_b32 (3 regs)", k_bitop3_d},
+        {"v_alignbit_b32 (3 regs)", k_alignbit_d}};
     hipEvent_t e0, e1;
     CHK(hipEventCreate(&e0)); CHK(hipEventCreate(&e1));
     const uint32_t iters = 4096;
