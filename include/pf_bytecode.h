@@ -113,6 +113,16 @@ enum pf_opcode {
  * never by the host lowering, whose programs the oracles evaluate as written. */
 #define PF_I_ASSERT (1u << 24)
 
+/* w0 bits 25 / 26: operand a / b is the set's constant const[a] / const[b] (the 8-bit
+ * register field holds the constant index) instead of a W register.  Set only by
+ * pf_batch_create's constant-operand peephole, which deletes a W_CONST whose every reader
+ * (up to the next write of its register) can take the constant this way — one dispatched
+ * instruction and one register write-back less per constant; the kernel reads the
+ * constant with a scalar load where it would have copied the register.  Never set by the
+ * host lowering (the oracles evaluate the program as lowered). */
+#define PF_I_KA (1u << 25)
+#define PF_I_KB (1u << 26)
+
 /* operand traffic bits (w0 >> 18): reads W[a], reads W[b], writes W[d] */
 #define PF_TR_RA 1u
 #define PF_TR_RB 2u

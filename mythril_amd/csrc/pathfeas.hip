@@ -284,11 +284,125 @@ int check_collect(Batch* B, hipStream_t st, pf_stats* stats, std::vector<uint32_
     return 0;
 }
 
+// The device form of a validated batch (traffic / unit bits already set): the peepholes
+// below rewrite the program the kernel runs, never the caller's arrays (the oracles evaluate
+// the program as lowered).  Shared by pf_batch_create and the host-only test export
+// pf_device_program.
+void device_program(const std::vector<uint32_t>& code_fixed, std::vector<pf_set_desc>& descs_out,
+                    std::vector<uint32_t>& code_out) {
+    // Peephole (semantics-preserving): an ASSERT of the B register that the instruction just
+    // before it wrote — a compare or a bool op, the shape every root takes — becomes the
+    // PF_I_ASSERT flag of that instruction, one dispatched instruction less per asserted
+    // root (DESIGN.md §3).  The caller's arrays are unchanged; the device gets the compacted
+    // program with shifted code ranges.
+    code_out.clear();
+    code_out.reserve(code_fixed.size());
+    const size_t n_sets = descs_out.size();
+    for (size_t s = 0; s < n_sets; s++) {
+        pf_set_desc& d = descs_out[s];
+        const uint32_t* src = code_fixed.data() + 4 * (size_t)d.code_off;
+        const size_t first = code_out.size() / 4;
+        for (uint32_t i = 0; i < d.n_ins; i++) {
+            const uint32_t* I = src + 4 * (size_t)i;
+            const uint32_t op = I[0] & 0xffu;
+            if (op == PF_ASSERT && code_out.size() / 4 > first) {
+                uint32_t* P = code_out.data() + code_out.size() - 4;
+                const uint32_t pop = P[0] & 0xffu, unit = pf_op_unit(pop);
+                if ((unit == PF_U_CMP || (unit == PF_U_BOOL && pop != PF_ASSERT && pop != PF_B_SPILL)) &&
+                    !(P[0] & PF_I_ASSERT) && (P[1] & 0xffu) == ((I[1] >> 8) & 0xffu)) {
+                    P[0] |= PF_I_ASSERT;
+                    continue;
+                }
+            }
+            code_out.insert(code_out.end(), I, I + 4);
+        }
+        d.code_off = (uint32_t)first;
+        d.n_ins = (uint32_t)(code_out.size() / 4 - first);
+    }
+#ifndef PF_NO_CONST_FUSE
+    // Peephole (semantics-preserving): a W_CONST whose register is read, until its next
+    // write, only as the a / b operand of W-reading instructions is deleted and those readers
+    // take the constant directly (PF_I_KA / PF_I_KB with the constant index in the register
+    // field, traffic bit cleared).  Config 3: ~7 of ~60 instructions per set are W_CONST.
+    {
+        std::vector<uint32_t> fused;
+        fused.reserve(code_out.size());
+        for (size_t s = 0; s < n_sets; s++) {
+            pf_set_desc& d = descs_out[s];
+            uint32_t* P = code_out.data() + 4 * (size_t)d.code_off;
+            std::vector<uint8_t> drop(d.n_ins, 0);
+            for (uint32_t i = 0; i < d.n_ins; i++) {
+                const uint32_t* I = P + 4 * (size_t)i;
+                if ((I[0] & 0xffu) != PF_W_CONST || I[2] > 0xffu) continue;
+                const uint32_t r = I[1] & 0xffu, k = I[2];
+                // the readers up to the next write of r: all must take the constant
+                bool ok = true;
+                uint32_t j = i + 1, n_read = 0;
+                for (; j < d.n_ins; j++) {
+                    const uint32_t* J = P + 4 * (size_t)j;
+                    const uint32_t jop = J[0] & 0xffu, jtr = (J[0] >> 18) & 7u;
+                    const uint32_t ja = (J[1] >> 8) & 0xffu, jb = (J[1] >> 16) & 0xffu;
+                    const bool ra = (jtr & PF_TR_RA) && ja == r, rb = (jtr & PF_TR_RB) && jb == r;
+                    if (ra || rb) {
+                        n_read++;
+                        if (jop == PF_W_SPILL || jop == PF_W_MOV) { ok = false; break; }
+                    }
+                    if ((jtr & PF_TR_WW) && (J[1] & 0xffu) == r) break;  // r rewritten (after the read)
+                    if (jop == PF_END) break;
+                }
+                if (!ok || n_read == 0) continue;
+                for (uint32_t t = i + 1; t < j || (t == j && t < d.n_ins); t++) {
+                    uint32_t* J = P + 4 * (size_t)t;
+                    const uint32_t jtr = (J[0] >> 18) & 7u;
+                    const uint32_t ja = (J[1] >> 8) & 0xffu, jb = (J[1] >> 16) & 0xffu;
+                    if ((jtr & PF_TR_RA) && ja == r) {
+                        J[0] = (J[0] & ~(PF_TR_RA << 18)) | PF_I_KA;
+                        J[1] = (J[1] & ~0xff00u) | (k << 8);
+                    }
+                    if ((jtr & PF_TR_RB) && jb == r) {
+                        J[0] = (J[0] & ~(PF_TR_RB << 18)) | PF_I_KB;
+                        J[1] = (J[1] & ~0xff0000u) | (k << 16);
+                    }
+                    if (t == j) break;
+                }
+                drop[i] = 1;
+            }
+            const size_t first = fused.size() / 4;
+            for (uint32_t i = 0; i < d.n_ins; i++)
+                if (!drop[i]) fused.insert(fused.end(), P + 4 * (size_t)i, P + 4 * (size_t)i + 4);
+            d.code_off = (uint32_t)first;
+            d.n_ins = (uint32_t)(fused.size() / 4 - first);
+        }
+        code_out.swap(fused);
+    }
+#endif
+}
+
 }  // namespace
 
 extern "C" {
 
 int pf_version(void) { return 2; }
+
+// Host only (no HIP call, tests/test_device_program.py): the program pf_batch_create would put
+// on the device — traffic / unit bits recomputed from the opcodes, then the peepholes.
+// code_out needs room for n_ins instructions (the peepholes only delete); descs_out n_sets.
+int pf_device_program(const uint32_t* code, size_t n_ins, const pf_set_desc* descs, size_t n_sets,
+                      uint32_t* code_out, size_t* n_ins_out, pf_set_desc* descs_out) {
+    std::vector<uint32_t> fixed(code, code + 4 * n_ins);
+    for (size_t i = 0; i < n_ins; i++) {
+        uint32_t* I = fixed.data() + 4 * i;
+        const uint32_t op = I[0] & 0xffu;
+        I[0] = (I[0] & 0x3ffffu) | (pf_op_traffic(op) << 18) | (pf_op_unit(op) << 21);
+    }
+    std::vector<pf_set_desc> d(descs, descs + n_sets);
+    std::vector<uint32_t> out;
+    device_program(fixed, d, out);
+    memcpy(code_out, out.data(), out.size() * 4);
+    *n_ins_out = out.size() / 4;
+    memcpy(descs_out, d.data(), n_sets * sizeof(pf_set_desc));
+    return 0;
+}
 
 #ifdef PF_PROFILE_UNITS
 // profiling builds only (tools/unitprof.py): per-unit s_memtime cycles of a batch's last launch
@@ -452,35 +566,9 @@ int pf_batch_create_on(int device, const uint32_t* code, size_t n_ins, const uin
             if (bres) bdef |= 1u << (rd & 31u);
         }
     }
-    // Peephole (semantics-preserving): an ASSERT of the B register that the instruction just
-    // before it wrote — a compare or a bool op, the shape every root takes — becomes the
-    // PF_I_ASSERT flag of that instruction, one dispatched instruction less per asserted
-    // root (DESIGN.md §3).  The caller's arrays are unchanged; the device gets the compacted
-    // program with shifted code ranges.
     std::vector<uint32_t> code_out;
-    code_out.reserve(code_fixed.size());
     std::vector<pf_set_desc> descs_out(descs, descs + n_sets);
-    for (size_t s = 0; s < n_sets; s++) {
-        pf_set_desc& d = descs_out[s];
-        const uint32_t* src = code_fixed.data() + 4 * (size_t)d.code_off;
-        const size_t first = code_out.size() / 4;
-        for (uint32_t i = 0; i < d.n_ins; i++) {
-            const uint32_t* I = src + 4 * (size_t)i;
-            const uint32_t op = I[0] & 0xffu;
-            if (op == PF_ASSERT && code_out.size() / 4 > first) {
-                uint32_t* P = code_out.data() + code_out.size() - 4;
-                const uint32_t pop = P[0] & 0xffu, unit = pf_op_unit(pop);
-                if ((unit == PF_U_CMP || (unit == PF_U_BOOL && pop != PF_ASSERT && pop != PF_B_SPILL)) &&
-                    !(P[0] & PF_I_ASSERT) && (P[1] & 0xffu) == ((I[1] >> 8) & 0xffu)) {
-                    P[0] |= PF_I_ASSERT;
-                    continue;
-                }
-            }
-            code_out.insert(code_out.end(), I, I + 4);
-        }
-        d.code_off = (uint32_t)first;
-        d.n_ins = (uint32_t)(code_out.size() / 4 - first);
-    }
+    device_program(code_fixed, descs_out, code_out);
     code = code_out.data();
     n_ins = code_out.size() / 4;
     descs = descs_out.data();

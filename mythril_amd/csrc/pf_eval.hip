@@ -619,6 +619,21 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
             if (__builtin_expect((tr & PF_TR_RA) != 0u, 1)) RD_W(x, W, a, LPB);
             if (__builtin_expect((tr & PF_TR_RB) != 0u, 1)) RD_W(y, W, b, LPB);
         }
+        // constant operands (pf_batch_create's peephole deleted their W_CONST): one scalar
+        // load of const[a] / const[b] each, waited for here, before the next fetch goes out
+        if (__builtin_expect((I.x & (PF_I_KA | PF_I_KB)) != 0u, 0)) {
+            if (I.x & PF_I_KA) {
+                const uint32_t* cp = S.consts + (size_t)a * 8u;
+#pragma unroll
+                for (int i = 0; i < 8; i++) x.l[i] = cp[i];
+            }
+            if (I.x & PF_I_KB) {
+                const uint32_t* cp = S.consts + (size_t)b * 8u;
+#pragma unroll
+                for (int i = 0; i < 8; i++) y.l[i] = cp[i];
+            }
+            PF_WAIT_LDS();
+        }
 #ifndef PF_FETCH_EARLY
         __builtin_amdgcn_sched_barrier(0);
         In = fetch_ins(++ip);

@@ -1,0 +1,157 @@
+"""CPU: the device form of a batch (pf_batch_create's peepholes, exported host-only as
+pf_device_program) computes what the lowered program computes.
+
+The kernel runs a rewritten program: an ASSERT folded into the compare before it
+(PF_I_ASSERT) and a W_CONST folded into every reader of its register (PF_I_KA / PF_I_KB:
+the register field holds the constant index).  ``eval_device`` below is the kernel's reading
+of those flags, restated for the test; the oracle evaluates the program as lowered.  The GPU
+parity tests then compare the kernel itself against the oracle."""
+
+import ctypes
+import random
+
+import numpy as np
+import pytest
+
+import pyoracle as O
+from mythril_amd import _lib, ir, synth
+
+I_ASSERT, I_KA, I_KB = 1 << 24, 1 << 25, 1 << 26
+
+
+def device_program(batch):
+    L = _lib.lib()
+    code = np.ascontiguousarray(batch.code, dtype=np.uint32)
+    descs = np.ascontiguousarray(batch.descs, dtype=np.uint32)
+    out = np.zeros_like(code)
+    dout = np.zeros_like(descs)
+    n = ctypes.c_size_t()
+    _lib.check(L.pf_device_program(_lib.ptr_u32(code), len(code), _lib.ptr_u32(descs), len(descs),
+                                   _lib.ptr_u32(out), ctypes.byref(n), _lib.ptr_u32(dout)),
+               "pf_device_program")
+    return out[:n.value], dout
+
+
+def eval_device(sv, code_rows, values):
+    """SetView.evaluate with the device flags: a KA / KB operand is const[a] / const[b] (held
+    here in two spare register slots), a PF_I_ASSERT op also asserts its B result."""
+    W, B, S = {}, {}, {}
+    root = True
+    for (w0, w1, aux0, aux1) in code_rows:
+        if w0 & 0xFF == O.OP["END"]:
+            break
+        if w0 & I_KA:
+            W[0xFE] = sv.consts[(w1 >> 8) & 0xFF]
+            w1 = (w1 & ~0xFF00) | (0xFE << 8)
+        if w0 & I_KB:
+            W[0xFD] = sv.consts[(w1 >> 16) & 0xFF]
+            w1 = (w1 & ~0xFF0000) | (0xFD << 16)
+        root = _step((w0 & ~(I_ASSERT | I_KA | I_KB), w1, aux0, aux1), sv.consts, W, B, S, values, root)
+        if w0 & I_ASSERT:
+            root = root and B[w1 & 0xFF]
+    return root
+
+
+def _step(ins, consts, W, B, S, values, root):
+    """One instruction of pyoracle's evaluator (SetView.evaluate) on shared registers."""
+    w0, w1, aux0, aux1 = ins
+    op, w = w0 & 0xFF, (w0 >> 8) & 0x3FF
+    d, a, b, c = w1 & 0xFF, (w1 >> 8) & 0xFF, (w1 >> 16) & 0xFF, (w1 >> 24) & 0xFF
+    M = O.M
+    if op == O.OP["W_CONST"]:
+        W[d] = consts[aux0] & M(w)
+    elif op == O.OP["W_VAR"]:
+        W[d] = int(values[aux0]) & M(w)
+    elif op == O.OP["W_MOV"]:
+        W[d] = W[a] & M(w)
+    elif op in O._WBIN:
+        W[d] = O._WBIN[op](W[a], W[b], w)
+    elif op == O.OP["W_NOT"]:
+        W[d] = O.bvnot(W[a], w)
+    elif op == O.OP["W_NEG"]:
+        W[d] = O.bvneg(W[a], w)
+    elif op == O.OP["W_EXTRACT"]:
+        W[d] = O.extract(W[a], aux0, w)
+    elif op == O.OP["W_CONCAT"]:
+        W[d] = O.concat(W[a], W[b], aux0) & M(w)
+    elif op == O.OP["W_SEXT"]:
+        W[d] = O.sign_extend(W[a], aux0, w)
+    elif op == O.OP["W_ITE"]:
+        W[d] = W[a] if B[c] else W[b]
+    elif op == O.OP["W_HASH"]:
+        W[d] = O.uf_hash(W[a], aux0) & M(w)
+    elif op == O.OP["W_SPILL"]:
+        S[aux0] = W[a]
+    elif op == O.OP["W_FILL"]:
+        W[d] = S[aux0] & M(w)
+    elif op == O.OP["B_SPILL"]:
+        S[aux0] = int(B[a])
+    elif op == O.OP["B_FILL"]:
+        B[d] = bool(S[aux0] & 1)
+    elif op == O.OP["B_CONST"]:
+        B[d] = bool(aux0 & 1)
+    elif op == O.OP["B_VAR"]:
+        B[d] = bool(int(values[aux0]) & 1)
+    elif op in O._BCMP:
+        B[d] = bool(O._BCMP[op](W[a], W[b], w))
+    elif op == O.OP["B_AND"]:
+        B[d] = B[a] and B[b]
+    elif op == O.OP["B_OR"]:
+        B[d] = B[a] or B[b]
+    elif op == O.OP["B_XOR"]:
+        B[d] = B[a] != B[b]
+    elif op == O.OP["B_NOT"]:
+        B[d] = not B[a]
+    elif op == O.OP["B_ITE"]:
+        B[d] = B[a] if B[c] else B[b]
+    elif op == O.OP["ASSERT"]:
+        root = root and B[a]
+    else:
+        raise ValueError(op)
+    return root
+
+
+def _programs(monkeypatch):
+    from mythril_amd import keccak_manager as KM
+    from mythril_amd.smt import symbol_factory
+
+    # concrete hashes from the oracle's Keccak (the corpus would ask the engine otherwise)
+    monkeypatch.setattr(KM.KeccakFunctionManager, "find_concrete_keccak", staticmethod(
+        lambda data: symbol_factory.BitVecVal(
+            int.from_bytes(O.keccak256(data.value.to_bytes(data.size() // 8, "big")), "big"), 256)))
+    progs = [synth.random_dag_set(i, plant=(i % 2 == 0))[0] for i in range(40)]
+    from mythril_amd import corpus
+    c = corpus.build(3, 2, seed=11)
+    from mythril_amd.smt.independence import buckets
+    from mythril_amd.smt.to_dag import TermLowering
+    from mythril_amd.lower import LoweringError, lower
+    n = 0
+    for q in c.queries:
+        for bk in buckets(q.constraints):
+            try:
+                lo = TermLowering(c.kfm.registry).lower(bk)
+            except LoweringError:
+                continue
+            progs.append(lower(lo.dag, seed=n))
+            n += 1
+            if n >= 60:
+                return progs
+    return progs
+
+
+def test_device_program_matches_the_lowered_program(monkeypatch):
+    batch = ir.Batch(_programs(monkeypatch))
+    code, descs = device_program(batch)
+    n_const_fused = int(((code[:, 0] & (I_KA | I_KB)) != 0).sum())
+    n_wconst = int(((batch.code[:, 0] & 0xFF) == ir.W_CONST).sum())
+    n_wconst_dev = int(((code[:, 0] & 0xFF) == ir.W_CONST).sum())
+    assert n_const_fused > 0 and n_wconst_dev < n_wconst
+    rng = random.Random(3)
+    for s in range(len(batch.descs)):
+        sv = O.SetView.from_batch(batch, s)
+        d = descs[s]
+        rows = [tuple(int(x) for x in r) for r in code[d[0]:d[0] + d[1]]]
+        assert rows[-1][0] & 0xFF == 0                      # still END-terminated
+        cands = sv.gen_assignments(np.arange(24, dtype=np.uint64), 5)
+        for vals in cands + [[rng.getrandbits(sv.var_width(v)) for v in range(len(sv.schema))]]:
+            assert eval_device(sv, rows, vals) == sv.evaluate(vals), s
