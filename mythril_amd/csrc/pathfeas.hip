@@ -862,6 +862,14 @@ int pf_keccak256_fixed_dev(const uint8_t* d_data, uint32_t len, size_t n, uint8_
     if (switch_stream(D, st)) return -1;
     HIPCHK(hipEventRecord(D->ev0, st));
     const bool fast = (len % 16u) == 0u && len < 136u && (((uintptr_t)d_data) & 15u) == 0u;
+#ifdef PF_KECCAK_PERSIST
+    if (fast && len == 64u) {
+        // chip-filling persistent grid: PF_KECCAK_PERSIST 256-thread blocks per CU
+        const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, (uint64_t)D->num_cus * PF_KECCAK_PERSIST);
+        hipLaunchKernelGGL(pf_keccak_fixed64_persist_kernel, dim3((uint32_t)blocks), dim3(256), 0,
+                           st, d_data, (uint64_t)n, d_out32);
+    } else
+#endif
     if (fast)
         hipLaunchKernelGGL(pf_keccak_fixed_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0,
                            st, d_data, len, (uint64_t)n, d_out32);

@@ -208,6 +208,51 @@ pf_keccak_stride_kernel(const uint8_t* __restrict__ data, uint32_t len, uint64_t
     absorb_and_squeeze(stage + threadIdx.x, data + i * (uint64_t)len, len, out32 + 32 * i);
 }
 
+// Persistent form of the fixed-length fast path (PF_KECCAK_PERSIST): a chip-filling grid in
+// which every lane walks messages i, i + stride, ...; the next message's 16-byte chunks are
+// loaded while the current permutation runs, so a wave's load latency overlaps its own
+// VALU work instead of relying on other waves alone.
+// NQ: 16-byte chunks per message (4 for the 64-byte key||slot preimages), a template so the
+// prefetch buffer holds only the chunks that exist
+template <int NQ>
+__device__ __forceinline__ void keccak_persist(const uint8_t* __restrict__ data, uint32_t len, uint64_t n,
+                                               uint8_t* __restrict__ out32) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    constexpr uint32_t nq = NQ;
+    uint4 nxt[NQ];
+#pragma unroll
+    for (int k = 0; k < NQ; k++)
+        nxt[k] = i < n ? ((const uint4*)(data + i * (uint64_t)len))[k] : make_uint4(0u, 0u, 0u, 0u);
+    for (; i < n; i += stride) {
+        Lane a[25];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint4 v = k < NQ ? nxt[k < NQ ? k : 0] : make_uint4(0u, 0u, 0u, 0u);
+            a[2 * k] = Lane{v.x, v.y};
+            a[2 * k + 1] = Lane{v.z, v.w};
+        }
+        const uint64_t j = i + stride;
+#pragma unroll
+        for (int k = 0; k < NQ; k++)
+            nxt[k] = j < n ? ((const uint4*)(data + j * (uint64_t)len))[k] : make_uint4(0u, 0u, 0u, 0u);
+        a[16] = Lane{0u, 0x80000000u};
+#pragma unroll
+        for (int k = 17; k < 25; k++) a[k] = Lane{0u, 0u};
+#pragma unroll
+        for (int k = 0; k < 17; k++)
+            if ((uint32_t)k == (len >> 3)) a[k].lo ^= 0x01u;
+        keccakf<true>(a);
+        squeeze(a, out32 + 32 * i);
+    }
+}
+
+// the 64-byte key||slot preimages (config 4); other lengths take pf_keccak_fixed_kernel
+extern "C" __global__ void __launch_bounds__(256)
+pf_keccak_fixed64_persist_kernel(const uint8_t* __restrict__ data, uint64_t n, uint8_t* __restrict__ out32) {
+    keccak_persist<4>(data, 64u, n, out32);
+}
+
 // fixed-length single-block fast path: the host launches it when len % 16 == 0,
 // len < 136 and the buffer is 16-byte aligned (16-byte vector loads, two 16-byte digest
 // stores, all 24 rounds unrolled).

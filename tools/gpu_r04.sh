@@ -10,3 +10,11 @@ if [ -x tools/movbench ]; then
   for w in 4 8; do timeout -k 10 120 ./tools/movbench $w >> $O/movbench.log 2>&1 || { echo "movbench failed"; exit 1; }; done
   echo MOVBENCH-DONE
 fi
+# Keccak variants (KECCAK="kp6 kp8"): one process per library, the product first and last
+if [ -n "$KECCAK" ]; then
+  for v in base $KECCAK base; do
+    if [ "$v" = base ]; then L=""; else L="--lib build_var/lib_$v.so"; fi
+    timeout -k 10 120 python -u tools/keccak_ab.py $L >> $O/keccak_ab.log 2>&1 || { echo "keccak $v failed"; tail -5 $O/keccak_ab.log; exit 1; }
+  done
+  cat $O/keccak_ab.log | grep ms_median
+fi
