@@ -354,7 +354,10 @@ PF_INL u256 gen_var(const SetCtx& S, uint32_t v, uint32_t cand) {
     for (int i = 0; i < 8; i++) g.l[i] = gp[i];
 #endif
     const uint4 r0 = philox_gen(p0, v, 0u, S.k0, S.k1);
-    const uint4 r1 = philox_gen(p0, v, 1u, S.k0, S.k1);
+    // r1 only feeds limbs 4..7 of the random arm, which the final mask clears for w <= 128
+    // (bytes, selectors, small counters): skipped there under a wave-uniform branch
+    uint4 r1 = make_uint4(0u, 0u, 0u, 0u);
+    if (w > 128u) r1 = philox_gen(p0, v, 1u, S.k0, S.k1);
     const bool has_parent = pslot != PF_NO_PARENT;
     u256 par = pf::zero256();
     if (has_parent) {
