@@ -319,6 +319,68 @@ void device_program(const std::vector<uint32_t>& code_fixed, std::vector<pf_set_
         d.code_off = (uint32_t)first;
         d.n_ins = (uint32_t)(code_out.size() / 4 - first);
     }
+#ifndef PF_NO_MOV_FUSE
+    // Peephole (semantics-preserving): a W_MOV that zero-extends (the last writer of its
+    // source register wrote a value no wider than the move's width — values are kept
+    // zero-extended, so the move copies it unchanged) is deleted and the readers of its
+    // destination, up to that register's next write, read the source register instead —
+    // provided the source is not rewritten before the last of them.
+    {
+        std::vector<uint32_t> kept;
+        kept.reserve(code_out.size());
+        for (size_t s = 0; s < n_sets; s++) {
+            pf_set_desc& d = descs_out[s];
+            uint32_t* P = code_out.data() + 4 * (size_t)d.code_off;
+            std::vector<uint8_t> drop(d.n_ins, 0);
+            for (uint32_t i = 0; i < d.n_ins; i++) {
+                const uint32_t* I = P + 4 * (size_t)i;
+                if ((I[0] & 0xffu) != PF_W_MOV) continue;
+                const uint32_t dst = I[1] & 0xffu, src = (I[1] >> 8) & 0xffu, w = (I[0] >> 8) & 0x3ffu;
+                // the width of the value in src: its last writer before i
+                uint32_t ww = 0xffffffffu;
+                for (uint32_t k = i; k-- > 0;) {
+                    const uint32_t* K = P + 4 * (size_t)k;
+                    if (drop[k]) continue;
+                    if ((((K[0] >> 18) & 7u) & PF_TR_WW) && (K[1] & 0xffu) == src) {
+                        ww = (K[0] >> 8) & 0x3ffu;
+                        break;
+                    }
+                }
+                if (ww > w) continue;  // a truncation (or no writer): keep the move
+                // readers of dst up to its next write; src must stay unwritten until the last
+                bool ok = true, src_dead = false;
+                uint32_t j = i + 1, last = i;
+                for (; j < d.n_ins; j++) {
+                    const uint32_t* J = P + 4 * (size_t)j;
+                    const uint32_t jtr = (J[0] >> 18) & 7u;
+                    const bool reads = ((jtr & PF_TR_RA) && ((J[1] >> 8) & 0xffu) == dst) ||
+                                       ((jtr & PF_TR_RB) && ((J[1] >> 16) & 0xffu) == dst);
+                    if (reads) {
+                        if (src_dead) { ok = false; break; }
+                        last = j;
+                    }
+                    if ((jtr & PF_TR_WW) && (J[1] & 0xffu) == dst) break;
+                    if ((jtr & PF_TR_WW) && (J[1] & 0xffu) == src) src_dead = true;
+                    if ((J[0] & 0xffu) == PF_END) break;
+                }
+                if (!ok) continue;
+                for (uint32_t t = i + 1; t <= last; t++) {
+                    uint32_t* J = P + 4 * (size_t)t;
+                    const uint32_t jtr = (J[0] >> 18) & 7u;
+                    if ((jtr & PF_TR_RA) && ((J[1] >> 8) & 0xffu) == dst) J[1] = (J[1] & ~0xff00u) | (src << 8);
+                    if ((jtr & PF_TR_RB) && ((J[1] >> 16) & 0xffu) == dst) J[1] = (J[1] & ~0xff0000u) | (src << 16);
+                }
+                drop[i] = 1;
+            }
+            const size_t first = kept.size() / 4;
+            for (uint32_t i = 0; i < d.n_ins; i++)
+                if (!drop[i]) kept.insert(kept.end(), P + 4 * (size_t)i, P + 4 * (size_t)i + 4);
+            d.code_off = (uint32_t)first;
+            d.n_ins = (uint32_t)(kept.size() / 4 - first);
+        }
+        code_out.swap(kept);
+    }
+#endif
 #ifndef PF_NO_CONST_FUSE
     // Peephole (semantics-preserving): a W_CONST whose register is read, until its next
     // write, only as the a / b operand of W-reading instructions is deleted and those readers
