@@ -306,13 +306,21 @@ void device_program(const std::vector<uint32_t>& code_fixed, std::vector<pf_set_
             const uint32_t* I = src + 4 * (size_t)i;
             const uint32_t op = I[0] & 0xffu;
             if (op == PF_ASSERT && code_out.size() / 4 > first) {
-                uint32_t* P = code_out.data() + code_out.size() - 4;
-                const uint32_t pop = P[0] & 0xffu, unit = pf_op_unit(pop);
-                if ((unit == PF_U_CMP || (unit == PF_U_BOOL && pop != PF_ASSERT && pop != PF_B_SPILL)) &&
-                    !(P[0] & PF_I_ASSERT) && (P[1] & 0xffu) == ((I[1] >> 8) & 0xffu)) {
-                    P[0] |= PF_I_ASSERT;
-                    continue;
+                // the last writer of the asserted B register (round 4: not only the
+                // instruction right before — the conjunction's value does not depend on where
+                // the and happens, and an earlier short-circuit only exits sooner)
+                const uint32_t r = (I[1] >> 8) & 0xffu;
+                for (size_t k = code_out.size() / 4; k-- > first;) {
+                    uint32_t* P = code_out.data() + 4 * k;
+                    const uint32_t pop = P[0] & 0xffu, unit = pf_op_unit(pop);
+                    if (!PF_OP_WRITES_B(pop) || (P[1] & 0xffu) != r) continue;
+                    if ((unit == PF_U_CMP || unit == PF_U_BOOL) && !(P[0] & PF_I_ASSERT)) {
+                        P[0] |= PF_I_ASSERT;
+                        I = nullptr;
+                    }
+                    break;
                 }
+                if (!I) continue;
             }
             code_out.insert(code_out.end(), I, I + 4);
         }

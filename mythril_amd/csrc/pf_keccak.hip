@@ -85,6 +85,19 @@ __device__ __forceinline__ void keccak_round(Lane a[25], uint32_t rc_lo, uint32_
     }
 #pragma unroll
     for (int x = 0; x < 5; x++) R[x] = rotl<1>(C[(x + 1) % 5]);
+#ifdef PF_KECCAK_THETA2
+    // D[x] = C[x-1] ^ rot1(C[x+1]) once per column, then two-source xors into the 25 lanes:
+    // 10 + 50 two-source ops instead of 50 three-source ones
+#pragma unroll
+    for (int x = 0; x < 5; x++) {
+        const uint32_t dlo = C[(x + 4) % 5].lo ^ R[x].lo, dhi = C[(x + 4) % 5].hi ^ R[x].hi;
+#pragma unroll
+        for (int y = 0; y < 25; y += 5) {
+            a[x + y].lo ^= dlo;
+            a[x + y].hi ^= dhi;
+        }
+    }
+#else
 #pragma unroll
     for (int x = 0; x < 5; x++)
 #pragma unroll
@@ -92,6 +105,7 @@ __device__ __forceinline__ void keccak_round(Lane a[25], uint32_t rc_lo, uint32_
             a[x + y].lo = xor3(a[x + y].lo, C[(x + 4) % 5].lo, R[x].lo);
             a[x + y].hi = xor3(a[x + y].hi, C[(x + 4) % 5].hi, R[x].hi);
         }
+#endif
     // rho + pi
     Lane t = a[1];
     rho_pi_step<0>(a, t);
