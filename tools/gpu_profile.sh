@@ -18,3 +18,8 @@ timeout -k 10 400 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_ACTIVE_INST_
 timeout -k 10 400 rocprofv3 --pmc SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_CVT --output-format csv -d $OUT/f64 -o run -- $P > $OUT/f64.log 2>&1 || { echo "f64 failed"; exit 1; }
 echo PROFILE-DONE
 tail -1 $OUT/trace.log | cut -c1-300
+# optional: WRITE_SIZE with another lowering spill policy (SPILLPOL=N -> PF_VAR_SPILL_USES=N)
+if [ -n "$SPILLPOL" ]; then
+  PF_VAR_SPILL_USES=$SPILLPOL timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write_sp$SPILLPOL -o run -- $P > $OUT/write_sp$SPILLPOL.log 2>&1 || { echo "write_sp failed"; exit 1; }
+  echo SPILLPOL-DONE
+fi

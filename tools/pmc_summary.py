@@ -50,7 +50,10 @@ def main():
     keys = ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_VALU_INT32", "SQ_INSTS_VALU_INT64", "SQ_INSTS_SALU",
             "SQ_INSTS_SMEM", "SQ_INSTS_BRANCH", "SQ_WAVE_CYCLES"]
     sqm = {k: mean(sq, k) for k in keys}
-    out = {"kernel": KERNEL, "dispatches": len(fetch), "fetch_bytes": fetch_b, "write_bytes": write_b,
+    import subprocess
+    head = subprocess.run(["git", "-C", root, "rev-parse", "--short", "HEAD"], capture_output=True,
+                          text=True).stdout.strip()
+    out = {"kernel": KERNEL, "head": head, "dispatches": len(fetch), "fetch_bytes": fetch_b, "write_bytes": write_b,
            "traffic_bytes": fetch_b + write_b, "sq": sqm,
            "workload": "bench.py default (1024 config-3 DAGs x 65536 candidates, full sweep)"}
     clk = per_dispatch(csvp("clk"))
