@@ -113,11 +113,16 @@ namespace {
     case R:                                                                               \
         _Pragma("unroll") for (int k_ = 0; k_ < 8; k_++)(W)[R][k_] = (src).l[k_];          \
         break;
-// An LDS operand read is waited for where it is issued, before the next instruction's
-// scalar fetch goes out (run_program): LDS reads and scalar loads share lgkmcnt and scalar
-// loads return out of order, so a wait at the join of the operand switch — where the compiler
-// put one for every later use of the operand, whichever register it came from — also waited
-// for the fetch in flight, exposing its latency on every instruction.
+// Where the next instruction's fetch is issued.  Default: right after this instruction's
+// decode, before its operand reads.  PF_FETCH_LATE issues it after the operand reads, with an
+// explicit lgkmcnt(0) after each LDS operand read: LDS reads and scalar loads share lgkmcnt
+// and scalar loads return out of order, so with the early fetch the compiler's wait at the
+// join of the operand switch also waits for the fetch in flight.  Measured on config 3
+// (round 4, two A/B pairs on one box): the late fetch is 1.9 % SLOWER (14.54 vs 14.26 ms) —
+// the fetch latency the early issue exposes at that join is smaller than what it hides.
+#ifndef PF_FETCH_LATE
+#define PF_FETCH_EARLY
+#endif
 #ifndef PF_FETCH_EARLY
 #define PF_WAIT_LDS() __builtin_amdgcn_s_waitcnt(0xC07F)  // lgkmcnt(0)
 #else
@@ -623,7 +628,7 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
             if (__builtin_expect((tr & PF_TR_RB) != 0u, 1)) RD_W(y, W, b, LPB);
         }
         // constant operands (pf_batch_create's peephole deleted their W_CONST): one scalar
-        // load of const[a] / const[b] each, waited for here, before the next fetch goes out
+        // load of const[a] / const[b] each
         if (__builtin_expect((I.x & (PF_I_KA | PF_I_KB)) != 0u, 0)) {
             if (I.x & PF_I_KA) {
                 const uint32_t* cp = S.consts + (size_t)a * 8u;
@@ -635,7 +640,6 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
 #pragma unroll
                 for (int i = 0; i < 8; i++) y.l[i] = cp[i];
             }
-            PF_WAIT_LDS();
         }
 #ifndef PF_FETCH_EARLY
         __builtin_amdgcn_sched_barrier(0);
