@@ -548,7 +548,13 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
     uint32_t Bk = 0u;
     // spill slots (lowering under register pressure): dynamically indexed, so the compiler
     // keeps them in private scratch memory, never in the VGPR banks
-    uint32_t spill[PF_MAX_SPILL * 8];
+#ifndef PF_SPILL_PAD
+#define PF_SPILL_PAD 0  // extra private dwords per lane (a probe of the scratch stride's L2 fit)
+#endif
+    uint32_t spill[PF_MAX_SPILL * 8 + PF_SPILL_PAD];
+#if PF_SPILL_PAD
+    if (__builtin_expect(cand == 0xFFFFFFFFu, 0)) spill[PF_MAX_SPILL * 8 + PF_SPILL_PAD - 1] = 0u;  // keep the pad
+#endif
 #define BGET(r) ((Bk >> ((r) & 31u)) & 1u)
 #define BSET(r, v) (Bk = (Bk & ~(1u << ((r) & 31u))) | (((v) & 1u) << ((r) & 31u)))
     // Ops with a B result (compares, bool logic, B_VAR, UMUL_NOOVF) set their bit and skip
