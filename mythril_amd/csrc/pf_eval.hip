@@ -548,8 +548,23 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
     uint32_t Bk = 0u;
     // spill slots (lowering under register pressure): dynamically indexed, so the compiler
     // keeps them in private scratch memory, never in the VGPR banks
+    // physical spill slot of bytecode slot k (PF_SPILL_ROT: rotated by the wave's hardware
+    // slot, a probe of how the scratch lines of the 4096 waves share the L2)
+#ifdef PF_SPILL_ROT
+    const uint32_t spill_rot = __builtin_amdgcn_readfirstlane(blockIdx.x);
+#define PF_SLOT(k) (((k) + spill_rot) & (PF_MAX_SPILL - 1u))
+#else
+#define PF_SLOT(k) ((k) & (PF_MAX_SPILL - 1u))
+#endif
+// Extra private dwords per lane.  The spill slots live in each wave's scratch window, and
+// with 2,064 B per lane the windows are 0x20400 bytes apart, so the slot-0 lines of the 4,096
+// resident waves collided in the L2 and were evicted to memory: WRITE_SIZE 115 MB per
+// config-3 launch, of which 11 MB without any spill (PF_VAR_SPILL_USES=99).  A 256-byte pad
+// per lane (window 0x24400) halves it, 53 MB, at the same speed (profiles/r04e_*, r04f_*:
+// pads of 32 B .. 1 KB and a per-wave slot rotation all land at 53–64 MB); the rest is the
+// spill stores themselves (PF_VAR_SPILL_USES=3: 31 MB at -0.4 %, =99: 11 MB at -0.9 %).
 #ifndef PF_SPILL_PAD
-#define PF_SPILL_PAD 0  // extra private dwords per lane (a probe of the scratch stride's L2 fit)
+#define PF_SPILL_PAD 64
 #endif
     uint32_t spill[PF_MAX_SPILL * 8 + PF_SPILL_PAD];
 #if PF_SPILL_PAD
@@ -805,10 +820,10 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
                     case PF_B_NOT: BSET(d, BGET(a) ^ 1u); break;
                     case PF_B_ITE: BSET(d, BGET(c) ? BGET(a) : BGET(b)); break;
                     case PF_B_FILL:
-                        BSET(d, spill[(aux & (PF_MAX_SPILL - 1u)) * 8u]);
+                        BSET(d, spill[PF_SLOT(aux) * 8u]);
                         PF_WAIT_ALL();
                         break;
-                    case PF_B_SPILL: spill[(aux & (PF_MAX_SPILL - 1u)) * 8u] = BGET(a); break;
+                    case PF_B_SPILL: spill[PF_SLOT(aux) * 8u] = BGET(a); break;
                     default:  // PF_ASSERT
                         PF_DO_ASSERT(BGET(a));
                         PF_NEXT();
@@ -841,13 +856,13 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
                     case PF_W_MOV: z = x; break;
                     case PF_W_SPILL:
 #pragma unroll
-                        for (int i = 0; i < 8; i++) spill[(aux & (PF_MAX_SPILL - 1u)) * 8u + i] = x.l[i];
+                        for (int i = 0; i < 8; i++) spill[PF_SLOT(aux) * 8u + i] = x.l[i];
                         if (NREG == 8) PF_NEXT();  // no W result (the wide kernels write the sink)
                         z = x;
                         break;
                     case PF_W_FILL:
 #pragma unroll
-                        for (int i = 0; i < 8; i++) z.l[i] = spill[(aux & (PF_MAX_SPILL - 1u)) * 8u + i];
+                        for (int i = 0; i < 8; i++) z.l[i] = spill[PF_SLOT(aux) * 8u + i];
                         PF_WAIT_ALL();
                         break;
                     case PF_W_NOT: z = pf::not256(x); break;
