@@ -284,168 +284,162 @@ int check_collect(Batch* B, hipStream_t st, pf_stats* stats, std::vector<uint32_
     return 0;
 }
 
-// The device form of a validated batch (traffic / unit bits already set): the peepholes
-// below rewrite the program the kernel runs, never the caller's arrays (the oracles evaluate
-// the program as lowered).  Shared by pf_batch_create and the host-only test export
-// pf_device_program.
+// The device form of a validated batch (traffic / unit bits already set): three
+// semantics-preserving peepholes rewrite the program the kernel runs, never the caller's
+// arrays (the oracles evaluate the program as lowered).  Each set is rewritten in a scratch
+// copy (descriptors may share or reorder code ranges) and appended to code_out; every pass is
+// one forward walk with per-register state.  Shared by pf_batch_create and the host-only test
+// export pf_device_program.
+//  1. ASSERT: folded into the last writer of its B register when that is a compare or bool op
+//     (PF_I_ASSERT) — the conjunction's value does not depend on where the and happens, and
+//     with PF_FLAG_SHORTCIRCUIT an earlier check only exits sooner (round 2 folded it only
+//     into the instruction right before it).
+//  2. W_MOV: a zero-extending move (its source holds a value no wider than the move — values
+//     are kept zero-extended, so the move copies it unchanged) is deleted and the readers of
+//     its destination, up to that register's next write, read the source — provided the
+//     source is not rewritten before the last of them.
+//  3. W_CONST: deleted when its register is read, until its next write, only as the a / b
+//     operand of W-reading instructions (not SPILL or MOV); those take the constant directly
+//     (PF_I_KA / PF_I_KB, the constant index in the register field, traffic bit cleared) and
+//     the kernel reads it with one scalar load.
 void device_program(const std::vector<uint32_t>& code_fixed, std::vector<pf_set_desc>& descs_out,
                     std::vector<uint32_t>& code_out) {
-    // Peephole (semantics-preserving): an ASSERT of the B register that the instruction just
-    // before it wrote — a compare or a bool op, the shape every root takes — becomes the
-    // PF_I_ASSERT flag of that instruction, one dispatched instruction less per asserted
-    // root.  The caller's arrays are unchanged; the device gets the compacted
-    // program with shifted code ranges.
     code_out.clear();
     code_out.reserve(code_fixed.size());
     const size_t n_sets = descs_out.size();
+    std::vector<uint32_t> P;      // the set being rewritten
+    std::vector<uint8_t> drop;
+    struct Pending {              // pass 3: the W_CONST a register holds, and its readers
+        int64_t at = -1;
+        bool ok = true;
+        std::vector<uint32_t> readers;
+    };
+    Pending pend[PF_NW + 1];
     for (size_t s = 0; s < n_sets; s++) {
         pf_set_desc& d = descs_out[s];
-        const uint32_t* src = code_fixed.data() + 4 * (size_t)d.code_off;
-        const size_t first = code_out.size() / 4;
-        for (uint32_t i = 0; i < d.n_ins; i++) {
-            const uint32_t* I = src + 4 * (size_t)i;
-            const uint32_t op = I[0] & 0xffu;
-            if (op == PF_ASSERT && code_out.size() / 4 > first) {
-                // the last writer of the asserted B register (round 4: not only the
-                // instruction right before — the conjunction's value does not depend on where
-                // the and happens, and an earlier short-circuit only exits sooner)
-                const uint32_t r = (I[1] >> 8) & 0xffu;
-                for (size_t k = code_out.size() / 4; k-- > first;) {
-                    uint32_t* P = code_out.data() + 4 * k;
-                    const uint32_t pop = P[0] & 0xffu, unit = pf_op_unit(pop);
-                    if (!PF_OP_WRITES_B(pop) || (P[1] & 0xffu) != r) continue;
-                    if ((unit == PF_U_CMP || unit == PF_U_BOOL) && !(P[0] & PF_I_ASSERT)) {
-                        P[0] |= PF_I_ASSERT;
-                        I = nullptr;
+        const uint32_t n = d.n_ins;
+        P.assign(code_fixed.begin() + 4 * (size_t)d.code_off, code_fixed.begin() + 4 * ((size_t)d.code_off + n));
+        drop.assign(n, 0);
+        auto tr_of = [&](uint32_t i) { return (P[4 * i] >> 18) & 7u; };
+        // ---- 1. ASSERT -> PF_I_ASSERT on the last writer of its register
+        {
+            int64_t last_b[PF_NB];
+            for (int r = 0; r < PF_NB; r++) last_b[r] = -1;
+            for (uint32_t i = 0; i < n; i++) {
+                const uint32_t op = P[4 * i] & 0xffu;
+                if (op == PF_ASSERT) {
+                    const int64_t k = last_b[(P[4 * i + 1] >> 8) & 31u];
+                    if (k >= 0) {
+                        const uint32_t unit = pf_op_unit(P[4 * (size_t)k] & 0xffu);
+                        if ((unit == PF_U_CMP || unit == PF_U_BOOL) && !(P[4 * (size_t)k] & PF_I_ASSERT)) {
+                            P[4 * (size_t)k] |= PF_I_ASSERT;
+                            drop[i] = 1;
+                        }
                     }
-                    break;
+                } else if (PF_OP_WRITES_B(op)) {
+                    last_b[P[4 * i + 1] & 31u] = i;
                 }
-                if (!I) continue;
             }
-            code_out.insert(code_out.end(), I, I + 4);
         }
+#ifndef PF_NO_MOV_FUSE
+        // ---- 2. zero-extending W_MOV -> its readers read the source
+        {
+            uint32_t wwidth[PF_NW + 1];  // width of the value each W register holds now
+            for (int r = 0; r <= PF_NW; r++) wwidth[r] = 0xffffffffu;
+            for (uint32_t i = 0; i < n; i++) {
+                if (drop[i]) continue;
+                const uint32_t op = P[4 * i] & 0xffu, tr = tr_of(i), dst = P[4 * i + 1] & 0xffu;
+                const uint32_t w = (P[4 * i] >> 8) & 0x3ffu;
+                if (op != PF_W_MOV) {
+                    if ((tr & PF_TR_WW) && dst <= PF_NW) wwidth[dst] = w;
+                    continue;
+                }
+                const uint32_t src = (P[4 * i + 1] >> 8) & 0xffu;
+                bool ok = src <= PF_NW && dst <= PF_NW && wwidth[src] <= w;
+                uint32_t last = i;
+                if (ok) {
+                    bool src_dead = false;
+                    for (uint32_t j = i + 1; j < n; j++) {
+                        if (drop[j]) continue;
+                        const uint32_t jtr = tr_of(j), jw1 = P[4 * j + 1];
+                        const bool reads = ((jtr & PF_TR_RA) && ((jw1 >> 8) & 0xffu) == dst) ||
+                                           ((jtr & PF_TR_RB) && ((jw1 >> 16) & 0xffu) == dst);
+                        if (reads) {
+                            if (src_dead) { ok = false; break; }
+                            last = j;
+                        }
+                        if ((jtr & PF_TR_WW) && (jw1 & 0xffu) == dst) break;
+                        if ((jtr & PF_TR_WW) && (jw1 & 0xffu) == src) src_dead = true;
+                        if ((P[4 * j] & 0xffu) == PF_END) break;
+                    }
+                }
+                if (!ok) {
+                    if (dst <= PF_NW) wwidth[dst] = w;
+                    continue;
+                }
+                for (uint32_t t = i + 1; t <= last; t++) {
+                    const uint32_t jtr = tr_of(t);
+                    uint32_t& w1 = P[4 * t + 1];
+                    if ((jtr & PF_TR_RA) && ((w1 >> 8) & 0xffu) == dst) w1 = (w1 & ~0xff00u) | (src << 8);
+                    if ((jtr & PF_TR_RB) && ((w1 >> 16) & 0xffu) == dst) w1 = (w1 & ~0xff0000u) | (src << 16);
+                }
+                drop[i] = 1;  // dst keeps its old value, which nothing reads before its next write
+            }
+        }
+#endif
+#ifndef PF_NO_CONST_FUSE
+        // ---- 3. W_CONST -> constant operands of its readers
+        {
+            auto settle = [&](uint32_t r) {
+                Pending& q = pend[r];
+                if (q.at >= 0 && q.ok && !q.readers.empty()) {
+                    const uint32_t k = P[4 * (size_t)q.at + 2];
+                    for (uint32_t t : q.readers) {
+                        uint32_t& w0 = P[4 * t];
+                        uint32_t& w1 = P[4 * t + 1];
+                        const uint32_t jtr = (w0 >> 18) & 7u;
+                        if ((jtr & PF_TR_RA) && ((w1 >> 8) & 0xffu) == r) {
+                            w0 = (w0 & ~(PF_TR_RA << 18)) | PF_I_KA;
+                            w1 = (w1 & ~0xff00u) | (k << 8);
+                        }
+                        if ((jtr & PF_TR_RB) && ((w1 >> 16) & 0xffu) == r) {
+                            w0 = (w0 & ~(PF_TR_RB << 18)) | PF_I_KB;
+                            w1 = (w1 & ~0xff0000u) | (k << 16);
+                        }
+                    }
+                    drop[q.at] = 1;
+                }
+                q.at = -1;
+                q.ok = true;
+                q.readers.clear();
+            };
+            for (uint32_t i = 0; i < n; i++) {
+                if (drop[i]) continue;
+                const uint32_t op = P[4 * i] & 0xffu, tr = tr_of(i), w1 = P[4 * i + 1];
+                const uint32_t ra = (w1 >> 8) & 0xffu, rb = (w1 >> 16) & 0xffu, rd = w1 & 0xffu;
+                if (op == PF_END) break;
+                // reads first (an instruction may read and rewrite the same register)
+                for (int side = 0; side < 2; side++) {
+                    const uint32_t r = side ? rb : ra;
+                    if (!(tr & (side ? PF_TR_RB : PF_TR_RA)) || r > PF_NW || pend[r].at < 0) continue;
+                    if (side && (tr & PF_TR_RA) && ra == r) continue;  // the same register twice
+                    if (op == PF_W_SPILL || op == PF_W_MOV) pend[r].ok = false;
+                    else pend[r].readers.push_back(i);
+                }
+                if ((tr & PF_TR_WW) && rd <= PF_NW) {
+                    settle(rd);
+                    if (op == PF_W_CONST && P[4 * i + 2] <= 0xffu) pend[rd].at = i;
+                }
+            }
+            for (uint32_t r = 0; r <= PF_NW; r++) settle(r);
+        }
+#endif
+        const size_t first = code_out.size() / 4;
+        for (uint32_t i = 0; i < n; i++)
+            if (!drop[i]) code_out.insert(code_out.end(), P.begin() + 4 * (size_t)i, P.begin() + 4 * (size_t)i + 4);
         d.code_off = (uint32_t)first;
         d.n_ins = (uint32_t)(code_out.size() / 4 - first);
     }
-#ifndef PF_NO_MOV_FUSE
-    // Peephole (semantics-preserving): a W_MOV that zero-extends (the last writer of its
-    // source register wrote a value no wider than the move's width — values are kept
-    // zero-extended, so the move copies it unchanged) is deleted and the readers of its
-    // destination, up to that register's next write, read the source register instead —
-    // provided the source is not rewritten before the last of them.
-    {
-        std::vector<uint32_t> kept;
-        kept.reserve(code_out.size());
-        for (size_t s = 0; s < n_sets; s++) {
-            pf_set_desc& d = descs_out[s];
-            uint32_t* P = code_out.data() + 4 * (size_t)d.code_off;
-            std::vector<uint8_t> drop(d.n_ins, 0);
-            for (uint32_t i = 0; i < d.n_ins; i++) {
-                const uint32_t* I = P + 4 * (size_t)i;
-                if ((I[0] & 0xffu) != PF_W_MOV) continue;
-                const uint32_t dst = I[1] & 0xffu, src = (I[1] >> 8) & 0xffu, w = (I[0] >> 8) & 0x3ffu;
-                // the width of the value in src: its last writer before i
-                uint32_t ww = 0xffffffffu;
-                for (uint32_t k = i; k-- > 0;) {
-                    const uint32_t* K = P + 4 * (size_t)k;
-                    if (drop[k]) continue;
-                    if ((((K[0] >> 18) & 7u) & PF_TR_WW) && (K[1] & 0xffu) == src) {
-                        ww = (K[0] >> 8) & 0x3ffu;
-                        break;
-                    }
-                }
-                if (ww > w) continue;  // a truncation (or no writer): keep the move
-                // readers of dst up to its next write; src must stay unwritten until the last
-                bool ok = true, src_dead = false;
-                uint32_t j = i + 1, last = i;
-                for (; j < d.n_ins; j++) {
-                    const uint32_t* J = P + 4 * (size_t)j;
-                    const uint32_t jtr = (J[0] >> 18) & 7u;
-                    const bool reads = ((jtr & PF_TR_RA) && ((J[1] >> 8) & 0xffu) == dst) ||
-                                       ((jtr & PF_TR_RB) && ((J[1] >> 16) & 0xffu) == dst);
-                    if (reads) {
-                        if (src_dead) { ok = false; break; }
-                        last = j;
-                    }
-                    if ((jtr & PF_TR_WW) && (J[1] & 0xffu) == dst) break;
-                    if ((jtr & PF_TR_WW) && (J[1] & 0xffu) == src) src_dead = true;
-                    if ((J[0] & 0xffu) == PF_END) break;
-                }
-                if (!ok) continue;
-                for (uint32_t t = i + 1; t <= last; t++) {
-                    uint32_t* J = P + 4 * (size_t)t;
-                    const uint32_t jtr = (J[0] >> 18) & 7u;
-                    if ((jtr & PF_TR_RA) && ((J[1] >> 8) & 0xffu) == dst) J[1] = (J[1] & ~0xff00u) | (src << 8);
-                    if ((jtr & PF_TR_RB) && ((J[1] >> 16) & 0xffu) == dst) J[1] = (J[1] & ~0xff0000u) | (src << 16);
-                }
-                drop[i] = 1;
-            }
-            const size_t first = kept.size() / 4;
-            for (uint32_t i = 0; i < d.n_ins; i++)
-                if (!drop[i]) kept.insert(kept.end(), P + 4 * (size_t)i, P + 4 * (size_t)i + 4);
-            d.code_off = (uint32_t)first;
-            d.n_ins = (uint32_t)(kept.size() / 4 - first);
-        }
-        code_out.swap(kept);
-    }
-#endif
-#ifndef PF_NO_CONST_FUSE
-    // Peephole (semantics-preserving): a W_CONST whose register is read, until its next
-    // write, only as the a / b operand of W-reading instructions is deleted and those readers
-    // take the constant directly (PF_I_KA / PF_I_KB with the constant index in the register
-    // field, traffic bit cleared).  Config 3: ~7 of ~60 instructions per set are W_CONST.
-    {
-        std::vector<uint32_t> fused;
-        fused.reserve(code_out.size());
-        for (size_t s = 0; s < n_sets; s++) {
-            pf_set_desc& d = descs_out[s];
-            uint32_t* P = code_out.data() + 4 * (size_t)d.code_off;
-            std::vector<uint8_t> drop(d.n_ins, 0);
-            for (uint32_t i = 0; i < d.n_ins; i++) {
-                const uint32_t* I = P + 4 * (size_t)i;
-                if ((I[0] & 0xffu) != PF_W_CONST || I[2] > 0xffu) continue;
-                const uint32_t r = I[1] & 0xffu, k = I[2];
-                // the readers up to the next write of r: all must take the constant
-                bool ok = true;
-                uint32_t j = i + 1, n_read = 0;
-                for (; j < d.n_ins; j++) {
-                    const uint32_t* J = P + 4 * (size_t)j;
-                    const uint32_t jop = J[0] & 0xffu, jtr = (J[0] >> 18) & 7u;
-                    const uint32_t ja = (J[1] >> 8) & 0xffu, jb = (J[1] >> 16) & 0xffu;
-                    const bool ra = (jtr & PF_TR_RA) && ja == r, rb = (jtr & PF_TR_RB) && jb == r;
-                    if (ra || rb) {
-                        n_read++;
-                        if (jop == PF_W_SPILL || jop == PF_W_MOV) { ok = false; break; }
-                    }
-                    if ((jtr & PF_TR_WW) && (J[1] & 0xffu) == r) break;  // r rewritten (after the read)
-                    if (jop == PF_END) break;
-                }
-                if (!ok || n_read == 0) continue;
-                for (uint32_t t = i + 1; t < j || (t == j && t < d.n_ins); t++) {
-                    uint32_t* J = P + 4 * (size_t)t;
-                    const uint32_t jtr = (J[0] >> 18) & 7u;
-                    const uint32_t ja = (J[1] >> 8) & 0xffu, jb = (J[1] >> 16) & 0xffu;
-                    if ((jtr & PF_TR_RA) && ja == r) {
-                        J[0] = (J[0] & ~(PF_TR_RA << 18)) | PF_I_KA;
-                        J[1] = (J[1] & ~0xff00u) | (k << 8);
-                    }
-                    if ((jtr & PF_TR_RB) && jb == r) {
-                        J[0] = (J[0] & ~(PF_TR_RB << 18)) | PF_I_KB;
-                        J[1] = (J[1] & ~0xff0000u) | (k << 16);
-                    }
-                    if (t == j) break;
-                }
-                drop[i] = 1;
-            }
-            const size_t first = fused.size() / 4;
-            for (uint32_t i = 0; i < d.n_ins; i++)
-                if (!drop[i]) fused.insert(fused.end(), P + 4 * (size_t)i, P + 4 * (size_t)i + 4);
-            d.code_off = (uint32_t)first;
-            d.n_ins = (uint32_t)(fused.size() / 4 - first);
-        }
-        code_out.swap(fused);
-    }
-#endif
 }
 
 }  // namespace
