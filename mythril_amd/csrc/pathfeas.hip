@@ -51,6 +51,13 @@ int g_default = -1;       // index in g_devs of the default device (lowest id)
 uint32_t g_waves_per_cu_full = 512;
 uint32_t g_waves_per_cu_early = 16;
 uint32_t g_early_chunk_groups = 8;
+// Early-exit searches of at most this many sets start with a probe launch: one wave per set
+// evaluates only candidates 0..63 (candidate 0 is the parent / hint model, which answers most
+// funnel queries), then the full queue search runs behind it on the stream and skips every set
+// the probe decided.  Without the probe a single query's chip-filling grid put ~4,000 waves on
+// the chunks of one set at once, so the witness group ran at a loaded chip's per-wave speed
+// instead of a lone wave's (PF_PROBE_MAX_SETS, 0 = off).
+uint32_t g_probe_max_sets = 4096;
 
 int fail(const char* fmt, ...) {
     char buf[512];
@@ -231,13 +238,23 @@ int check_enqueue(Batch* B, uint64_t gseed, uint32_t budget, uint32_t flags, uin
     HIPCHK(hipEventRecord(B->ev0, st));
     const uint64_t deadline = timeout_ms ? (uint64_t)timeout_ms * 100000ull : 0ull;  // 100 MHz
     const bool early = flags & PF_FLAG_EARLY_EXIT;
+    // phase 0: the probe (early exit, small batches: candidates 0..63 of every set, one wave
+    // per set); phase 1: the search over the whole budget, whose waves skip decided sets
+    const bool probe = early && budget > 64u && B->n_sets <= g_probe_max_sets;
+    for (int phase = probe ? 0 : 1; phase < 2; ++phase) {
+    const uint32_t pbudget = phase == 0 ? 64u : budget;
+    if (phase == 1 && probe)  // fresh queue heads for the second launch (stream-ordered)
+        HIPCHK(hipMemsetAsync(B->d_scratch + PF_EARLY_QUEUE_OFF / 4, 0,
+                              2 * PF_EARLY_QUEUES * PF_EARLY_QUEUE_STRIDE * 4, st));
     // the 8-register sets first, then the 16-register ones (usually none)
     for (int part = 0; part < 2; ++part) {
         const size_t first = part ? B->n_narrow : 0;
         const size_t n = part ? B->n_sets - B->n_narrow : B->n_narrow;
         if (n == 0 || budget == 0) continue;
         uint32_t per_wave, slices;
-        geometry(D->num_cus, (uint32_t)n, budget, flags, &per_wave, &slices);
+        // phase 1 after a probe: candidates 64.. only (the probe evaluated 0..63)
+        const uint32_t cbegin = (phase == 1 && probe) ? 64u : 0u;
+        geometry(D->num_cus, (uint32_t)n, pbudget - cbegin, flags, &per_wave, &slices);
         const uint64_t items = (uint64_t)n * slices;
         if (items > 0xffffffffull) return fail("batch too large: %llu waves", (unsigned long long)items);
         // early exit: a chip-filling grid of persistent waves takes the items from the queue
@@ -252,9 +269,10 @@ int check_enqueue(Batch* B, uint64_t gseed, uint32_t budget, uint32_t flags, uin
                                      : (early ? pf_check_early_r16_kernel : pf_check_r16_kernel),
                            dim3(blocks), dim3(64 * PF_SEARCH_WG_WAVES), 0, st, B->d_descs, B->d_order + first,
                            (uint32_t)n, B->d_code, B->d_consts, B->d_schema, B->d_parents,
-                           gseed, budget, per_wave, slices, flags, deadline, d_t0, d_found, d_counters,
-                           d_queue);
+                           gseed, pbudget, per_wave, slices, flags, deadline, d_t0, d_found, d_counters,
+                           d_queue, cbegin);
         HIPCHK(hipGetLastError());
+    }
     }
     HIPCHK(hipEventRecord(B->ev1, st));
     return 0;
@@ -507,6 +525,10 @@ int pf_init(uint64_t device_mask) {
     if (const char* e = getenv("PF_WAVES_PER_CU_EARLY")) {  // the early-exit search alone
         long v = strtol(e, nullptr, 10);
         if (v >= 1 && v <= 4096) g_waves_per_cu_early = (uint32_t)v;
+    }
+    if (const char* e = getenv("PF_PROBE_MAX_SETS")) {
+        long v = strtol(e, nullptr, 10);
+        if (v >= 0) g_probe_max_sets = (uint32_t)v;
     }
     if (const char* e = getenv("PF_EARLY_CHUNK_GROUPS")) {
         long v = strtol(e, nullptr, 10);

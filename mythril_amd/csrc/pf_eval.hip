@@ -1001,7 +1001,7 @@ PF_INL void check_body(const pf_set_desc* __restrict__ descs, const uint32_t* __
                        uint64_t gseed, uint32_t budget, uint32_t per_wave, uint32_t slices,
                        uint32_t flags, uint64_t deadline_ticks, uint64_t* __restrict__ t0_slot,
                        uint32_t* __restrict__ found, unsigned long long* __restrict__ counters,
-                       uint32_t* __restrict__ queue) {
+                       uint32_t* __restrict__ queue, uint32_t cand_begin) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
     const uint32_t n_items = n_sets * slices;
@@ -1042,7 +1042,7 @@ PF_INL void check_body(const pf_set_desc* __restrict__ descs, const uint32_t* __
         const uint32_t set = __builtin_amdgcn_readfirstlane(order[wave / slices]);
         const uint32_t slice = wave % slices;
         search_item<EARLY, NREG>(make_ctx(descs, set, code, consts, schema, parents, gseed), set,
-                                 slice * per_wave, min(budget, slice * per_wave + per_wave), flags,
+                                 cand_begin + slice * per_wave, min(budget, cand_begin + slice * per_wave + per_wave), flags,
                                  deadline_ticks, t0, found, exp_tbl, evals_full, decided, ops, cut, prof);
     } else {
         // PF_EARLY_QUEUES heads, 128 B apart: queue q hands out items q, q + Q, q + 2Q, ...
@@ -1063,7 +1063,7 @@ PF_INL void check_body(const pf_set_desc* __restrict__ descs, const uint32_t* __
                 const uint32_t set = __builtin_amdgcn_readfirstlane(order[EARLY ? item % n_sets : item / slices]);
                 const uint32_t slice = EARLY ? item / n_sets : item % slices;
                 search_item<EARLY, NREG>(make_ctx(descs, set, code, consts, schema, parents, gseed), set,
-                                         slice * per_wave, min(budget, slice * per_wave + per_wave), flags,
+                                         cand_begin + slice * per_wave, min(budget, cand_begin + slice * per_wave + per_wave), flags,
                                          deadline_ticks, t0, found, exp_tbl, evals_full, decided, ops, cut, prof);
                 if (cut) break;
             }
@@ -1091,10 +1091,10 @@ PF_INL void check_body(const pf_set_desc* __restrict__ descs, const uint32_t* __
         const uint4 *__restrict__ schema, const uint32_t *__restrict__ parents, uint64_t gseed, \
         uint32_t budget, uint32_t per_wave, uint32_t slices, uint32_t flags,                   \
         uint64_t deadline_ticks, uint64_t *__restrict__ t0_slot, uint32_t *__restrict__ found, \
-        unsigned long long *__restrict__ counters, uint32_t *__restrict__ queue
+        unsigned long long *__restrict__ counters, uint32_t *__restrict__ queue, uint32_t cand_begin
 #define PF_CHECK_ARGS                                                                         \
     descs, order, n_sets, code, consts, schema, parents, gseed, budget, per_wave, slices, flags, \
-        deadline_ticks, t0_slot, found, counters, queue
+        deadline_ticks, t0_slot, found, counters, queue, cand_begin
 
 // The search kernels exist twice: over 8 registers at 3 waves per SIMD (programs whose
 // lowering fits PF_NW_NARROW registers — the host picks per batch, pathfeas.hip) and over 16
