@@ -51,13 +51,14 @@ int g_default = -1;       // index in g_devs of the default device (lowest id)
 uint32_t g_waves_per_cu_full = 512;
 uint32_t g_waves_per_cu_early = 16;
 uint32_t g_early_chunk_groups = 8;
-// Early-exit searches of at most this many sets start with a probe launch: one wave per set
-// evaluates only candidates 0..63 (candidate 0 is the parent / hint model, which answers most
-// funnel queries), then the full queue search runs behind it on the stream and skips every set
-// the probe decided.  Without the probe a single query's chip-filling grid put ~4,000 waves on
-// the chunks of one set at once, so the witness group ran at a loaded chip's per-wave speed
-// instead of a lone wave's (PF_PROBE_MAX_SETS, 0 = off).
-uint32_t g_probe_max_sets = 4096;
+// Early-exit searches of at most this many sets may start with a probe launch: one wave per
+// set evaluates only candidates 0..63 (candidate 0 is the parent / hint model, which answers
+// most funnel queries), then the queue search runs behind it on the stream from candidate 64
+// and skips every set the probe decided.  Measured (round 4, profiles/r04h_bench.jsonl against
+// r04g): single funnel query median 0.686 -> 0.770 ms, search phase 0.28 -> 0.34 ms, planted
+// 1024-set batch 0.372 -> 0.398 ms — the second launch costs more than the chip-filling grid's
+// contention it avoids, so it is off by default (PF_PROBE_MAX_SETS > 0 turns it on).
+uint32_t g_probe_max_sets = 0;
 
 int fail(const char* fmt, ...) {
     char buf[512];
