@@ -94,7 +94,7 @@ struct Batch {
     uint32_t* d_parents = nullptr;
     uint32_t* d_found = nullptr;
     uint32_t* d_order = nullptr;    // set ids, most expensive first (search-kernel wave order)
-    uint32_t* d_scratch = nullptr;  // this batch's launch counters (u64 [0..3]) and t0 (u64 [4])
+    uint32_t* d_scratch = nullptr;  // this batch's t0 (u64 [4]), queue heads and counter lines (pf_bytecode.h)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     ~Batch() {  // the device block goes back to its device's pool first (release_batch)
         if (d_mem) hipFree(d_mem);
@@ -228,13 +228,9 @@ int check_enqueue(Batch* B, uint64_t gseed, uint32_t budget, uint32_t flags, uin
 #ifndef PF_FULL_QUEUE
 #define PF_FULL_QUEUE 1
 #endif
-    // counters (and the profiling slots) at the front, the work-queue heads of both launch
-    // parts from PF_EARLY_QUEUE_OFF: one fill for both when the queues are used
-    if ((flags & PF_FLAG_EARLY_EXIT) || PF_FULL_QUEUE)
-        HIPCHK(hipMemsetAsync(B->d_scratch, 0, PF_EARLY_QUEUE_OFF + 2 * PF_EARLY_QUEUES * PF_EARLY_QUEUE_STRIDE * 4,
-                              st));
-    else
-        HIPCHK(hipMemsetAsync(B->d_scratch, 0, PF_EARLY_QUEUE_OFF, st));
+    // t0 and the profiling slots at the front, the work-queue heads of both launch parts from
+    // PF_EARLY_QUEUE_OFF, the counter lines from PF_COUNTER_OFF: one fill for all
+    HIPCHK(hipMemsetAsync(B->d_scratch, 0, PF_SCRATCH_BYTES, st));
     HIPCHK(hipMemsetAsync(d_found, 0xff, std::max<size_t>(B->n_sets, 1) * sizeof(uint32_t), st));
     HIPCHK(hipEventRecord(B->ev0, st));
     const uint64_t deadline = timeout_ms ? (uint64_t)timeout_ms * 100000ull : 0ull;  // 100 MHz
@@ -283,13 +279,16 @@ int check_enqueue(Batch* B, uint64_t gseed, uint32_t budget, uint32_t flags, uin
 // counters and kernel time of the last launch; with `found`, the verdicts too, copied before
 // the one stream synchronisation (a second round trip was ~4 % of a single query's search)
 int check_collect(Batch* B, hipStream_t st, pf_stats* stats, std::vector<uint32_t>* found = nullptr) {
-    unsigned long long h[4];
-    HIPCHK(hipMemcpyAsync(h, B->d_scratch, sizeof(h), hipMemcpyDeviceToHost, st));
+    unsigned long long hs[PF_COUNTER_STRIPES * 16];
+    HIPCHK(hipMemcpyAsync(hs, B->d_scratch + PF_COUNTER_OFF / 4, sizeof(hs), hipMemcpyDeviceToHost, st));
     if (found) {
         found->assign(std::max<size_t>(B->n_sets, 1), 0u);
         HIPCHK(hipMemcpyAsync(found->data(), B->d_found, found->size() * 4, hipMemcpyDeviceToHost, st));
     }
     HIPCHK(hipStreamSynchronize(st));
+    unsigned long long h[4] = {0, 0, 0, 0};
+    for (int i = 0; i < PF_COUNTER_STRIPES; i++)
+        for (int k = 0; k < 4; k++) h[k] += hs[i * 16 + k];
     float ms = 0.f;
     HIPCHK(hipEventElapsedTime(&ms, B->ev0, B->ev1));
     if (stats) {
@@ -690,7 +689,7 @@ int pf_batch_create_on(int device, const uint32_t* code, size_t n_ins, const uin
                  o_par = o_schema + al(n_vars * 16), o_desc = o_par + al(n_parents * 32),
                  o_order = o_desc + al(n_sets * sizeof(pf_set_desc)), o_found = o_order + al(n_sets * 4),
                  o_scr = o_found + al(std::max<size_t>(n_sets, 1) * 4),
-                 total = o_scr + PF_EARLY_QUEUE_OFF + 2 * PF_EARLY_QUEUES * PF_EARLY_QUEUE_STRIDE * 4;
+                 total = o_scr + PF_SCRATCH_BYTES;
     std::vector<uint8_t> stage(o_found, 0);  // found / scratch are cleared by every search
     auto put = [&](size_t off, const void* src, size_t bytes) {
         if (bytes && src) memcpy(stage.data() + off, src, bytes);

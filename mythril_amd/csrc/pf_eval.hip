@@ -962,8 +962,16 @@ PF_INL void search_item(const SetCtx& S, uint32_t set, uint32_t begin, uint32_t 
         const bool active = cand < end;
         uint32_t complete = 0;
         uint64_t lane_ops = 0;
+#ifdef PF_PRIO_FIRST
+        // the group holding candidate 0 (the parent / hint model: the witness of most live
+        // queries) is issued ahead of the other waves on its SIMD
+        if (EARLY && base == 0u) __builtin_amdgcn_s_setprio(3);
+#endif
         uint32_t sat = run_program<MODE_GEN, NREG>(S, cand, active, flags, nullptr, 0u, exp_tbl, &complete,
                                              &lane_ops, &prof);
+#ifdef PF_PRIO_FIRST
+        if (EARLY && base == 0u) __builtin_amdgcn_s_setprio(0);
+#endif
         const uint64_t m_act = __ballot(active);
         const uint64_t m_sat = __ballot((uint32_t)active & sat);
         const uint64_t m_full = __ballot((uint32_t)active & complete);
@@ -1053,6 +1061,18 @@ PF_INL void check_body(const pf_set_desc* __restrict__ descs, const uint32_t* __
         for (uint32_t qi = 0; qi < PF_EARLY_QUEUES; ++qi) {
             const uint32_t q = (wave + qi) % PF_EARLY_QUEUES;
             const uint32_t nq = n_items > q ? (n_items - q + PF_EARLY_QUEUES - 1u) / PF_EARLY_QUEUES : 0u;
+#ifndef PF_QUEUE_NO_PEEK
+            // another wave's queue is read before it is claimed from: once the items run out,
+            // every wave passes every queue on its way out, and as atomics those probes
+            // serialise on the 16 heads (~14 ns each: ~60 us for a 4,096-wave grid, the
+            // larger part of a small batch's search); a plain load of a drained head does not
+            if (qi > 0u) {
+                uint32_t h = 0u;
+                if (lane == 0u) h = __hip_atomic_load(queue + q * PF_EARLY_QUEUE_STRIDE, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+                if (__builtin_amdgcn_readfirstlane(h) >= nq) continue;
+            }
+#endif
             for (;;) {
                 uint32_t v = 0u;
                 if (lane == 0u) v = atomicAdd(queue + q * PF_EARLY_QUEUE_STRIDE, 1u);
@@ -1071,10 +1091,11 @@ PF_INL void check_body(const pf_set_desc* __restrict__ descs, const uint32_t* __
         }
     }
     if (lane == 0) {
-        atomicAdd(counters + 0, (unsigned long long)evals_full);
-        atomicAdd(counters + 1, (unsigned long long)decided);
-        if (flags & PF_FLAG_COUNT_OPS) atomicAdd(counters + 2, (unsigned long long)ops);
-        if (cut) atomicAdd(counters + 3, 1ull);
+        unsigned long long* cs = counters + PF_COUNTER_OFF / 8 + (wave % PF_COUNTER_STRIPES) * 16u;
+        if (evals_full) atomicAdd(cs + 0, (unsigned long long)evals_full);
+        if (decided) atomicAdd(cs + 1, (unsigned long long)decided);
+        if ((flags & PF_FLAG_COUNT_OPS) && ops) atomicAdd(cs + 2, (unsigned long long)ops);
+        if (cut) atomicAdd(cs + 3, 1ull);
 #ifdef PF_PROFILE_UNITS
 #pragma unroll
         for (int i = 0; i < PF_PROF_BUCKETS; i++)
