@@ -230,8 +230,12 @@ int check_enqueue(Batch* B, uint64_t gseed, uint32_t budget, uint32_t flags, uin
 #endif
     // t0 and the profiling slots at the front, the work-queue heads of both launch parts from
     // PF_EARLY_QUEUE_OFF, the counter lines from PF_COUNTER_OFF: one fill for all
-    HIPCHK(hipMemsetAsync(B->d_scratch, 0, PF_SCRATCH_BYTES, st));
-    HIPCHK(hipMemsetAsync(d_found, 0xff, std::max<size_t>(B->n_sets, 1) * sizeof(uint32_t), st));
+    {
+        const uint32_t nz = PF_SCRATCH_BYTES / 4, nf = (uint32_t)std::max<size_t>(B->n_sets, 1);
+        const uint32_t blocks = std::min<uint32_t>((nz + nf + 255u) / 256u, 1024u);
+        hipLaunchKernelGGL(pf_reset_kernel, dim3(blocks), dim3(256), 0, st, B->d_scratch, nz, d_found, nf);
+        HIPCHK(hipGetLastError());
+    }
     HIPCHK(hipEventRecord(B->ev0, st));
     const uint64_t deadline = timeout_ms ? (uint64_t)timeout_ms * 100000ull : 0ull;  // 100 MHz
     const bool early = flags & PF_FLAG_EARLY_EXIT;
@@ -275,17 +279,49 @@ int check_enqueue(Batch* B, uint64_t gseed, uint32_t budget, uint32_t flags, uin
     return 0;
 }
 
+// Pinned host staging for the counter lines and verdicts a search reads back: a copy into
+// pageable memory is staged and synchronous in the runtime (two of them were ~25 us of a
+// single-query search's ~45 us outside the kernel); per host thread, grown on demand, never
+// shrunk, and kept to process exit.  nullptr (pageable fallback) if the allocation fails.
+uint8_t* pinned_staging(size_t bytes) {
+    struct Pin {
+        uint8_t* p = nullptr;
+        size_t cap = 0;
+    };
+    thread_local Pin t;
+    if (bytes > t.cap) {
+        if (t.p) (void)hipHostFree(t.p);
+        t.p = nullptr;
+        t.cap = 0;
+        const size_t cap = std::max<size_t>((bytes + 65535) & ~size_t(65535), 65536);
+        void* p = nullptr;
+        if (hipHostMalloc(&p, cap, hipHostMallocPortable) != hipSuccess) return nullptr;
+        t.p = static_cast<uint8_t*>(p);
+        t.cap = cap;
+    }
+    return t.p;
+}
+
 // Wait for B's last search on stream st and read its counters.
 // counters and kernel time of the last launch; with `found`, the verdicts too, copied before
 // the one stream synchronisation (a second round trip was ~4 % of a single query's search)
 int check_collect(Batch* B, hipStream_t st, pf_stats* stats, std::vector<uint32_t>* found = nullptr) {
+    constexpr size_t cbytes = PF_COUNTER_STRIPES * 128;
+    const size_t nf = std::max<size_t>(B->n_sets, 1);
     unsigned long long hs[PF_COUNTER_STRIPES * 16];
-    HIPCHK(hipMemcpyAsync(hs, B->d_scratch + PF_COUNTER_OFF / 4, sizeof(hs), hipMemcpyDeviceToHost, st));
+    uint8_t* pin = pinned_staging(cbytes + (found ? nf * 4 : 0));
+    HIPCHK(hipMemcpyAsync(pin ? static_cast<void*>(pin) : static_cast<void*>(hs), B->d_scratch + PF_COUNTER_OFF / 4,
+                          cbytes, hipMemcpyDeviceToHost, st));
     if (found) {
-        found->assign(std::max<size_t>(B->n_sets, 1), 0u);
-        HIPCHK(hipMemcpyAsync(found->data(), B->d_found, found->size() * 4, hipMemcpyDeviceToHost, st));
+        found->assign(nf, 0u);
+        HIPCHK(hipMemcpyAsync(pin ? static_cast<void*>(pin + cbytes) : static_cast<void*>(found->data()), B->d_found,
+                              nf * 4, hipMemcpyDeviceToHost, st));
     }
     HIPCHK(hipStreamSynchronize(st));
+    if (pin) {
+        memcpy(hs, pin, cbytes);
+        if (found) memcpy(found->data(), pin + cbytes, nf * 4);
+    }
     unsigned long long h[4] = {0, 0, 0, 0};
     for (int i = 0; i < PF_COUNTER_STRIPES; i++)
         for (int k = 0; k < 4; k++) h[k] += hs[i * 16 + k];

@@ -1122,6 +1122,19 @@ PF_INL void check_body(const pf_set_desc* __restrict__ descs, const uint32_t* __
 // at 2 waves.  Occupancy is the lever: config 3 runs +22 % faster on the 8-register build
 // (DESIGN.md §3), the interpreter's scalar dispatch and memory latency being what a third
 // wave hides.
+// Per-search reset of a batch: the scratch words (t0, queue heads, counter lines) to 0 and
+// the verdicts to "none" (0xFFFFFFFF) — one launch where two runtime fills were two enqueues
+extern "C" __global__ void __launch_bounds__(256) pf_reset_kernel(uint32_t* __restrict__ scratch, uint32_t n_scratch,
+                                                                  uint32_t* __restrict__ found, uint32_t n_found) {
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n_scratch + n_found; i += stride) {
+        if (i < n_scratch)
+            scratch[i] = 0u;
+        else
+            found[i - n_scratch] = 0xFFFFFFFFu;
+    }
+}
+
 extern "C" __global__ void __launch_bounds__(64 * PF_SEARCH_WG_WAVES, PF_WG_PER_CU_NARROW) pf_check_kernel(PF_CHECK_PARAMS) {
     check_body<false, PF_NW_NARROW + 1>(PF_CHECK_ARGS);
 }
