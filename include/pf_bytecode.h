@@ -43,17 +43,18 @@
 #ifndef PF_SEARCH_WG_WAVES
 #define PF_SEARCH_WG_WAVES 1
 #endif
-/* early-exit search work queue: heads per launch part, PF_EARLY_QUEUE_STRIDE u32 (128 B,
- * one L2 line) apart, in the batch scratch from byte PF_EARLY_QUEUE_OFF on */
+/* search work queues: PF_EARLY_QUEUES heads per launch (probe / search phase x narrow / wide
+ * part: 4 launches), PF_EARLY_QUEUE_STRIDE u32 (128 B, one L2 line) apart, in the batch scratch
+ * from byte PF_EARLY_QUEUE_OFF on */
 #define PF_EARLY_QUEUES 16
 #define PF_EARLY_QUEUE_STRIDE 32
 #define PF_EARLY_QUEUE_OFF 512
 /* per-launch counters (evals_full, cands_decided, ops, timed-out items): PF_COUNTER_STRIPES
- * lines of 4 u64, 128 B apart, after both parts' queue heads; a wave adds its non-zero totals
+ * lines of 4 u64, 128 B apart, after the queue heads; a wave adds its non-zero totals
  * into line wave % PF_COUNTER_STRIPES and the host sums the lines (one line took every wave's
  * atomics in series: ~60 us at the end of a 4,096-wave grid) */
 #define PF_COUNTER_STRIPES 16
-#define PF_COUNTER_OFF (PF_EARLY_QUEUE_OFF + 2 * PF_EARLY_QUEUES * PF_EARLY_QUEUE_STRIDE * 4)
+#define PF_COUNTER_OFF (PF_EARLY_QUEUE_OFF + 4 * PF_EARLY_QUEUES * PF_EARLY_QUEUE_STRIDE * 4)
 #define PF_SCRATCH_BYTES (PF_COUNTER_OFF + PF_COUNTER_STRIPES * 128)
 #define PF_NB 32          /* bool registers                                          */
 #define PF_LIMBS 8        /* 8 x 32-bit limbs = 256 bits, little-endian limb order   */

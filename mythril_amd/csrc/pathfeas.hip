@@ -51,14 +51,18 @@ int g_default = -1;       // index in g_devs of the default device (lowest id)
 uint32_t g_waves_per_cu_full = 512;
 uint32_t g_waves_per_cu_early = 16;
 uint32_t g_early_chunk_groups = 8;
-// Early-exit searches of at most this many sets may start with a probe launch: one wave per
-// set evaluates only candidates 0..63 (candidate 0 is the parent / hint model, which answers
-// most funnel queries), then the queue search runs behind it on the stream from candidate 64
-// and skips every set the probe decided.  Measured (round 4, profiles/r04h_bench.jsonl against
-// r04g): single funnel query median 0.686 -> 0.770 ms, search phase 0.28 -> 0.34 ms, planted
-// 1024-set batch 0.372 -> 0.398 ms — the second launch costs more than the chip-filling grid's
-// contention it avoids, so it is off by default (PF_PROBE_MAX_SETS > 0 turns it on).
-uint32_t g_probe_max_sets = 0;
+// Early-exit searches of 2 .. g_probe_max_sets sets that all carry a parent / hint model
+// (candidate 0) start with a probe launch: one wave per set evaluates only candidates 0..63,
+// then the queue search runs behind it on the stream from candidate 64 and skips every set the
+// probe decided.  Without it every wave of the chip-filling grid claims its item before any
+// witness exists, so the grid evaluates one group per wave at 4 waves/SIMD and the candidate-0
+// waves finish at that contention.  Measured (tools/search_overhead_probe.py,
+// profiles/r04o_search_overhead_probe.log, after the striped counters made a grid of skipping
+// waves cheap): 4 planted sets 0.130 -> 0.110 ms, 16: 0.175 -> 0.128 ms; one set 0.064 ->
+// 0.071 ms and sets without a candidate-0 witness (16 unplanted: 0.237 -> 0.321 ms) lose, hence
+// the conditions.  (Round 4 before the striped counters: a single funnel query 0.686 -> 0.770 ms
+// with the probe on for every batch.)  PF_PROBE_MAX_SETS sets the bound, 0 turns it off.
+uint32_t g_probe_max_sets = 64;
 
 int fail(const char* fmt, ...) {
     char buf[512];
@@ -94,6 +98,7 @@ struct Batch {
     uint32_t* d_parents = nullptr;
     uint32_t* d_found = nullptr;
     uint32_t* d_order = nullptr;    // set ids, most expensive first (search-kernel wave order)
+    bool all_parented = false;      // every set carries a parent / hint model (candidate 0)
     uint32_t* d_scratch = nullptr;  // this batch's t0 (u64 [4]), queue heads and counter lines (pf_bytecode.h)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     ~Batch() {  // the device block goes back to its device's pool first (release_batch)
@@ -241,12 +246,10 @@ int check_enqueue(Batch* B, uint64_t gseed, uint32_t budget, uint32_t flags, uin
     const bool early = flags & PF_FLAG_EARLY_EXIT;
     // phase 0: the probe (early exit, small batches: candidates 0..63 of every set, one wave
     // per set); phase 1: the search over the whole budget, whose waves skip decided sets
-    const bool probe = early && budget > 64u && B->n_sets <= g_probe_max_sets;
+    const bool probe = early && budget > 64u && B->n_sets >= 2 && B->n_sets <= g_probe_max_sets &&
+                       B->all_parented;
     for (int phase = probe ? 0 : 1; phase < 2; ++phase) {
     const uint32_t pbudget = phase == 0 ? 64u : budget;
-    if (phase == 1 && probe)  // fresh queue heads for the second launch (stream-ordered)
-        HIPCHK(hipMemsetAsync(B->d_scratch + PF_EARLY_QUEUE_OFF / 4, 0,
-                              2 * PF_EARLY_QUEUES * PF_EARLY_QUEUE_STRIDE * 4, st));
     // the 8-register sets first, then the 16-register ones (usually none)
     for (int part = 0; part < 2; ++part) {
         const size_t first = part ? B->n_narrow : 0;
@@ -263,8 +266,9 @@ int check_enqueue(Batch* B, uint64_t gseed, uint32_t budget, uint32_t flags, uin
         const uint64_t waves = early ? std::min<uint64_t>(items, (uint64_t)D->num_cus * g_waves_per_cu_early)
                              : PF_FULL_QUEUE ? std::min<uint64_t>(items, (uint64_t)D->num_cus * 16u)
                                              : items;
+        // each (phase, part) launch has its own heads, all zeroed by the reset above
         uint32_t* d_queue =
-            B->d_scratch + PF_EARLY_QUEUE_OFF / 4 + part * PF_EARLY_QUEUES * PF_EARLY_QUEUE_STRIDE;
+            B->d_scratch + PF_EARLY_QUEUE_OFF / 4 + (phase * 2 + part) * PF_EARLY_QUEUES * PF_EARLY_QUEUE_STRIDE;
         const uint32_t blocks = (uint32_t)((waves + PF_SEARCH_WG_WAVES - 1) / PF_SEARCH_WG_WAVES);
         hipLaunchKernelGGL(part == 0 ? (early ? pf_check_early_kernel : pf_check_kernel)
                                      : (early ? pf_check_early_r16_kernel : pf_check_r16_kernel),
@@ -746,6 +750,7 @@ int pf_batch_create_on(int device, const uint32_t* code, size_t n_ins, const uin
     B->n_sets = n_sets;
     B->max_vars = max_vars;
     B->n_narrow = (size_t)std::count(wide.begin(), wide.end(), (uint8_t)0);
+    B->all_parented = std::all_of(descs, descs + n_sets, [](const pf_set_desc& d) { return d.parent_off != PF_NO_PARENT; });
     B->h_descs.assign(descs, descs + n_sets);
     B->d_mem = pool_acquire(Dv, total, &B->mem_cap);
     if (!B->d_mem) {

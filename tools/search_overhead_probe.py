@@ -40,6 +40,17 @@ def main():
         print(f"{'planted' if plant else 'search '} sets {n:3d} ({int(r.sat.sum())} sat): wall median {np.median(w):.4f} ms mean {w.mean():.4f} | kernel (events) "
               f"median {np.median(k):.4f} ms | host+runtime {np.median(w) - np.median(k):.4f} ms | witnesses {[int(x) for x in r.found[:16]]}", flush=True)
         db.free()
+    # upload (pf_batch_create: validation, device program, one copy) of one prepared batch
+    from mythril_amd.ir import Batch
+    for n in (1, 4, 16):
+        b = Batch([synth.random_dag_set(i, plant=True)[0] for i in range(n)])
+        ts = []
+        for _ in range(reps):
+            t = time.perf_counter()
+            db = eng.upload(b)
+            ts.append(1e3 * (time.perf_counter() - t))
+            db.free()
+        print(f"upload sets {n:3d}: median {np.median(ts):.4f} ms mean {np.mean(ts):.4f}", flush=True)
 
 
 if __name__ == "__main__":
