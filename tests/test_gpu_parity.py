@@ -167,6 +167,36 @@ def test_planted_witness_found_at_candidate_zero(engine):
     assert (res.found == 0).all()
 
 
+@pytest.mark.parametrize("n_sets", [1, 2, 20, 64, 65])
+def test_parented_small_batches_match_oracle(engine, n_sets):
+    """Batches whose every set carries a parent model (2..64 of them take the probe launch,
+    pathfeas.hip check_enqueue): candidate 0 is the witness for the untouched planted sets,
+    not for the sets whose parent values were shifted by one (the search then continues from
+    candidate 64 in the second launch, or finds a neighbourhood candidate among 1..63).  The
+    smallest witness equals the oracle's either way, and with 1 or 65 sets (no probe) too."""
+    import copy
+
+    budget, seed = 2048, 0x5EED_0042
+    progs = []
+    for i in range(n_sets):
+        p = synth.random_dag_set(500 + i, plant=True)[0]
+        if i % 3 == 1:
+            p = copy.deepcopy(p)
+            for v in p.vars:
+                if v.parent is not None:
+                    v.parent = (v.parent + 1) & ((1 << v.width) - 1)
+        progs.append(p)
+    assert all(p.has_parent for p in progs)
+    res = engine.check(engine.upload(progs), budget=budget, seed=seed,
+                       flags=ir.FLAG_EARLY_EXIT | ir.FLAG_SHORTCIRCUIT)
+    for i, p in enumerate(progs):
+        want = _oracle_first(p, budget, seed)
+        got = None if res.found[i] == 0xFFFFFFFF else int(res.found[i])
+        assert got == want, (n_sets, i, got, want)
+        if i % 3 != 1:
+            assert got == 0
+
+
 def test_materialize_matches_generator(engine):
     progs = [synth.random_dag_set(400 + i, plant=(i % 2 == 0))[0] for i in range(6)]
     progs.append(synth.mythril_like_set(5))
