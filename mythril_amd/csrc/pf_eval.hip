@@ -962,16 +962,8 @@ PF_INL void search_item(const SetCtx& S, uint32_t set, uint32_t begin, uint32_t 
         const bool active = cand < end;
         uint32_t complete = 0;
         uint64_t lane_ops = 0;
-#ifdef PF_PRIO_FIRST
-        // the group holding candidate 0 (the parent / hint model: the witness of most live
-        // queries) is issued ahead of the other waves on its SIMD
-        if (EARLY && base == 0u) __builtin_amdgcn_s_setprio(3);
-#endif
         uint32_t sat = run_program<MODE_GEN, NREG>(S, cand, active, flags, nullptr, 0u, exp_tbl, &complete,
                                              &lane_ops, &prof);
-#ifdef PF_PRIO_FIRST
-        if (EARLY && base == 0u) __builtin_amdgcn_s_setprio(0);
-#endif
         const uint64_t m_act = __ballot(active);
         const uint64_t m_sat = __ballot((uint32_t)active & sat);
         const uint64_t m_full = __ballot((uint32_t)active & complete);
