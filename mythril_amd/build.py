@@ -30,7 +30,7 @@ def _stale() -> bool:
 
 
 LOWER_OUT = os.path.join(HERE, "libpflower.so")
-LOWER_SOURCES = ["pf_lower.cpp", "pf_seed.cpp", "pf_terms.cpp", "pf_recheck.cpp", os.path.join("..", "..", "include", "pf_lower.h"),
+LOWER_SOURCES = ["pf_lower.cpp", "pf_seed.cpp", "pf_terms.cpp", "pf_recheck.cpp", "pf_pool.h", os.path.join("..", "..", "include", "pf_lower.h"),
                  os.path.join("..", "..", "include", "pf_bytecode.h")]
 
 

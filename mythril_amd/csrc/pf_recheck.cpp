@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "../../include/pf_lower.h"
+#include "pf_pool.h"
 
 namespace {
 
@@ -752,16 +753,5 @@ extern "C" void pflt_recheck_many(void* store, void* const* results, size_t n, c
         for (size_t i = 0; i < nro; i++) ok &= out[i] ? 1 : 0;
         status[j] = ok;
     };
-    const size_t nt = std::min<size_t>(n_threads ? n_threads : 1, n);
-    if (nt <= 1) {
-        for (size_t j = 0; j < n; j++) one(j);
-        return;
-    }
-    std::atomic<size_t> next{0};
-    std::vector<std::thread> pool;
-    for (size_t t = 0; t < nt; t++)
-        pool.emplace_back([&]() {
-            for (size_t j; (j = next.fetch_add(1)) < n;) one(j);
-        });
-    for (auto& th : pool) th.join();
+    pfpool::parallel_for(n, n_threads, one);
 }

@@ -32,6 +32,7 @@
 
 #include "../../include/pf_bytecode.h"
 #include "../../include/pf_lower.h"
+#include "pf_pool.h"
 
 namespace {
 
@@ -2051,18 +2052,7 @@ void pflt_lower_many(void* st, const pflt_job* jobs, size_t n, const uint32_t* r
         results[j] = lower_job(S, std::vector<uint32_t>(jb.roots, jb.roots + jb.n_roots),
                                jb.parents ? *(const Parents*)jb.parents : none, registry, n_registry, jb.flags);
     };
-    const size_t nt = std::min<size_t>(n_threads ? n_threads : 1, n);
-    if (nt <= 1) {
-        for (size_t j = 0; j < n; j++) one(j);
-        return;
-    }
-    std::atomic<size_t> next{0};
-    std::vector<std::thread> pool;
-    for (size_t t = 0; t < nt; t++)
-        pool.emplace_back([&]() {
-            for (size_t j; (j = next.fetch_add(1)) < n;) one(j);
-        });
-    for (auto& th : pool) th.join();
+    pfpool::parallel_for(n, n_threads, one);
 }
 
 int pflt_result_status(const void* res) { return ((const Result*)res)->rc; }
