@@ -362,7 +362,16 @@ PF_INL u256 gen_var(const SetCtx& S, uint32_t v, uint32_t cand) {
     // r1 only feeds limbs 4..7 of the random arm, which the final mask clears for w <= 128
     // (bytes, selectors, small counters): skipped there under a wave-uniform branch
     uint4 r1 = make_uint4(0u, 0u, 0u, 0u);
+#ifdef PF_DIAG_R1_CHEAP  // timing probe only (wrong values): limbs 4..7 from a cheap mix of r0
+    if (w > 128u) {
+        r1.x = __umulhi(r0.x ^ 0x9E3779B9u, 0xD2511F53u) ^ r0.w;
+        r1.y = __umulhi(r0.y ^ 0x7F4A7C15u, 0xCD9E8D57u) ^ r0.x;
+        r1.z = __umulhi(r0.z ^ 0x85EBCA6Bu, 0xD2511F53u) ^ r0.y;
+        r1.w = __umulhi(r0.w ^ 0xC2B2AE35u, 0xCD9E8D57u) ^ r0.z;
+    }
+#else
     if (w > 128u) r1 = philox_gen(p0, v, 1u, S.k0, S.k1);
+#endif
     const bool has_parent = pslot != PF_NO_PARENT;
     u256 par = pf::zero256();
     if (has_parent) {
