@@ -285,14 +285,15 @@ int check_enqueue(Batch* B, uint64_t gseed, uint32_t budget, uint32_t flags, uin
 
 // Pinned host staging for the counter lines and verdicts a search reads back: a copy into
 // pageable memory is staged and synchronous in the runtime (two of them were ~25 us of a
-// single-query search's ~45 us outside the kernel); per host thread, grown on demand, never
-// shrunk, and kept to process exit.  nullptr (pageable fallback) if the allocation fails.
+// single-query search's ~45 us outside the kernel); one buffer for the process (every entry
+// point that reads results back holds g_mu), grown on demand, never shrunk, kept to process
+// exit.  nullptr (pageable fallback) if the allocation fails.
 uint8_t* pinned_staging(size_t bytes) {
     struct Pin {
         uint8_t* p = nullptr;
         size_t cap = 0;
     };
-    thread_local Pin t;
+    static Pin t;
     if (bytes > t.cap) {
         if (t.p) (void)hipHostFree(t.p);
         t.p = nullptr;
