@@ -130,7 +130,7 @@ class Witness:
                 last = r
         for i in range(last + 1):
             it, sel = reads[i]
-            if self.ev(it) == iv:
+            if self._evr(it) == iv:
                 return self.reads.get(sel, 0)
         return 0
 
@@ -140,7 +140,7 @@ class Witness:
         for name, reads in self.array_reads.items():
             tab: Dict[int, int] = {}
             for it, sel in reads:
-                iv = self.ev(it)
+                iv = self._evr(it)
                 if iv not in tab:
                     tab[iv] = self.reads.get(sel, 0)
             out[name] = tab
@@ -149,17 +149,20 @@ class Witness:
         return out
 
     def _select(self, arr: T.Term, iv: int, idx: Optional[T.Term] = None) -> int:
-        if arr.op == "store":
-            if self.ev(arr.args[1]) == iv:
-                return self.ev(arr.args[2])
-            return self._select(arr.args[0], iv, idx)
-        if arr.op == "K":
-            return self.ev(arr.args[0])
-        if arr.op == "ite":
-            return self._select(arr.args[1] if self.ev(arr.args[0]) else arr.args[2], iv, idx)
-        if arr.op == "array":
-            return self._array_read(arr, idx, iv)
-        raise ValueError(f"select over {arr.op}")
+        while True:  # a loop, not recursion: LASER's store chains are thousands deep
+            if arr.op == "store":
+                if self._evr(arr.args[1]) == iv:
+                    return self._evr(arr.args[2])
+                arr = arr.args[0]
+                continue
+            if arr.op == "K":
+                return self._evr(arr.args[0])
+            if arr.op == "ite":
+                arr = arr.args[1] if self._evr(arr.args[0]) else arr.args[2]
+                continue
+            if arr.op == "array":
+                return self._array_read(arr, idx, iv)
+            raise ValueError(f"select over {arr.op}")
 
     # ---- UFs ----------------------------------------------------------------------------
     def _keccak(self, n: int, x: int) -> int:
@@ -183,11 +186,11 @@ class Witness:
             before.append((fname, args, app))
         for (fname, args, app) in before:
             if fname == f"keccak256_{n}":
-                x = self.ev(args[0])
+                x = self._evr(args[0])
                 if self._keccak(n, x) == y:
                     return x
         for (fname, args, app) in before:
-            if fname == f"keccak256_{n}-1" and app in self.reads and self.ev(args[0]) == y:
+            if fname == f"keccak256_{n}-1" and app in self.reads and self._evr(args[0]) == y:
                 return self.reads[app]
         return self.reads.get(term, 0)
 
@@ -198,20 +201,20 @@ class Witness:
             n = int(m.group(1))
             a = t.args[0]
             if m.group(2) is not None and a.op == "apply" and a.val[0] == f"keccak256_{n}":
-                return self.ev(a.args[0])  # inv(f(x)) = x, as substituted by the lowering
-            x = self.ev(a)
+                return self._evr(a.args[0])  # inv(f(x)) = x, as substituted by the lowering
+            x = self._evr(a)
             return self._keccak(n, x) if m.group(2) is None else self._keccak_inv(n, x, t)
         if fname == "Power" and len(t.args) == 2 and t.width == 256:
             return self._power(t)
         h = None
         for a in t.args:
-            for c in _chunks(self.ev(a), a.width):
+            for c in _chunks(self._evr(a), a.width):
                 h = uf_hash(c if h is None else h ^ c, salt_of(fname))
         return h & T.M(t.width)
 
     def _power(self, t: T.Term) -> int:
         """The lowering's Power interpretation (to_dag.TermLowering._power), by value."""
-        b, e = self.ev(t.args[0]), self.ev(t.args[1])
+        b, e = self._evr(t.args[0]), self._evr(t.args[1])
         apps = [(args, app) for (fname, args, app) in self.uf_apps if fname == "Power" and len(args) == 2]
         for args, _ in apps:
             if args[0].op == "bv" and args[1].op == "bv" and (args[0].val, args[1].val) == (b, e):
@@ -219,12 +222,45 @@ class Witness:
         if b == 256:
             return 1 << (8 * (e % 32))
         for args, app in apps:
-            if app in self.reads and (self.ev(args[0]), self.ev(args[1])) == (b, e):
+            if app in self.reads and (self._evr(args[0]), self._evr(args[1])) == (b, e):
                 return self.reads[app]
         return 1   # model completion outside the set's applications: a positive value
 
     # ---- evaluator ------------------------------------------------------------------------
     def ev(self, t: T.Term):
+        """Value of ``t`` under this witness.  A term nested deeper than Python's recursion
+        limit (long and / or / ite chains of a large LASER state) is first evaluated bottom-up
+        without recursion — every subterm, in post-order, each from its memoised children —
+        and the recursive evaluator then finishes on memo hits."""
+        try:
+            return self._evr(t)
+        except RecursionError:
+            self._prefill(t)
+            return self._evr(t)
+
+    def _prefill(self, root: T.Term) -> None:
+        order, seen, stack = [], set(), [(root, False)]
+        while stack:
+            t, done = stack.pop()
+            if done:
+                order.append(t)
+                continue
+            if t in seen or t in self._memo:
+                continue
+            seen.add(t)
+            stack.append((t, True))
+            for a in t.args:
+                if a not in seen and a not in self._memo:
+                    stack.append((a, False))
+        for t in order:
+            if t in self._memo:
+                continue
+            try:
+                self._memo[t] = self._ev(t)
+            except Exception:  # array-sorted terms, or a value only a lazy branch may need
+                pass
+
+    def _evr(self, t: T.Term):
         r = self._memo.get(t)
         if r is not None:
             return r
@@ -246,40 +282,40 @@ class Witness:
             return self.bools.get(t.val, False)
         w = t.width
         if op in T._FOLD2:
-            return T._FOLD2[op](self.ev(t.args[0]), self.ev(t.args[1]), w)
+            return T._FOLD2[op](self._evr(t.args[0]), self._evr(t.args[1]), w)
         if op in T._CMP:
             a = t.args[0]
-            return bool(T._CMP[op](self.ev(a), self.ev(t.args[1]), a.width))
+            return bool(T._CMP[op](self._evr(a), self._evr(t.args[1]), a.width))
         if op == "bvnot":
-            return ~self.ev(t.args[0]) & T.M(w)
+            return ~self._evr(t.args[0]) & T.M(w)
         if op == "bvneg":
-            return -self.ev(t.args[0]) & T.M(w)
+            return -self._evr(t.args[0]) & T.M(w)
         if op == "extract":
             hi, lo = t.val
-            return (self.ev(t.args[0]) >> lo) & T.M(hi - lo + 1)
+            return (self._evr(t.args[0]) >> lo) & T.M(hi - lo + 1)
         if op == "concat":
             v = 0
             for a in t.args:
-                v = (v << a.width) | self.ev(a)
+                v = (v << a.width) | self._evr(a)
             return v
         if op == "zero_extend":
-            return self.ev(t.args[0])
+            return self._evr(t.args[0])
         if op == "ite":
-            return self.ev(t.args[1]) if self.ev(t.args[0]) else self.ev(t.args[2])
+            return self._evr(t.args[1]) if self._evr(t.args[0]) else self._evr(t.args[2])
         if op == "select":
-            return self._select(t.args[0], self.ev(t.args[1]), t.args[1])
+            return self._select(t.args[0], self._evr(t.args[1]), t.args[1])
         if op == "apply":
             return self._apply(t)
         if op == "=":
-            return self.ev(t.args[0]) == self.ev(t.args[1])
+            return self._evr(t.args[0]) == self._evr(t.args[1])
         if op == "iff":
-            return bool(self.ev(t.args[0])) == bool(self.ev(t.args[1]))
+            return bool(self._evr(t.args[0])) == bool(self._evr(t.args[1]))
         if op == "and":
-            return all(self.ev(a) for a in t.args)
+            return all(self._evr(a) for a in t.args)
         if op == "or":
-            return any(self.ev(a) for a in t.args)
+            return any(self._evr(a) for a in t.args)
         if op == "not":
-            return not self.ev(t.args[0])
+            return not self._evr(t.args[0])
         if op == "xor":
-            return bool(self.ev(t.args[0])) != bool(self.ev(t.args[1]))
+            return bool(self._evr(t.args[0])) != bool(self._evr(t.args[1]))
         raise ValueError(f"cannot evaluate {op}")

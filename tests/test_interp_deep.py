@@ -1,0 +1,51 @@
+"""The host witness evaluator (smt/interp.py, Model.eval's interpretation) on terms nested
+deeper than Python's recursion limit: a large LASER state's constraints are long and / or /
+ite chains and thousands-deep storage store chains.  Values must equal a direct
+(non-recursive) evaluation; found at 5x corpus scale, where the planted-model check raised
+RecursionError."""
+
+import sys
+
+from mythril_amd import corpus
+from mythril_amd.smt import terms as T
+from mythril_amd.smt.to_dag import UFRegistry
+
+
+def _eval(vars_, arrays=None):
+    return corpus._PlantedEval(corpus.Planted(vars=dict(vars_), arrays=dict(arrays or {})), UFRegistry())
+
+
+def test_deep_and_or_chain():
+    depth = 4 * sys.getrecursionlimit()
+    x = T.var("x", 256)
+    t = T.cmp("bvult", x, T.const(10, 256))
+    want = True
+    for i in range(depth):
+        c = T.eq(x, T.const(3 + (i % 5), 256))
+        if i % 2:
+            t = T.and_(t, T.or_(c, T.not_(c)))
+        else:
+            t = T.or_(t, T.and_(c, T.not_(c)))
+    assert _eval({"x": 4}).ev(t) == want
+    assert not _eval({"x": 40}).ev(t)
+
+
+def test_deep_arithmetic_and_ite_chain():
+    depth = 4 * sys.getrecursionlimit()
+    x = T.var("x", 256)
+    v, want, xv = x, 7, 7
+    for i in range(depth):
+        v = T.ite(T.cmp("bvult", v, T.const(1 << 200, 256)), T.binop("bvadd", v, T.const(i, 256)), v)
+        want = (want + i) % (1 << 256) if want < (1 << 200) else want
+    assert _eval({"x": xv}).ev(v) == want
+
+
+def test_deep_store_chain_select():
+    n = 4 * sys.getrecursionlimit()
+    a = T.const_array(256, T.const(0, 256))
+    for i in range(n):
+        a = T.store(a, T.const(i, 256), T.const(i * i + 1, 256))
+    ev = _eval({})
+    assert ev.ev(T.select(a, T.const(0, 256))) == 1
+    assert ev.ev(T.select(a, T.const(n - 1, 256))) == (n - 1) ** 2 + 1
+    assert ev.ev(T.select(a, T.const(n + 5, 256))) == 0
