@@ -24,24 +24,33 @@ _REBUILD = {
 
 
 def substitute(t: T.Term, old: T.Term, new: T.Term, _memo=None) -> T.Term:
+    """``t`` with every occurrence of ``old`` replaced by ``new``: an iterative post-order walk
+    (LASER terms nest deeper than Python's recursion limit), each node rebuilt through its
+    folding constructor only when one of its arguments changed."""
     memo = {} if _memo is None else _memo
+    stack = [(t, False)]
+    while stack:
+        u, ready = stack.pop()
+        if u is old or not u.args or u in memo:
+            continue
+        if not ready:
+            stack.append((u, True))
+            for a in u.args:
+                if a is not old and a.args and a not in memo:
+                    stack.append((a, False))
+            continue
+        args = [new if a is old else (memo.get(a, a) if a.args else a) for a in u.args]
+        if all(x is y for x, y in zip(args, u.args)):
+            r = u
+        elif u.op in _REBUILD:
+            r = _REBUILD[u.op](u, args)
+        elif u.op in T._FOLD2:
+            r = T.binop(u.op, *args)
+        elif u.op in T._CMP:
+            r = T.cmp(u.op, *args)
+        else:
+            raise ValueError(f"substitute: unknown op {u.op}")
+        memo[u] = r
     if t is old:
         return new
-    if not t.args:
-        return t
-    r = memo.get(t)
-    if r is not None:
-        return r
-    args = [substitute(a, old, new, memo) for a in t.args]
-    if all(x is y for x, y in zip(args, t.args)):
-        r = t
-    elif t.op in _REBUILD:
-        r = _REBUILD[t.op](t, args)
-    elif t.op in T._FOLD2:
-        r = T.binop(t.op, *args)
-    elif t.op in T._CMP:
-        r = T.cmp(t.op, *args)
-    else:
-        raise ValueError(f"substitute: unknown op {t.op}")
-    memo[t] = r
-    return r
+    return memo.get(t, t) if t.args else t

@@ -49,3 +49,20 @@ def test_deep_store_chain_select():
     assert ev.ev(T.select(a, T.const(0, 256))) == 1
     assert ev.ev(T.select(a, T.const(n - 1, 256))) == (n - 1) ** 2 + 1
     assert ev.ev(T.select(a, T.const(n + 5, 256))) == 0
+
+
+def test_substitute_deep_chain():
+    from mythril_amd.smt.subst import substitute
+
+    depth = 4 * sys.getrecursionlimit()
+    x, y = T.var("x", 256), T.var("y", 256)
+    v = x
+    for i in range(depth):
+        v = T.binop("bvadd", T.binop("bvmul", v, T.const(3, 256)), T.const(i, 256))
+    w = substitute(v, x, y)
+    want = 5
+    for i in range(depth):
+        want = (want * 3 + i) % (1 << 256)
+    assert _eval({"y": 5}).ev(w) == want
+    folded = substitute(v, x, T.const(5, 256))   # the folding constructors reduce it to a constant
+    assert folded.op == "bv" and folded.val == want
