@@ -289,7 +289,41 @@ def apply_indexed(op: str, params: List[int], args: List[T.Term]) -> T.Term:
 
 
 def read_query(text: str) -> Query:
-    return Reader().read(text)
+    """One --solver-log query.  z3 prints shared subterms as nested ``let`` bindings, so a
+    large dump nests thousands deep: past Python's recursion limit the reader runs again on
+    a thread with a 512 MiB stack and a raised limit."""
+    try:
+        return Reader().read(text)
+    except RecursionError:
+        return _on_deep_stack(lambda: Reader().read(text))
+
+
+def _on_deep_stack(fn):
+    import sys
+    import threading
+
+    out = {}
+
+    def run():
+        old = sys.getrecursionlimit()
+        sys.setrecursionlimit(max(old, 1_000_000))
+        try:
+            out["r"] = fn()
+        except BaseException as e:  # re-raised on the caller's thread
+            out["e"] = e
+        finally:
+            sys.setrecursionlimit(old)
+
+    prev = threading.stack_size(512 << 20)
+    try:
+        th = threading.Thread(target=run, name="smtlib-deep")
+        th.start()
+    finally:
+        threading.stack_size(prev)
+    th.join()
+    if "e" in out:
+        raise out["e"]
+    return out["r"]
 
 
 def read_file(path: str) -> Query:

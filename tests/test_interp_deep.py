@@ -66,3 +66,23 @@ def test_substitute_deep_chain():
     assert _eval({"y": 5}).ev(w) == want
     folded = substitute(v, x, T.const(5, 256))   # the folding constructors reduce it to a constant
     assert folded.op == "bv" and folded.val == want
+
+
+def test_smtlib_reader_deep_let_chain():
+    """z3's --solver-log output nests a let per shared subterm."""
+    from mythril_amd import smtlib
+
+    depth = 6 * sys.getrecursionlimit()
+    body = "x"
+    for i in range(depth):
+        body = f"(let ((a!{i} (bvadd {body} #x{(i % 251):064x}))) a!{i})"
+    text = f"(declare-fun x () (_ BitVec 256))\n(assert (= {body} #x{0:064x}))\n(check-sat)\n"
+    import pytest
+
+    with pytest.raises(RecursionError):   # the recursive reader alone cannot take it
+        smtlib.Reader().read(text)
+    q = smtlib.read_query(text)
+    assert len(q.assertions) == 1
+    want = (-sum(i % 251 for i in range(depth))) % (1 << 256)
+    assert _eval({"x": want}).ev(q.assertions[0])
+    assert not _eval({"x": want + 1}).ev(q.assertions[0])
