@@ -42,6 +42,10 @@ struct TermError {
     int rc;
 };
 
+#ifndef PF_MAX_TERM_DEPTH
+#define PF_MAX_TERM_DEPTH 5000u
+#endif
+
 [[noreturn]] void lerr(const char* fmt, ...) {
     char buf[256];
     va_list ap;
@@ -152,6 +156,7 @@ uint32_t crc32_of(const std::string& s) {  // zlib.crc32 (to_dag.salt_of)
 // ---- the term store -------------------------------------------------------------------
 struct TermRec {
     uint32_t op, sortk, w1, w2;
+    uint32_t depth = 1;  // nesting depth (1 + the deepest argument's), set by pflt_add
     std::vector<uint32_t> args;
     int64_t i0, i1;
     Big val;
@@ -1475,8 +1480,14 @@ Result* lower_job(const Store& S, const std::vector<uint32_t>& rs, const Parents
             }
             L.kspecs[n] = sp;
         }
-        for (uint32_t r : rs)
+        for (uint32_t r : rs) {
             if (r >= S.t.size()) lerr("root not in the store");
+            // the term -> DAG -> program passes recurse over the nesting: past this depth a
+            // host thread's 8 MiB stack could overflow (a 25,000-deep chain did), so such a
+            // bucket is left to z3 like any other LoweringError
+            if (S.t[r].depth > PF_MAX_TERM_DEPTH)
+                lerr("term nested %u deep (more than %u): left to z3", S.t[r].depth, (unsigned)PF_MAX_TERM_DEPTH);
+        }
         L.lower(rs);
         R->var_terms = L.var_terms;
         R->uf_apps = L.uf_apps;
@@ -1628,6 +1639,7 @@ int64_t pflt_add(void* st, uint32_t op, uint32_t sortk, uint32_t w1, uint32_t w2
             return -1;
         }
         r.args.push_back(args[i]);
+        r.depth = std::max(r.depth, S->t[args[i]].depth + 1u);
     }
     r.i0 = i0;
     r.i1 = i1;

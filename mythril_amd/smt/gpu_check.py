@@ -297,9 +297,10 @@ def _lower_chunk(job):
             lo, prog = _lower_bucket(bucket, reg, parent, hints)
             out.append((Lowered(None, lo.var_terms, lo.uf_apps, lo.array_reads), prog, None))
             lo = None
-        except (LoweringError, ValueError, OverflowError) as e:
-            # one bucket the lowering cannot take (or whose native emission fails) is that
-            # bucket's failure only: the rest of the batch is still searched
+        except (LoweringError, ValueError, OverflowError, RecursionError) as e:
+            # one bucket the lowering cannot take (or whose native emission fails; or, on the
+            # Python lowering, a term nested past the recursion limit) is that bucket's
+            # failure only: the rest of the batch is still searched
             out.append((None, None, f"{type(e).__name__}: {e}" if not isinstance(e, LoweringError) else str(e)))
     return out
 

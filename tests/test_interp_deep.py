@@ -86,3 +86,27 @@ def test_smtlib_reader_deep_let_chain():
     want = (-sum(i % 251 for i in range(depth))) % (1 << 256)
     assert _eval({"x": want}).ev(q.assertions[0])
     assert not _eval({"x": want + 1}).ev(q.assertions[0])
+
+
+def test_native_lowering_leaves_over_deep_terms_to_z3():
+    """The native term -> program passes recurse over the nesting; a term deeper than
+    PF_MAX_TERM_DEPTH (5000) is a LoweringError (the bucket goes to z3) instead of a host
+    stack overflow (a 25,000-deep chain segfaulted the process before)."""
+    import pytest
+
+    from mythril_amd.smt import gpu_check, native_terms
+    if native_terms.batch_api() is None:
+        pytest.skip("libpflower.so not built")
+    x, y = T.var("x", 256), T.var("y", 256)
+
+    def chain(depth):
+        v = x
+        for i in range(depth):
+            v = T.binop("bvxor", T.binop("bvadd", v, y), T.const(i + 1, 256)) if i % 2 else T.binop("bvmul", v, y)
+        return T.cmp("bvult", v, T.const(12345, 256))
+
+    shallow, deep = chain(1000), chain(20000)
+    res = native_terms.lower_many([([shallow], None), ([deep], None)], UFRegistry(), True,
+                                  [gpu_check._set_seed([shallow]), gpu_check._set_seed([deep])], 1)
+    assert res[0][2] is None and res[0][1] is not None
+    assert res[1][0] is None and "left to z3" in res[1][2]
