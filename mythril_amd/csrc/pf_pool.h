@@ -19,7 +19,9 @@ namespace pfpool {
 
 class Pool {
    public:
-    // fn(0) .. fn(n - 1) on the caller and up to n_threads - 1 workers; returns when all ran
+    // fn(0) .. fn(n - 1) on the caller and up to n_threads - 1 workers; returns when all ran.
+    // fn must not throw (lower_job and the re-check report failures in their results) and
+    // must not call run() itself (one fork-join at a time)
     void run(size_t n, size_t n_threads, const std::function<void(size_t)>& fn) {
         const size_t nt = n_threads < n ? n_threads : n;
         if (nt <= 1) {
