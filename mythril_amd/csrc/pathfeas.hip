@@ -887,25 +887,50 @@ int pf_materialize(uint64_t handle, uint64_t global_seed, const uint32_t* set_id
     }
     if (total == 0) return 0;
     if (switch_stream(D, st)) return -1;
-    DevBuf b_sets, b_cands, b_off, b_out;
-    HIPCHK(hipMalloc(&b_sets.p, n * 4));
-    HIPCHK(hipMalloc(&b_cands.p, n * 4));
-    HIPCHK(hipMalloc(&b_off.p, n * 4));
-    HIPCHK(hipMalloc(&b_out.p, total * 32));
-    uint32_t *d_sets = b_sets.as<uint32_t>(), *d_cands = b_cands.as<uint32_t>(),
-             *d_off = b_off.as<uint32_t>(), *d_out = b_out.as<uint32_t>();
-    HIPCHK(hipMemcpyAsync(d_sets, set_ids, n * 4, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(d_cands, cand_ids, n * 4, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(d_off, off.data(), n * 4, hipMemcpyHostToDevice, st));
-    const uint32_t mv = std::max<uint32_t>(B->max_vars, 1u);
-    const uint64_t threads = (uint64_t)n * mv;
-    hipLaunchKernelGGL(pf_materialize_kernel, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0,
-                       st, B->d_descs, B->d_code, B->d_consts, B->d_schema, B->d_parents,
-                       global_seed, d_sets, d_cands, d_off, (uint32_t)n, mv, d_out);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(values_out, d_out, total * 32, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    return 0;
+    // one block from the device pool ([sets | cands | offsets | values], the index arrays
+    // 256-byte aligned) and the pinned staging buffer for both copies: no hipMalloc / hipFree
+    // (hipFree synchronises the device) and no pageable copies per call — this runs once per
+    // funnel query whose witness is not a parented candidate 0
+    const size_t o_in = ((3 * n * 4) + 255) & ~size_t(255), bytes = o_in + total * 32;
+    size_t cap = 0;
+    uint8_t* dm = static_cast<uint8_t*>(pool_acquire(D, bytes, &cap));
+    if (!dm) return fail("pf_materialize: hipMalloc(%zu) failed", bytes);
+    uint32_t *d_sets = reinterpret_cast<uint32_t*>(dm), *d_cands = d_sets + n, *d_off = d_cands + n,
+             *d_out = reinterpret_cast<uint32_t*>(dm + o_in);
+    uint8_t* pin = pinned_staging(std::max<size_t>(3 * n * 4, total * 32));
+    int rc = 0;
+    if (pin) {
+        memcpy(pin, set_ids, n * 4);
+        memcpy(pin + n * 4, cand_ids, n * 4);
+        memcpy(pin + 2 * n * 4, off.data(), n * 4);
+        if (hipMemcpyAsync(d_sets, pin, 3 * n * 4, hipMemcpyHostToDevice, st) != hipSuccess) rc = -1;
+    } else if (hipMemcpyAsync(d_sets, set_ids, n * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
+               hipMemcpyAsync(d_cands, cand_ids, n * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
+               hipMemcpyAsync(d_off, off.data(), n * 4, hipMemcpyHostToDevice, st) != hipSuccess) {
+        rc = -1;
+    }
+    if (!rc) {
+        const uint32_t mv = std::max<uint32_t>(B->max_vars, 1u);
+        const uint64_t threads = (uint64_t)n * mv;
+        hipLaunchKernelGGL(pf_materialize_kernel, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0,
+                           st, B->d_descs, B->d_code, B->d_consts, B->d_schema, B->d_parents,
+                           global_seed, d_sets, d_cands, d_off, (uint32_t)n, mv, d_out);
+        // the staging buffer is reused for the values: the stream orders the copies after the
+        // kernel, which has consumed the index copy
+        if (hipGetLastError() != hipSuccess ||
+            hipMemcpyAsync(pin ? static_cast<void*>(pin) : static_cast<void*>(values_out), d_out, total * 32,
+                           hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            rc = -1;
+    }
+    if (!rc && pin) memcpy(values_out, pin, total * 32);
+    // back to the pool (the stream is drained, or the launch failed)
+    if (D->pool.size() >= kPoolBlocks) {
+        hipFree(D->pool.front().first);
+        D->pool.erase(D->pool.begin());
+    }
+    D->pool.emplace_back(dm, cap);
+    return rc ? fail("pf_materialize: HIP call failed") : 0;
 }
 
 static int eval_launch(Batch* B, uint32_t set, const uint32_t* d_soa, uint32_t n_cand,
