@@ -72,10 +72,12 @@ int pf_batch_create_on(int device, const uint32_t* code, size_t n_ins, const uin
 
 /* Host only (no device call; for tests): the program pf_batch_create puts on the device for
  * this batch — traffic/unit bits recomputed, then its peepholes (an ASSERT folded into the
- * compare before it, PF_I_ASSERT; a W_CONST folded into its readers, PF_I_KA / PF_I_KB).
+ * compare before it, PF_I_ASSERT; a W_CONST folded into its readers, PF_I_KA / PF_I_KB, only
+ * when its constant fits the W_CONST's width — consts may be NULL: all taken to fit).
  * code_out: room for n_ins instructions; descs_out: n_sets entries (code ranges shifted). */
-int pf_device_program(const uint32_t* code, size_t n_ins, const pf_set_desc* descs, size_t n_sets,
-                      uint32_t* code_out, size_t* n_ins_out, pf_set_desc* descs_out);
+int pf_device_program(const uint32_t* code, size_t n_ins, const uint32_t* consts, size_t n_const,
+                      const pf_set_desc* descs, size_t n_sets, uint32_t* code_out, size_t* n_ins_out,
+                      pf_set_desc* descs_out);
 int pf_batch_free(uint64_t handle);
 
 /* Generate candidates [0, budget) on device for every set and search for a witness.

@@ -67,7 +67,7 @@ SIGNATURES = {
                                            ctypes.c_uint32, _u8p]),
     "pf_eval_assignments_dev": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p,
                                                ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
-    "pf_device_program": (ctypes.c_int, [_u32p, _sz, _u32p, _sz, _u32p, ctypes.POINTER(_sz), _u32p]),
+    "pf_device_program": (ctypes.c_int, [_u32p, _sz, _u32p, _sz, _u32p, _sz, _u32p, ctypes.POINTER(_sz), _u32p]),
     "pf_keccak256_batch": (ctypes.c_int, [_u8p, _u64p, _sz, _u8p]),
     "pf_keccak256_fixed_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, _sz,
                                               ctypes.c_void_p, ctypes.POINTER(ctypes.c_float),

@@ -361,8 +361,25 @@ int check_collect(Batch* B, hipStream_t st, pf_stats* stats, std::vector<uint32_
 //     operand of W-reading instructions (not SPILL or MOV); those take the constant directly
 //     (PF_I_KA / PF_I_KB, the constant index in the register field, traffic bit cleared) and
 //     the kernel reads it with one scalar load.
+//     A constant is folded only when it fits the W_CONST's width: the W_CONST masks its value
+//     at write-back, a folded operand is read raw (ADVICE r4 — the lowering never packs a
+//     wider one, but pf_batch_create trusts nothing the caller packed).
+// consts (n_const x 8 u32, set-relative indices resolved through const_off) may be null: then
+// every constant is taken to fit (pf_device_program's callers that pass none).
+bool const_fits(const uint32_t* consts, size_t n_const, uint32_t idx, uint32_t w) {
+    if (!consts) return true;
+    if (idx >= n_const) return false;
+    const uint32_t* c = consts + 8 * (size_t)idx;
+    for (uint32_t j = 0; j < 8; j++) {
+        const uint32_t lo = 32u * j;
+        const uint32_t keep = w >= lo + 32u ? 0xffffffffu : (w > lo ? (1u << (w - lo)) - 1u : 0u);
+        if (c[j] & ~keep) return false;
+    }
+    return true;
+}
+
 void device_program(const std::vector<uint32_t>& code_fixed, std::vector<pf_set_desc>& descs_out,
-                    std::vector<uint32_t>& code_out) {
+                    std::vector<uint32_t>& code_out, const uint32_t* consts = nullptr, size_t n_const = 0) {
     code_out.clear();
     code_out.reserve(code_fixed.size());
     const size_t n_sets = descs_out.size();
@@ -487,7 +504,9 @@ void device_program(const std::vector<uint32_t>& code_fixed, std::vector<pf_set_
                 }
                 if ((tr & PF_TR_WW) && rd <= PF_NW) {
                     settle(rd);
-                    if (op == PF_W_CONST && P[4 * i + 2] <= 0xffu) pend[rd].at = i;
+                    if (op == PF_W_CONST && P[4 * i + 2] <= 0xffu &&
+                        const_fits(consts, n_const, d.const_off + P[4 * i + 2], (P[4 * i] >> 8) & 0x3ffu))
+                        pend[rd].at = i;
                 }
             }
             for (uint32_t r = 0; r <= PF_NW; r++) settle(r);
@@ -510,8 +529,9 @@ int pf_version(void) { return 2; }
 // Host only (no HIP call, tests/test_device_program.py): the program pf_batch_create would put
 // on the device — traffic / unit bits recomputed from the opcodes, then the peepholes.
 // code_out needs room for n_ins instructions (the peepholes only delete); descs_out n_sets.
-int pf_device_program(const uint32_t* code, size_t n_ins, const pf_set_desc* descs, size_t n_sets,
-                      uint32_t* code_out, size_t* n_ins_out, pf_set_desc* descs_out) {
+int pf_device_program(const uint32_t* code, size_t n_ins, const uint32_t* consts, size_t n_const,
+                      const pf_set_desc* descs, size_t n_sets, uint32_t* code_out, size_t* n_ins_out,
+                      pf_set_desc* descs_out) {
     std::vector<uint32_t> fixed(code, code + 4 * n_ins);
     for (size_t i = 0; i < n_ins; i++) {
         uint32_t* I = fixed.data() + 4 * i;
@@ -520,7 +540,7 @@ int pf_device_program(const uint32_t* code, size_t n_ins, const pf_set_desc* des
     }
     std::vector<pf_set_desc> d(descs, descs + n_sets);
     std::vector<uint32_t> out;
-    device_program(fixed, d, out);
+    device_program(fixed, d, out, consts, n_const);
     memcpy(code_out, out.data(), out.size() * 4);
     *n_ins_out = out.size() / 4;
     memcpy(descs_out, d.data(), n_sets * sizeof(pf_set_desc));
@@ -695,7 +715,7 @@ int pf_batch_create_on(int device, const uint32_t* code, size_t n_ins, const uin
     }
     std::vector<uint32_t> code_out;
     std::vector<pf_set_desc> descs_out(descs, descs + n_sets);
-    device_program(code_fixed, descs_out, code_out);
+    device_program(code_fixed, descs_out, code_out, consts, n_const);
     code = code_out.data();
     n_ins = code_out.size() / 4;
     descs = descs_out.data();
@@ -924,13 +944,21 @@ int pf_materialize(uint64_t handle, uint64_t global_seed, const uint32_t* set_id
             rc = -1;
     }
     if (!rc && pin) memcpy(values_out, pin, total * 32);
-    // back to the pool (the stream is drained, or the launch failed)
+    if (rc) {
+        // a failed copy or synchronisation after the copy-in may leave work on the stream
+        // that still reads or writes the block: it is not pooled again — freed
+        // after a full device synchronisation (whose own failure leaks it rather than hand
+        // memory in use to the next pool_acquire)
+        if (hipDeviceSynchronize() == hipSuccess) hipFree(dm);
+        return fail("pf_materialize: HIP call failed");
+    }
+    // back to the pool (the stream is drained)
     if (D->pool.size() >= kPoolBlocks) {
         hipFree(D->pool.front().first);
         D->pool.erase(D->pool.begin());
     }
     D->pool.emplace_back(dm, cap);
-    return rc ? fail("pf_materialize: HIP call failed") : 0;
+    return 0;
 }
 
 static int eval_launch(Batch* B, uint32_t set, const uint32_t* d_soa, uint32_t n_cand,

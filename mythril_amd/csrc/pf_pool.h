@@ -4,7 +4,14 @@
 // a thread creation and join per call (std::thread per call was ~20-40 us each — as long as
 // lowering a small bucket).  Host-only C++; the pool is never destroyed (its detached workers
 // would otherwise wait on a destroyed condition variable at process exit).
+// fork(): the child has none of the parent's workers, and the pool's mutexes may have been
+// held by a parent thread at the fork — so a pthread_atfork child handler gives the child a
+// fresh pool (the parent's is left untouched: its state is garbage in the child).  Without it
+// a child of a process that had used the pool waited forever on busy_ for workers that do
+// not exist (tools/full_pass.py's default-fork ProcessPoolExecutor).
 #pragma once
+
+#include <pthread.h>
 
 #include <atomic>
 #include <condition_variable>
@@ -76,9 +83,15 @@ class Pool {
     std::atomic<size_t> next_{0};
 };
 
-inline Pool& pool() {
+inline Pool*& pool_ptr() {
     static Pool* p = new Pool();  // never destroyed (see above)
-    return *p;
+    return p;
+}
+
+inline Pool& pool() {
+    static const int registered = pthread_atfork(nullptr, nullptr, [] { pool_ptr() = new Pool(); });
+    (void)registered;
+    return *pool_ptr();
 }
 
 inline void parallel_for(size_t n, size_t n_threads, const std::function<void(size_t)>& fn) {

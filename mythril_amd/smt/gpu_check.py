@@ -182,13 +182,14 @@ def _recent_parent(bucket: List[T.Term]) -> Optional[dict]:
     if _native_batch():
         from . import native_terms
 
-        h = native_terms.recent_parent_handle(bucket)
+        st = native_terms.batch_api()   # one store for the handle's whole life
+        h = native_terms.recent_parent_handle(bucket, st)
         if h is None:
             return None
         try:
-            return native_terms.parent_dict(h)
+            return native_terms.parent_dict(h, st)
         finally:
-            native_terms.free_parent(h)
+            native_terms.free_parent(h, st)
 
     keys = set()
     for c in bucket:
@@ -384,11 +385,16 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
     reg_sig = tuple(sorted((n, s.lo, len(s.concrete)) for n, s in reg.keccak.items()))
     jobs, job_keys, pending = [], [], set()
     nat = _native_batch()
+    st = None
     if nat:
         from . import native_terms
 
         if native_terms.new_generation(cfg.store_limit):
             reset_cache()   # cached witnesses hold results of the retired store
+        # this call's store, pinned: another thread's check_sets may retire the process's
+        # store (new_generation) while this one holds parent handles whose read keys are
+        # this store's term ids — every handle is made, lowered against and freed here
+        st = native_terms.batch_api()
     phases: Dict[str, float] = {}
     tp = [t0]
 
@@ -434,10 +440,10 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
                 # parent handles: the caller's model, or the store's recent values now (cache
                 # hits above recorded theirs first, as _note_witness does)
                 if parent is not None:
-                    with native_terms.store().lock:
-                        bp = (native_terms._parent_handle(native_terms.store(), parent), bool(parent))
+                    with st.lock:
+                        bp = (native_terms._parent_handle(st, parent), bool(parent))
                 elif cfg.parents:
-                    h = native_terms.recent_parent_handle(b)
+                    h = native_terms.recent_parent_handle(b, st)
                     bp = (h, h is not None)
                 else:
                     bp = (None, False)
@@ -454,10 +460,10 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
         try:
             lowered_all = native_terms.lower_many(
                 [(b, h) for b, (h, _) in jobs], reg, cfg.hints, [_set_seed(b) for b, _ in jobs],
-                _host_threads(cfg, len(jobs)))
+                _host_threads(cfg, len(jobs)), st=st)
         finally:
             for _, (h, _) in jobs:
-                native_terms.free_parent(h)
+                native_terms.free_parent(h, st)
     else:
         job_parent = {k: bool(j[1]) for k, j in zip(job_keys, jobs)}
         lowered_all = _lower_all(jobs, reg, cfg)

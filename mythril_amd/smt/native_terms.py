@@ -543,18 +543,23 @@ def _parent_handle(st: TermStore, parent: dict):
                                 prv.ctypes.data_as(_u32p), npr)
 
 
-def recent_parent_handle(bucket: List[T.Term]):
+def recent_parent_handle(bucket: List[T.Term], st: Optional[TermStore] = None):
     """The bucket's parent model from the store's recent values (pflt_recent_parent), as a
-    handle for lower_many, or None when no value is known (gpu_check._recent_parent)."""
-    st = batch_api()
+    handle for lower_many, or None when no value is known (gpu_check._recent_parent).
+
+    ``st``: the store the caller pinned for its whole call: a handle's read keys
+    are that store's term ids, so the handle must be read (parent_dict), lowered against
+    (lower_many) and freed with the same store even if new_generation retires it meanwhile."""
+    st = st or batch_api()
     with st.lock:
         roots = np.array([st.export(c) for c in bucket] or [0], dtype=np.uint32)
         return st.L.pflt_recent_parent(st.h, roots.ctypes.data_as(_u32p), len(bucket)) or None
 
 
-def parent_dict(h) -> dict:
-    """A parent handle as gpu_check's parent dict (names -> value, select term -> value)."""
-    st = batch_api()
+def parent_dict(h, st: Optional[TermStore] = None) -> dict:
+    """A parent handle as gpu_check's parent dict (names -> value, select term -> value);
+    ``st`` = the store the handle was made from (recent_parent_handle)."""
+    st = st or batch_api()
     info = (ctypes.c_uint64 * 4)()
     st.L.pflt_parent_info(h, info)
     nn, nb, nw, nr = (int(x) for x in info)
@@ -575,9 +580,9 @@ def parent_dict(h) -> dict:
     return out
 
 
-def free_parent(h) -> None:
+def free_parent(h, st: Optional[TermStore] = None) -> None:
     if h:
-        batch_api().L.pflt_parent_free(h)
+        (st or batch_api()).L.pflt_parent_free(h)
 
 
 def note_vars(vals: Dict[str, int], recent_size: int) -> None:
@@ -621,10 +626,12 @@ _JOB = np.dtype([("roots", "<u8"), ("n", "<u8"), ("parents", "<u8"), ("flags", "
 
 
 def lower_many(jobs: List[Tuple[List[T.Term], object]], reg: UFRegistry, hints: bool, seeds: List[int],
-               threads: int) -> list:
+               threads: int, st: Optional[TermStore] = None, flags: Optional[int] = None) -> list:
     """[(bucket, parent handle or None)] -> [(NativeLowered, NativeProgram, None) or
-    (None, None, error)], lowered concurrently on ``threads`` host threads."""
-    st = batch_api()
+    (None, None, error)], lowered concurrently on ``threads`` host threads.  ``st``: the
+    store the parent handles were made from (the caller's pinned store); ``flags``: the
+    pflt_lower flags (default PROGRAM, plus HINTS when ``hints``)."""
+    st = st or batch_api()
     n = len(jobs)
     if n == 0:
         return []
@@ -642,7 +649,7 @@ def lower_many(jobs: List[Tuple[List[T.Term], object]], reg: UFRegistry, hints: 
         arr["roots"] = roots.ctypes.data + 4 * offs
         arr["n"] = lens
         arr["parents"] = [h or 0 for _, h in jobs]
-        arr["flags"] = PROGRAM | (HINTS if hints else 0)
+        arr["flags"] = flags if flags is not None else PROGRAM | (HINTS if hints else 0)
         arr["seed"] = np.array(seeds, dtype=np.uint64) & 0xFFFFFFFF
         regb = _registry_blob(reg)
         res = (ctypes.c_void_p * n)()

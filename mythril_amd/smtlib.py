@@ -107,6 +107,10 @@ _OVFL = {
 }
 
 
+_EVAL, _LET, _RESTORE, _APPLY = range(4)
+_UNBOUND = object()
+
+
 class Reader:
     def __init__(self):
         self.q = Query()
@@ -143,26 +147,67 @@ class Reader:
 
     # ---- terms ---------------------------------------------------------------------------
     def term(self, e, env: Dict[str, T.Term]) -> T.Term:
-        if isinstance(e, str):
-            return self._atom(e, env)
-        head = e[0]
-        if head == "_" and len(e) == 3 and e[1].startswith("bv") and e[1][2:].isdigit():
-            return T.const(int(e[1][2:]), int(e[2]))  # (_ bvN w) literal
-        if head == "let":
-            env2 = dict(env)
-            for binding in e[1]:
-                env2[_sym(binding[0])] = self.term(binding[1], env)  # parallel let
-            return self.term(e[2], env2)
-        if isinstance(head, list):
-            return self._indexed(head, [self.term(a, env) for a in e[1:]])
-        args = [self.term(a, env) for a in e[1:]]
-        h = _sym(head)
-        if h in self.funs:
-            doms, rng = self.funs[h]
-            if rng[0] != "bv":
-                raise LoweringError(f"smtlib: UF {h} with range {rng}")
-            return T.apply(h, rng[1], *args)
-        return apply_named(h, args)
+        """One s-expression as a term, without recursion: z3 prints every shared subterm as a
+        nested ``let`` (``a!1`` …), so a large dump nests thousands deep.  An explicit work
+        stack evaluates it on the caller's thread at any depth (the recursive
+        reader had to re-run on a big-stack thread under a raised process-wide recursion
+        limit, which made deep recursion on other threads segfault meanwhile).
+
+        ``let`` is parallel (the bindings see the outer scope) and scoped: the bound names
+        are set in one mutable environment for the body and restored after it."""
+        env = dict(env)
+        vals: List[T.Term] = []
+        work: list = [(_EVAL, e)]
+        while work:
+            kind, x = work.pop()
+            if kind == _EVAL:
+                if isinstance(x, str):
+                    vals.append(self._atom(x, env))
+                    continue
+                head = x[0]
+                if head == "_" and len(x) == 3 and x[1].startswith("bv") and x[1][2:].isdigit():
+                    vals.append(T.const(int(x[1][2:]), int(x[2])))  # (_ bvN w) literal
+                    continue
+                if head == "let":
+                    work.append((_LET, x))
+                    for binding in reversed(x[1]):
+                        work.append((_EVAL, binding[1]))
+                    continue
+                work.append((_APPLY, x))
+                for a in reversed(x[1:]):
+                    work.append((_EVAL, a))
+            elif kind == _LET:          # the bindings' values are on the stack: the body
+                names = [_sym(b[0]) for b in x[1]]
+                bound = vals[len(vals) - len(names):]
+                del vals[len(vals) - len(names):]
+                undo = [(nm, env.get(nm, _UNBOUND)) for nm in names]
+                for nm, v in zip(names, bound):
+                    env[nm] = v
+                work.append((_RESTORE, undo))
+                work.append((_EVAL, x[2]))
+            elif kind == _RESTORE:      # leave the let's scope
+                for nm, old in reversed(x):
+                    if old is _UNBOUND:
+                        env.pop(nm, None)
+                    else:
+                        env[nm] = old
+            else:                       # _APPLY: the arguments are on the stack
+                n = len(x) - 1
+                args = vals[len(vals) - n:] if n else []
+                del vals[len(vals) - n:]
+                head = x[0]
+                if isinstance(head, list):
+                    vals.append(self._indexed(head, args))
+                    continue
+                h = _sym(head)
+                if h in self.funs:
+                    doms, rng = self.funs[h]
+                    if rng[0] != "bv":
+                        raise LoweringError(f"smtlib: UF {h} with range {rng}")
+                    vals.append(T.apply(h, rng[1], *args))
+                else:
+                    vals.append(apply_named(h, args))
+        return vals[0]
 
     def _atom(self, tok: str, env) -> T.Term:
         s = _sym(tok)
@@ -290,40 +335,8 @@ def apply_indexed(op: str, params: List[int], args: List[T.Term]) -> T.Term:
 
 def read_query(text: str) -> Query:
     """One --solver-log query.  z3 prints shared subterms as nested ``let`` bindings, so a
-    large dump nests thousands deep: past Python's recursion limit the reader runs again on
-    a thread with a 512 MiB stack and a raised limit."""
-    try:
-        return Reader().read(text)
-    except RecursionError:
-        return _on_deep_stack(lambda: Reader().read(text))
-
-
-def _on_deep_stack(fn):
-    import sys
-    import threading
-
-    out = {}
-
-    def run():
-        old = sys.getrecursionlimit()
-        sys.setrecursionlimit(max(old, 1_000_000))
-        try:
-            out["r"] = fn()
-        except BaseException as e:  # re-raised on the caller's thread
-            out["e"] = e
-        finally:
-            sys.setrecursionlimit(old)
-
-    prev = threading.stack_size(512 << 20)
-    try:
-        th = threading.Thread(target=run, name="smtlib-deep")
-        th.start()
-    finally:
-        threading.stack_size(prev)
-    th.join()
-    if "e" in out:
-        raise out["e"]
-    return out["r"]
+    large dump nests thousands deep: the reader's term walk is iterative (Reader.term)."""
+    return Reader().read(text)
 
 
 def read_file(path: str) -> Query:

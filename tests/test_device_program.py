@@ -26,7 +26,10 @@ def device_program(batch):
     out = np.zeros_like(code)
     dout = np.zeros_like(descs)
     n = ctypes.c_size_t()
-    _lib.check(L.pf_device_program(_lib.ptr_u32(code), len(code), _lib.ptr_u32(descs), len(descs),
+    consts = np.ascontiguousarray(batch.consts, dtype=np.uint32)
+    _lib.check(L.pf_device_program(_lib.ptr_u32(code), len(code),
+                                   _lib.ptr_u32(consts.reshape(-1)) if consts.size else None, len(consts),
+                                   _lib.ptr_u32(descs), len(descs),
                                    _lib.ptr_u32(out), ctypes.byref(n), _lib.ptr_u32(dout)),
                "pf_device_program")
     return out[:n.value], dout
@@ -155,3 +158,41 @@ def test_device_program_matches_the_lowered_program(monkeypatch):
         cands = sv.gen_assignments(np.arange(24, dtype=np.uint64), 5)
         for vals in cands + [[rng.getrandbits(sv.var_width(v)) for v in range(len(sv.schema))]]:
             assert eval_device(sv, rows, vals) == sv.evaluate(vals), s
+
+
+def test_out_of_width_constant_is_not_folded(monkeypatch):
+    """a W_CONST masks its constant to its width at write-back, a folded operand
+    (PF_I_KA / PF_I_KB) reads it raw — so a constant wider than its W_CONST stays a W_CONST,
+    and the device program still computes what the lowered one does."""
+    batch = ir.Batch(_programs(monkeypatch))     # corpus buckets carry narrow constants
+    code0, descs0 = device_program(batch)
+
+    def n_wconst(code, descs, s):
+        d = descs[s]
+        return int(((code[d[0]:d[0] + d[1], 0] & 0xFF) == ir.W_CONST).sum())
+
+    tried = kept = 0
+    for s, d in enumerate(batch.descs):
+        for i in range(d[0], d[0] + d[1]):
+            w0 = int(batch.code[i, 0])
+            if w0 & 0xFF != ir.W_CONST or ((w0 >> 8) & 0x3FF) >= 224:
+                continue
+            k = int(d[2]) + int(batch.code[i, 2])
+            saved = int(batch.consts[k, 7])
+            batch.consts[k, 7] = saved | 0x80000000      # bit 255: outside any width < 224
+            code1, descs1 = device_program(batch)
+            tried += 1
+            # folded before (the W_CONST was deleted) -> kept now
+            if n_wconst(code1, descs1, s) == n_wconst(code0, descs0, s) + 1:
+                kept += 1
+            sv = O.SetView.from_batch(batch, s)
+            e = descs1[s]
+            rows = [tuple(int(x) for x in r) for r in code1[e[0]:e[0] + e[1]]]
+            for vals in sv.gen_assignments(np.arange(16, dtype=np.uint64), 9):
+                assert eval_device(sv, rows, vals) == sv.evaluate(vals)
+            batch.consts[k, 7] = saved
+            if tried >= 12:
+                break
+        if tried >= 12:
+            break
+    assert tried > 0 and kept > 0, (tried, kept)

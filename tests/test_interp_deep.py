@@ -77,11 +77,11 @@ def test_smtlib_reader_deep_let_chain():
     for i in range(depth):
         body = f"(let ((a!{i} (bvadd {body} #x{(i % 251):064x}))) a!{i})"
     text = f"(declare-fun x () (_ BitVec 256))\n(assert (= {body} #x{0:064x}))\n(check-sat)\n"
-    import pytest
-
-    with pytest.raises(RecursionError):   # the recursive reader alone cannot take it
-        smtlib.Reader().read(text)
+    # the reader walks the nesting iteratively, on the caller's thread, with the process's
+    # recursion limit untouched
+    limit = sys.getrecursionlimit()
     q = smtlib.read_query(text)
+    assert sys.getrecursionlimit() == limit
     assert len(q.assertions) == 1
     want = (-sum(i % 251 for i in range(depth))) % (1 << 256)
     assert _eval({"x": want}).ev(q.assertions[0])

@@ -227,3 +227,26 @@ def test_candidate_zero_witnesses_are_not_materialised(small_corpus, monkeypatch
     for a, b in zip(nat, py):
         if a is not None:
             assert a.w.vars == b.w.vars
+
+
+def test_worker_pool_survives_fork(small_corpus):
+    """a forked child of a process that used the persistent worker pool (the
+    default fork context of tools/full_pass.py's ProcessPoolExecutor) lowers on host threads
+    too — it gets a fresh pool instead of waiting for the parent's workers, which it lacks."""
+    import os
+    import signal
+
+    c, bks = small_corpus
+    reg = c.kfm.registry
+    jobs = [(b, None) for b in bks[:24]]
+    NT.lower_many(jobs, reg, True, [3] * len(jobs), 8)      # the parent's pool is running
+    pid = os.fork()
+    if pid == 0:   # child: the same call, bounded by an alarm
+        signal.alarm(60)
+        try:
+            out = NT.lower_many(jobs, reg, True, [3] * len(jobs), 8)
+            os._exit(0 if len(out) == len(jobs) else 2)
+        except BaseException:
+            os._exit(3)
+    _, status = os.waitpid(pid, 0)
+    assert os.WIFEXITED(status) and os.WEXITSTATUS(status) == 0, status

@@ -430,3 +430,37 @@ def test_store_generation_retires_and_results_keep_their_store(monkeypatch):
     assert new is not old and lo_old.res.st is old
     assert native_terms.recheck_many([lo_old], np.asarray(ir.limbs_array([m1.w.vars["gen_x"]])),
                                      gpu_check.DEFAULT_REGISTRY, 1).tolist() == [1]
+
+
+def test_parent_handle_survives_store_retirement(monkeypatch):
+    """a parent handle is made, read and lowered against with the store the caller
+    pinned, even when another thread's call retires the process's store in between (its
+    read keys are the old store's term ids)."""
+    from mythril_amd.smt import native_terms
+    from mythril_amd.smt import terms as T
+
+    if native_terms.batch_api() is None:
+        pytest.skip("libpflower.so not built")
+    oracle_engine.install(monkeypatch)
+    from dataclasses import replace
+
+    from mythril_amd.smt import ULT, symbol_factory
+
+    x = symbol_factory.BitVecSym("ret_x", 256)
+    arr = T.array("ret_storage", 256, 256)
+    sel = T.select(arr, T.const(7, 256))
+    q = [ULT(x, symbol_factory.BitVecVal(10, 256)).raw, T.eq(T.const(5, 256), sel)]
+    cfg = replace(gpu_check.CONFIG, budget=256)
+    assert gpu_check.check_sets([q], config=cfg)[0] is not None   # notes ret_x and the read
+    st = native_terms.batch_api()
+    h = native_terms.recent_parent_handle(q, st)
+    assert h is not None
+    # another caller retires the store now
+    assert native_terms.new_generation(1)
+    assert native_terms.batch_api() is not st
+    par = native_terms.parent_dict(h, st)
+    assert par.get(sel) == 5 and "ret_x" in par
+    out = native_terms.lower_many([(q, h)], gpu_check.DEFAULT_REGISTRY, True, [1], 1, st=st)
+    native_terms.free_parent(h, st)
+    lo, prog, err = out[0]
+    assert err is None and lo.res.st is st
