@@ -51,6 +51,14 @@ typedef struct pf_stats {
  * is the default one (pf_batch_create, Keccak).  One process can drive every GPU of a node
  * this way (Mythril's analysis is one process); one process per GPU passes one bit.      */
 int pf_init(uint64_t device_mask);
+/* Add one execution context per entry of devices[]: its own library stream, device-block pool
+ * and events on that HIP device — the same device may appear several times.  ctx_out[i]
+ * receives the context's id (>= PF_CONTEXT_BASE), usable wherever an entry point takes a
+ * device (pf_batch_create_on; batches remember it).  A node's split
+ * (pf_check_batches over one batch per context) can so run with two contexts on one GPU:
+ * the same code path as two GPUs, each context's launches on its own stream.           */
+#define PF_CONTEXT_BASE 64
+int pf_init_contexts(const int32_t* devices, size_t n, int32_t* ctx_out);
 int pf_shutdown(void);
 const char* pf_last_error(void);
 int pf_version(void);               /* ABI version                                         */

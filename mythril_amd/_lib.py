@@ -43,6 +43,7 @@ _sz = ctypes.c_size_t
 # name -> (restype, argtypes); kept in sync with include/pathfeas.h (tests/test_abi.py)
 SIGNATURES = {
     "pf_init": (ctypes.c_int, [ctypes.c_uint64]),
+    "pf_init_contexts": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int32), _sz, ctypes.POINTER(ctypes.c_int32)]),
     "pf_shutdown": (ctypes.c_int, []),
     "pf_last_error": (ctypes.c_char_p, []),
     "pf_version": (ctypes.c_int, []),
@@ -138,6 +139,21 @@ def init(devices=0) -> None:
         mask |= 1 << d
     check(L.pf_init(mask), f"pf_init({devs})")
     _initialised.update(devs)
+
+
+def init_contexts(devices) -> list:
+    """One execution context per entry of ``devices`` (repeats allowed: two contexts on one
+    GPU, each with its own stream — pf_init_contexts); returns their ids, which stand in for
+    device indices wherever the engine names a device."""
+    devs = [int(d) for d in devices]
+    L = lib()
+    n = L.pf_device_count()
+    if n <= 0:
+        raise PathFeasError("no HIP device visible: the MI355X path-feasibility engine has no CPU fallback")
+    arr = (ctypes.c_int32 * len(devs))(*devs)
+    out = (ctypes.c_int32 * len(devs))()
+    check(L.pf_init_contexts(arr, len(devs), out), f"pf_init_contexts({devs})")
+    return list(out)
 
 
 def ptr_u32(a: np.ndarray):

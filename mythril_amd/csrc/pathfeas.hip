@@ -29,7 +29,9 @@ std::string g_err;
 // the Keccak launches and the launch geometry inputs.  Batches live on one device each and
 // carry their own counters and events, so launches of different batches never share scratch.
 struct Dev {
-    int id = -1;
+    int id = -1;            // the HIP device
+    int key = -1;           // what the API calls it: the device id (pf_init) or a context id
+                            // >= PF_CONTEXT_BASE (pf_init_contexts: several per device)
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     int num_cus = 256;
@@ -116,9 +118,9 @@ struct DevBuf {
     T* as() { return static_cast<T*>(p); }
 };
 
-Dev* find_dev(int id) {
+Dev* find_dev(int key) {
     for (auto& d : g_devs)
-        if (d.id == id) return &d;
+        if (d.key == key) return &d;
     return nullptr;
 }
 
@@ -603,14 +605,44 @@ int pf_init(uint64_t device_mask) {
         if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
             return fail("pf_init: device %d is %s, this build targets gfx950", id, prop.gcnArchName);
         Dev D;
-        D.id = id;
+        D.id = D.key = id;
         D.num_cus = prop.multiProcessorCount;
         HIPCHK(hipStreamCreateWithFlags(&D.stream, hipStreamNonBlocking));
         HIPCHK(hipEventCreate(&D.ev0));
         HIPCHK(hipEventCreate(&D.ev1));
         g_devs.push_back(D);
     }
-    std::sort(g_devs.begin(), g_devs.end(), [](const Dev& a, const Dev& b) { return a.id < b.id; });
+    std::sort(g_devs.begin(), g_devs.end(), [](const Dev& a, const Dev& b) { return a.key < b.key; });
+    g_default = 0;
+    return 0;
+}
+
+int pf_init_contexts(const int32_t* devices, size_t n, int32_t* ctx_out) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    int nd = 0;
+    HIPCHK(hipGetDeviceCount(&nd));
+    if (!devices || !ctx_out || n == 0) return fail("pf_init_contexts: no devices");
+    int next = PF_CONTEXT_BASE;
+    for (const Dev& D : g_devs) next = std::max(next, D.key + 1);
+    for (size_t i = 0; i < n; ++i) {
+        const int id = devices[i];
+        if (id < 0 || id >= nd) return fail("pf_init_contexts: device %d of %d visible", id, nd);
+        HIPCHK(hipSetDevice(id));
+        hipDeviceProp_t prop;
+        HIPCHK(hipGetDeviceProperties(&prop, id));
+        if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+            return fail("pf_init_contexts: device %d is %s, this build targets gfx950", id, prop.gcnArchName);
+        Dev D;
+        D.id = id;
+        D.key = next++;
+        D.num_cus = prop.multiProcessorCount;
+        HIPCHK(hipStreamCreateWithFlags(&D.stream, hipStreamNonBlocking));
+        HIPCHK(hipEventCreate(&D.ev0));
+        HIPCHK(hipEventCreate(&D.ev1));
+        g_devs.push_back(D);
+        ctx_out[i] = D.key;
+    }
+    std::sort(g_devs.begin(), g_devs.end(), [](const Dev& a, const Dev& b) { return a.key < b.key; });
     g_default = 0;
     return 0;
 }
@@ -763,7 +795,7 @@ int pf_batch_create_on(int device, const uint32_t* code, size_t n_ins, const uin
     put(o_order, order.data(), n_sets * 4);
 
     Batch* B = new Batch();
-    B->device = Dv->id;
+    B->device = Dv->key;
     B->n_ins = n_ins;
     B->n_const = n_const;
     B->n_vars = n_vars;

@@ -82,7 +82,12 @@ class Engine:
 
     def __init__(self, device: int = 0, devices: Optional[Sequence[int]] = None):
         self.devices = list(devices) if devices is not None else [device]
-        _lib.init(self.devices)
+        if len(set(self.devices)) < len(self.devices):
+            # a device named twice: one execution context (own stream) per entry, so the
+            # node split (upload_sharded + check_many) runs its multi-device path on one GPU
+            self.devices = _lib.init_contexts(self.devices)
+        else:
+            _lib.init(self.devices)
         self.device = self.devices[0]
 
     # ---- search -------------------------------------------------------------------
@@ -217,7 +222,8 @@ _engine: Optional[Engine] = None
 def get_engine(device: Optional[int] = None) -> Engine:
     """The process's engine.  Device selection: an explicit ``device``; else ``PF_DEVICES``
     (comma-separated indices, or ``all``: one process driving every visible GPU — the live
-    analysis, which Mythril runs as one process); else ``LOCAL_RANK`` (one process per GPU)."""
+    analysis, which Mythril runs as one process; an index named twice, e.g. ``0,0``, makes two
+    execution contexts on that GPU); else ``LOCAL_RANK`` (one process per GPU)."""
     global _engine
     if _engine is None:
         import os

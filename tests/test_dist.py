@@ -78,3 +78,35 @@ def test_two_rank_gather_matches_single_process(tmp_path):
         want.append(NOT_FOUND if first is None else first)
     assert list(f0) == want
     assert (f0[::3] == 0).all()  # planted witnesses are candidate 0
+
+
+def _gather_worker(rank, world, port, out_path):
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mythril_amd.dist import gather_found
+
+    res = []
+    for sizes in ((7, 2), (9, 0), (0, 4)):
+        lo = sum(sizes[:rank])
+        mine = np.array([(lo + i) * 3 if (lo + i) % 2 else NOT_FOUND for i in range(sizes[rank])],
+                        dtype=np.uint32)
+        res.append(gather_found(mine, lo, sum(sizes)))
+    np.save(f"{out_path}.{rank}.npy", np.concatenate(res))
+    dist.destroy_process_group()
+
+
+def test_gather_sends_shards_of_any_length(tmp_path):
+    """gather_found all-gathers each rank's own shard (padded to the longest), not a
+    full-length array per rank: uneven and empty shards reassemble into the global verdicts,
+    u32 values above 2^31 included."""
+    port = _free_port()
+    out = str(tmp_path / "g")
+    mp.spawn(_gather_worker, args=(2, port, out), nprocs=2, join=True)
+    g0, g1 = np.load(out + ".0.npy"), np.load(out + ".1.npy")
+    assert (g0 == g1).all()
+    want = np.concatenate([np.array([i * 3 if i % 2 else NOT_FOUND for i in range(n)], dtype=np.uint32)
+                           for n in (9, 9, 4)])
+    assert (g0 == want).all()

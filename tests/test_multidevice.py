@@ -185,3 +185,54 @@ def test_plugin_batch_spreads_over_all_visible_devices(monkeypatch):
     assert all(s.constraints.is_possible() for s in states)
     monkeypatch.setattr(E, "_engine", None)
     gpu_check.reset_cache()
+
+
+@pytest.mark.gpu
+def test_gpu_two_contexts_on_one_device(engine, monkeypatch):
+    """The node split as it runs on a multi-GPU box, on the one visible GPU: the device named
+    twice (PF_DEVICES=0,0) makes two execution contexts (pf_init_contexts), each with its own
+    stream.  upload_sharded cuts the batch into two cost-balanced shards, one per context,
+    pf_check_batches enqueues both before reading either, and the gathered verdicts equal the
+    single-context search — bare programs and check_sets' whole pipeline alike."""
+    progs = _progs(160, first=900, plant=False)
+    flags = ir.FLAG_EARLY_EXIT | ir.FLAG_SHORTCIRCUIT
+    one = E.Engine(devices=[0])
+    whole = one.upload(progs)
+    r1 = one.check(whole, budget=8192, seed=0, flags=flags)
+    two = E.Engine(devices=[0, 0])
+    assert len(two.devices) == 2 and len(set(two.devices)) == 2 and min(two.devices) >= 64
+    dbs = two.upload_sharded(progs)
+    assert len(dbs) == 2 and sum(len(d) for d in dbs) == len(progs)
+    assert [d.device for d in dbs] == two.devices
+    r2 = two.check_many(dbs, budget=8192, seed=0, flags=flags)
+    assert np.array_equal(r1.found, r2.found)
+    # the witnesses materialise from either context's batch
+    sat = [k for k in range(len(progs)) if r2.found[k] != E.NOT_FOUND]
+    assert sat
+    k0 = sat[0]
+    base = 0 if k0 < len(dbs[0]) else len(dbs[0])
+    db = dbs[0] if k0 < len(dbs[0]) else dbs[1]
+    assert two.materialize(db, [k0 - base], [int(r2.found[k0])]) == \
+        one.materialize(whole, [k0], [int(r1.found[k0])])
+    for d in dbs + [whole]:
+        d.free()
+    # check_sets through an engine of two contexts: the same answers as through one
+    import pyoracle as O
+    from mythril_amd import corpus
+    from mythril_amd import keccak_manager as KM
+    from mythril_amd.smt import symbol_factory
+
+    monkeypatch.setattr(KM.KeccakFunctionManager, "find_concrete_keccak", staticmethod(
+        lambda data: symbol_factory.BitVecVal(
+            int.from_bytes(O.keccak256(data.value.to_bytes(data.size() // 8, "big")), "big"), 256)))
+    c = corpus.build(6, 2, seed=7)
+    sets = [q.constraints for q in c.queries][:80]
+    answers = {}
+    for name, eng in (("one", one), ("two", two)):
+        monkeypatch.setattr(E, "get_engine", lambda device=None, eng=eng: eng)
+        gpu_check.reset_cache()
+        ms = gpu_check.check_sets(sets, registry=c.kfm.registry)
+        answers[name] = [None if m is None else sorted(m.w.vars.items()) for m in ms]
+    assert answers["one"] == answers["two"]
+    assert any(a is not None for a in answers["one"])
+    gpu_check.reset_cache()
