@@ -54,6 +54,8 @@ def parse(argv=None):
                     help="one waited pf_check_batch call per step instead of all K enqueued at once")
     ap.add_argument("--corpus-scenarios", type=int, default=48,
                     help="LASER-shaped scenarios for the %% discharged half of the metric (0 = skip)")
+    ap.add_argument("--quick-sat-queries", type=int, default=120,
+                    help="queries of the quick-sat (100 cached models) and funnel legs (0 = skip)")
     return ap.parse_args(argv)
 
 
@@ -218,6 +220,26 @@ def discharge(args):
             "queries_per_s_terms_known": n / max(t_rep, 1e-9), "phase_s_terms_known": phase_rep,
             "corpus": f"mythril_amd/corpus.py, {args.corpus_scenarios} planted 2-tx scenarios "
                       f"(config-2 substitute: no z3/solc for --solver-log dumps)"}
+
+
+def quick_sat_leg(args):
+    """The quick-sat loop before every objective-free query (support/model.py:95-98,
+    support_utils.py:57-71) with 100 cached models — the reference loop (deep copy + eval per
+    model) vs the GPU-resident ModelCache (mythril_amd/model_cache.py), same models, same
+    queries, every choice compared — for a live-like cache of GPU witnesses and for a mixed
+    one (GPU witnesses, z3-shaped models, empty models); then the whole funnel's per-query
+    cost with the drop-in installed.  Runs in a Mythril-shaped process made of the test
+    stand-ins (tests/fake_z3.py, tests/mythril_standin.py: Mythril and z3 are absent here),
+    so z3's own eval / simplify costs are the stand-in's, not libz3's."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import model_cache_workload as W
+
+    n = args.quick_sat_queries
+    gc.collect()
+    return {"witness_cache": W.quick_sat_profile(n_models=100, n_scenarios=24, n_queries=n,
+                                                 gpu_frac=1.0, empty_frac=0.0),
+            "mixed_cache": W.quick_sat_profile(n_models=100, n_scenarios=16, n_queries=n),
+            "funnel": W.funnel_profile(n_scenarios=16, n_queries=2 * n)}
 
 
 # SURVEY.md §8(d): Keccak-f[1600] = 6,500 int32 ops per permutation; a 64-byte key||slot
@@ -512,6 +534,8 @@ def run(args, rank, world, local, dist, engine=None, cdev="cuda"):
                 line["keccak"]["cpu_baseline"] = coracle_py.keccak_baseline(64, 5.0)
         if args.corpus_scenarios > 0:
             line["discharge"] = discharge(args)
+        if args.quick_sat_queries > 0:
+            line["quick_sat"] = quick_sat_leg(args)
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(step_progs[args.warmup], args.budget, args.seed,
                                                 args.cpu_sample_s)

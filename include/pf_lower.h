@@ -114,6 +114,8 @@ int pfl_version(void);
 /* pflt_lower flags */
 #define PFLT_HINTS 1u    /* derive the hint model (seed.apply_hints) */
 #define PFLT_PROGRAM 2u  /* allocate registers and emit (lower.lower) */
+#define PFLT_EXPLICIT 4u /* explicit-model lowering (to_dag.ExplicitLowering): every base-array
+                            read and UF application is a leaf variable (GPU-resident ModelCache) */
 /* pflt_result_get selectors */
 #define PFLT_GET_VARS 0
 #define PFLT_GET_VAR_TERMS 1
@@ -128,6 +130,9 @@ int pfl_version(void);
 #define PFLT_GET_IN_ROOTS 10  /* the bucket's conjuncts as given */
 
 void* pflt_store_new(void);
+/* optional pflt_lower modes this build has (PFLT_FEAT_*) */
+#define PFLT_FEAT_EXPLICIT 1u
+uint32_t pflt_features(void);
 void pflt_store_free(void* store);
 size_t pflt_store_size(void* store);
 int64_t pflt_add(void* store, uint32_t op, uint32_t sortk, uint32_t w1, uint32_t w2, const uint32_t* args,

@@ -1016,15 +1016,40 @@ int pf_eval_assignments(uint64_t handle, uint32_t set, const uint32_t* soa, uint
     const size_t nv = std::max<uint32_t>(B->h_descs[set].n_vars, 1u);
     const size_t bytes = nv * 8 * (size_t)n_cand * 4;
     if (switch_stream(D, st)) return -1;
-    DevBuf b_soa, b_out;
-    HIPCHK(hipMalloc(&b_soa.p, bytes));
-    HIPCHK(hipMalloc(&b_out.p, n_cand));
-    uint32_t* d_soa = b_soa.as<uint32_t>();
-    uint8_t* d_out = b_out.as<uint8_t>();
-    HIPCHK(hipMemcpyAsync(d_soa, soa, bytes, hipMemcpyHostToDevice, st));
-    if (eval_launch(B, set, d_soa, n_cand, d_out, st)) return -1;
-    HIPCHK(hipMemcpyAsync(sat_out, d_out, n_cand, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+    // one pooled block [assignments | verdicts] and the pinned staging buffer for both
+    // copies (the GPU-resident ModelCache calls this once per quick-sat query: no hipMalloc /
+    // hipFree, no pageable copies — pf_materialize's pattern)
+    const size_t o_out = (bytes + 255) & ~size_t(255), total = o_out + n_cand;
+    size_t cap = 0;
+    uint8_t* dm = static_cast<uint8_t*>(pool_acquire(D, total, &cap));
+    if (!dm) return fail("pf_eval_assignments: hipMalloc(%zu) failed", total);
+    uint32_t* d_soa = reinterpret_cast<uint32_t*>(dm);
+    uint8_t* d_out = dm + o_out;
+    uint8_t* pin = pinned_staging(std::max<size_t>(bytes, n_cand));
+    int rc = 0;
+    if (pin) memcpy(pin, soa, bytes);
+    if (hipMemcpyAsync(d_soa, pin ? static_cast<const void*>(pin) : static_cast<const void*>(soa), bytes,
+                       hipMemcpyHostToDevice, st) != hipSuccess)
+        rc = -1;
+    if (!rc && eval_launch(B, set, d_soa, n_cand, d_out, st)) rc = -1;
+    // the staging buffer is reused for the verdicts: the stream orders the copy after the
+    // kernel, which ran after the copy-in
+    if (!rc && (hipMemcpyAsync(pin ? static_cast<void*>(pin) : static_cast<void*>(sat_out), d_out, n_cand,
+                               hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipStreamSynchronize(st) != hipSuccess))
+        rc = -1;
+    if (!rc && pin) memcpy(sat_out, pin, n_cand);
+    if (rc) {
+        // work may still be in flight on the block: freed after a full synchronisation, never
+        // pooled (the pf_materialize rule)
+        if (hipDeviceSynchronize() == hipSuccess) hipFree(dm);
+        return fail("pf_eval_assignments: HIP call failed");
+    }
+    if (D->pool.size() >= kPoolBlocks) {
+        hipFree(D->pool.front().first);
+        D->pool.erase(D->pool.begin());
+    }
+    D->pool.emplace_back(dm, cap);
     return 0;
 }
 

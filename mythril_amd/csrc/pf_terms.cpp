@@ -540,6 +540,11 @@ struct Lowering {
     std::vector<uint32_t> uf_apps;   // app term ids, registration order
     std::vector<int32_t> side;
     bool actors_forced = false;
+    // explicit-model lowering (PFLT_EXPLICIT): leaves by (array, index) / by UF-application term
+    bool explicit_ = false;
+    std::map<std::pair<uint32_t, uint32_t>, int32_t> leaf_reads;
+    std::unordered_map<uint32_t, int32_t> leaf_apps;
+    uint32_t n_leaves = 0;
     uint32_t actor_start = 0;
     std::vector<C8> actors;
     std::map<uint32_t, KSpec> kspecs;
@@ -1051,6 +1056,7 @@ struct Lowering {
         const std::string& name = A.name;
         const uint32_t rng = A.w2;
         if (width(idx) > 256) lerr("array index wider than 256 bits");
+        if (explicit_) return leaf_read(arr, idx, rng);
         auto it = arrays.find(name);
         if (it == arrays.end()) {
             array_order.push_back(name);
@@ -1208,7 +1214,39 @@ struct Lowering {
         return false;
     }
 
+    // ---- explicit-model leaves (ExplicitLowering._leaf / _select / _apply) ----------------
+    int32_t leaf_var(uint32_t w, const VarTerm& vt) {
+        return mkvar("@leaf" + std::to_string(n_leaves++), w, vt, nullptr, nullptr);
+    }
+
+    int32_t leaf_read(uint32_t arr, uint32_t idx, uint32_t rng) {
+        const auto key = std::make_pair(arr, idx);
+        auto it = leaf_reads.find(key);
+        if (it != leaf_reads.end()) return it->second;
+        const int32_t n = leaf_var(rng, VarTerm{PFLT_VT_SELECT, arr, idx, 0});
+        leaf_reads.emplace(key, n);
+        return n;
+    }
+
+    Val leaf_apply(uint32_t t) {
+        const uint32_t wd = width(t);
+        if (wd <= 256) {
+            auto it = leaf_apps.find(t);
+            if (it != leaf_apps.end()) return V(it->second);
+            const int32_t n = leaf_var(wd, VarTerm{PFLT_VT_TERM, t, 0, 0});
+            leaf_apps.emplace(t, n);
+            return V(n);
+        }
+        Chunks out;  // one leaf per 256-bit chunk, recorded as its extract term
+        for (uint32_t lo = 0; lo < wd; lo += 256) {
+            const uint32_t cw = std::min<uint32_t>(256, wd - lo);
+            out.push_back({leaf_var(cw, VarTerm{PFLT_VT_EXTRACT, t, lo, lo + cw - 1}), cw});
+        }
+        return VW(out);
+    }
+
     Val apply(uint32_t t) {
+        if (explicit_) return leaf_apply(t);
         const TermRec& r = T(t);
         uint32_t n;
         bool inv;
@@ -1374,7 +1412,7 @@ struct Lowering {
     }
 
     void lower(const std::vector<uint32_t>& roots) {
-        collect_power_facts(roots);
+        if (!explicit_) collect_power_facts(roots);
         for (uint32_t c : roots) {
             if (T(c).sortk != 0) lerr("constraint is not a Bool");
             if (T(c).op == T_TRUE) continue;
@@ -1451,6 +1489,7 @@ Result* lower_job(const Store& S, const std::vector<uint32_t>& rs, const Parents
     R->parented = !P.empty();
     try {
         Lowering L(S, P);
+        L.explicit_ = (flags & PFLT_EXPLICIT) != 0;
         // registry: n_actors, actors x 8; n_specs; per spec: n, has_lo, base x 8, n_concrete,
         // per concrete: value limbs (ceil(n / 32)), digest x 8
         size_t p = 0;
@@ -1619,6 +1658,8 @@ Result* lower_job(const Store& S, const std::vector<uint32_t>& rs, const Parents
 extern "C" {
 
 void* pflt_store_new(void) { return new Store(); }
+
+uint32_t pflt_features(void) { return PFLT_FEAT_EXPLICIT; }
 
 void pflt_store_free(void* st) { delete (Store*)st; }
 

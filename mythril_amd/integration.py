@@ -349,7 +349,8 @@ def discharge_ratio() -> Optional[float]:
 
 
 def install() -> None:
-    """Rebind the funnel's Optimize (support/model.py:13 binds it by value at import).  The
+    """Rebind the funnel's Optimize (support/model.py:13 binds it by value at import) and its
+    ``model_cache`` (support/model.py:20; ``PF_MODEL_CACHE=0`` keeps the reference's).  The
     analysis process does not use torch, so the engine is loaded without it (PF_TORCH=0,
     mythril_amd/_lib.py) unless the caller chose otherwise.
 
@@ -364,6 +365,12 @@ def install() -> None:
         os.environ.setdefault("PF_DEVICES", "all")
 
     funnel.Optimize = gpu_optimize_class()
+    if os.environ.get("PF_MODEL_CACHE", "1") != "0":
+        # the quick-sat loop before every objective-free query (support/model.py:95-98) as
+        # one engine call over the cached models (mythril_amd/model_cache.py)
+        from . import model_cache
+
+        model_cache.install()
 
 
 def state_terms(state) -> List[T.Term]:

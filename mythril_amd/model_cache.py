@@ -1,0 +1,392 @@
+"""GPU-resident ``ModelCache`` — the reference's quick-sat loop as one engine call.
+
+Reference (mythril/support/support_utils.py:57-71, called before every objective-free query
+at mythril/support/model.py:95-98)::
+
+    @lru_cache(maxsize=2**10)
+    def check_quick_sat(self, constraints):
+        for model in reversed(self.model_cache.lru_cache.keys()):     # most recent first
+            model_copy = deepcopy(model)
+            if is_true(model_copy.eval(constraints, model_completion=True)):
+                self.model_cache.put(model, self.model_cache.get(model) + 1)   # LRU bump
+                return model
+        return False
+
+Up to 100 models are deep-copied and evaluated one after the other.  Here the query
+``constraints`` (``simplify(And(*cs)).raw``) is converted once (the AST-id-cached walker,
+z3_terms.py) and lowered once by the EXPLICIT lowering (to_dag.ExplicitLowering, or
+libpflower.so's ``PFLT_EXPLICIT``): every base-array read and UF application is a leaf
+variable.  Each cached model supplies its values of those leaves — a z3 model through
+``eval(leaf, model_completion=True)`` on one private copy, a GPU witness through its own
+interpretation (``Witness.ev``) — memoised per (model, leaf term), so a leaf is evaluated once
+per model for the whole analysis (LASER's queries share almost all of their leaves).  All
+models are then evaluated in ONE ``pf_eval_assignments`` launch (one lane per model) and the
+answer is the first model, most recent first, whose lane is true — the model the reference
+loop returns, with the same LRU bump and the same ``lru_cache`` on the method.
+
+A model whose leaves cannot be evaluated (an empty ``Model()``, a leaf its evaluator rejects)
+is evaluated by the reference's own statement for that query, in its place in the order; a
+query the converter or the lowering cannot take runs the reference loop unchanged.  The
+decision itself is never approximated: the program computes the conjunction's exact value
+(SMT-LIB bit-vector semantics, GPU-parity-tested against the oracle) from exact leaf values.
+"""
+
+from __future__ import annotations
+
+import logging
+import threading
+import time
+from collections import OrderedDict
+from copy import deepcopy
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from .lower import LoweringError, lower
+from .smt import terms as T
+from .smt.to_dag import ExplicitLowering
+
+log = logging.getLogger(__name__)
+
+
+@dataclass
+class QuickSatStats:
+    queries: int = 0          # check_quick_sat calls that reached the engine path (lru misses)
+    hits: int = 0             # ... that returned a model
+    engine_calls: int = 0     # pf_eval_assignments launches
+    models_engine: int = 0    # model evaluations done on the engine
+    models_host: int = 0      # model evaluations done by the reference statement (fallback)
+    reference_loops: int = 0  # queries the converter / lowering could not take (reference loop)
+    leaf_evals: int = 0       # (model, leaf) values computed (the rest were memoised)
+    phase_s: Dict[str, float] = field(default_factory=dict)
+
+
+STATS = QuickSatStats()
+_STATS_LOCK = threading.Lock()
+
+# query term -> (leaf terms, program) or the LoweringError text; the quick-sat of a query is
+# lru-cached by the caller, but the same conjunction term reaches here from distinct z3 ASTs
+_PROGRAMS: "OrderedDict[T.Term, object]" = OrderedDict()
+_PROGRAMS_MAX = 512
+_PROG_LOCK = threading.Lock()
+
+
+def explicit_program(query: T.Term):
+    """(leaf terms, program) of a Bool query term under the explicit lowering; raises
+    LoweringError for a query outside the lowering's vocabulary."""
+    with _PROG_LOCK:
+        hit = _PROGRAMS.get(query)
+        if hit is not None:
+            _PROGRAMS.move_to_end(query)
+    if hit is None:
+        conj = list(query.args) if query.op == "and" else [query]
+        try:
+            hit = _lower_explicit(conj)
+        except (LoweringError, ValueError, OverflowError, RecursionError) as e:
+            hit = f"{type(e).__name__}: {e}"
+        with _PROG_LOCK:
+            _PROGRAMS[query] = hit
+            while len(_PROGRAMS) > _PROGRAMS_MAX:
+                _PROGRAMS.popitem(last=False)
+    if isinstance(hit, str):
+        raise LoweringError(hit)
+    return hit
+
+
+def _lower_explicit(conj: List[T.Term]):
+    """Native (libpflower.so PFLT_EXPLICIT) when built, else the Python reference lowering —
+    the same program node for node (tests/test_model_cache.py)."""
+    from .smt import native_terms
+
+    if native_terms.store() is not None and native_terms.has_explicit():
+        r = native_terms.lower_native(conj, _EMPTY_REG, None, native_terms.PROGRAM | native_terms.EXPLICIT, 0)
+        return r.lowered().var_terms, native_terms.NativeProgram(r, 0).decode()
+    return lower_explicit_py(conj)
+
+
+def lower_explicit_py(conj: List[T.Term]):
+    lo = ExplicitLowering().lower(conj)
+    return lo.var_terms, lower(lo.dag, seed=0)
+
+
+class _EmptyRegistry:
+    """The registry the explicit lowering reads: no actors, no keccak specs (UFs are leaves)."""
+
+    keccak: dict = {}
+    actors: tuple = ()
+
+
+_EMPTY_REG = _EmptyRegistry()
+
+
+# ---- per-model leaf values --------------------------------------------------------------
+
+class LeafValues:
+    """One cached model's values of leaf terms (term -> int), each computed once."""
+
+    __slots__ = ("evaluate", "vals")
+
+    def __init__(self, evaluate: Callable[[T.Term], int]):
+        self.evaluate = evaluate
+        self.vals: Dict[T.Term, int] = {}
+
+    def row(self, leaves: Sequence[T.Term]) -> Optional[List[int]]:
+        """The values of ``leaves``; None if the model's evaluator rejects one of them."""
+        vals = self.vals
+        out = []
+        new = 0
+        for t in leaves:
+            v = vals.get(t)
+            if v is None:
+                try:
+                    v = int(self.evaluate(t))
+                except Exception as e:  # noqa: BLE001 - the reference statement decides then
+                    log.debug("leaf %s not evaluated: %s", t.op, e)
+                    return None
+                v &= T.M(max(t.width, 1))
+                vals[t] = v
+                new += 1
+            out.append(v)
+        if new:
+            with _STATS_LOCK:
+                STATS.leaf_evals += new
+        return out
+
+
+def soa_of(rows: Sequence[Sequence[int]], n_vars: int) -> np.ndarray:
+    """[var][limb][cand] u32 (pf_eval_assignments' layout) from per-candidate value rows."""
+    nv = max(n_vars, 1)
+    n = len(rows)
+    if n_vars == 0:
+        return np.zeros((1, 8, n), dtype=np.uint32)
+    buf = b"".join(v.to_bytes(32, "little") for r in rows for v in r)
+    a = np.frombuffer(buf, dtype="<u4").reshape(n, nv, 8)
+    return np.ascontiguousarray(a.transpose(1, 2, 0), dtype=np.uint32)
+
+
+def eval_rows(program, rows: Sequence[Sequence[int]], engine=None) -> np.ndarray:
+    """SAT flag of each explicit assignment: one pf_eval_assignments launch."""
+    if engine is None:
+        from .engine import get_engine
+
+        engine = get_engine()
+    db = engine.upload([program])
+    try:
+        return engine.eval_assignments(db, 0, soa_of(rows, len(program.vars)))
+    finally:
+        db.free()
+
+
+# models evaluated in the first launch: the reference loop stops at the first model that
+# holds, and in a live analysis that is most often one of the newest (the parent state's
+# model, bumped to the front by the previous query) — evaluating every model's leaves for
+# such a query would cost more than the loop it replaces; the rest go in a second launch
+FIRST_STAGE = 4
+
+
+def choose(query: T.Term, leaf_values: Sequence[Optional[LeafValues]],
+           reference: Callable[[int], bool], engine=None, first_stage: Optional[int] = None) -> Optional[int]:
+    """Index (in the given most-recent-first order) of the first model under which ``query``
+    is true, or None.  ``leaf_values[i]`` None, or a leaf it cannot evaluate, sends model i to
+    ``reference(i)`` — the reference statement — in its place in the order.  The models are
+    evaluated in at most two launches: the newest ``first_stage``, then (if none of them
+    holds) all the others.  Raises LoweringError when the query cannot be lowered (the
+    caller runs the reference loop)."""
+    n = len(leaf_values)
+    if n == 0 or query is T.FALSE:
+        return None
+    k1 = FIRST_STAGE if first_stage is None else first_stage
+    t0 = time.perf_counter()
+    phases: Dict[str, float] = {}
+
+    def lap(name, t):
+        now = time.perf_counter()
+        phases[name] = phases.get(name, 0.0) + now - t
+        return now
+
+    if query is T.TRUE:
+        leaves, program = [], None
+    else:
+        leaves, program = explicit_program(query)
+    t = lap("lower", t0)
+    choice = None
+    host = launches = on_engine_n = 0
+    lo = 0
+    stages = [(0, min(k1, n)), (min(k1, n), n)] if 0 < k1 < n else [(0, n)]
+    for lo, hi in stages:
+        rows = [leaf_values[i].row(leaves) if leaf_values[i] is not None else None for i in range(lo, hi)]
+        t = lap("leaves", t)
+        on_engine = [i for i in range(lo, hi) if rows[i - lo] is not None]
+        flags: Dict[int, bool] = {}
+        if on_engine:
+            if program is None:          # literal True: every model satisfies it
+                flags = {i: True for i in on_engine}
+            else:
+                sat = eval_rows(program, [rows[i - lo] for i in on_engine], engine)
+                flags = dict(zip(on_engine, (bool(x) for x in sat)))
+                launches += 1
+                on_engine_n += len(on_engine)
+        t = lap("eval", t)
+        for i in range(lo, hi):
+            if i in flags:
+                if flags[i]:
+                    choice = i
+                    break
+            else:
+                host += 1
+                if reference(i):
+                    choice = i
+                    break
+        t = lap("host", t)
+        if choice is not None:
+            break
+    with _STATS_LOCK:
+        STATS.queries += 1
+        STATS.hits += choice is not None
+        STATS.engine_calls += launches
+        STATS.models_engine += on_engine_n
+        STATS.models_host += host
+        for k, v in phases.items():
+            STATS.phase_s[k] = STATS.phase_s.get(k, 0.0) + v
+    return choice
+
+
+# ---- the Mythril seam ---------------------------------------------------------------------
+
+def z3_literal(z3, v) -> int:
+    """An evaluated leaf as an int: a bit-vector numeral or a Bool literal."""
+    if z3.is_bv_value(v):
+        return v.as_long()
+    if z3.is_true(v):
+        return 1
+    if z3.is_false(v):
+        return 0
+    raise ValueError(f"not a literal: {v}")
+
+
+def internal_for(model, expression):
+    """The internal model ``mythril.laser.smt.Model.eval`` would use for ``expression``
+    (laser/smt/model.py:45-59): the first whose ``decls()`` holds the expression's
+    declaration, else the last; None for an empty ``Model()`` (whose ``eval`` is None)."""
+    raw = getattr(model, "raw", None)
+    if not raw:
+        return None
+    if len(raw) == 1:
+        return raw[0]
+    d = expression.decl()
+    for im in raw:
+        if d in list(im.decls()):
+            return im
+    return raw[-1]
+
+
+def leaf_evaluator(z3, internal):
+    """Term -> int under one internal model: a GPU witness (integration.Z3WitnessView)
+    through its own interpretation, anything else (a z3 ``ModelRef``) through ``eval`` of the
+    leaf's z3 AST with completion on a private copy (completion adds interpretations to the
+    model it runs on, which is why the reference deep-copies before every eval)."""
+    w = getattr(getattr(internal, "internal", None), "w", None)
+    if w is not None and hasattr(w, "ev"):
+        return lambda t: int(w.ev(t))
+    from .z3_terms import converter
+
+    conv = converter(z3)
+    holder: list = []
+
+    def ev(t: T.Term) -> int:
+        if not holder:
+            holder.append(deepcopy(internal))
+        return z3_literal(z3, holder[0].eval(conv.ast_of(t), model_completion=True))
+
+    return ev
+
+
+_GPU_MODEL_CACHE = None
+
+
+def gpu_model_cache_class():
+    """The drop-in subclass of ``mythril.support.support_utils.ModelCache`` (needs Mythril's
+    module, or the test stand-in); built once per binding."""
+    global _GPU_MODEL_CACHE
+    from mythril.support.support_utils import ModelCache
+
+    if _GPU_MODEL_CACHE is not None and _GPU_MODEL_CACHE.__bases__[0] is ModelCache:
+        return _GPU_MODEL_CACHE
+    import functools
+
+    import z3
+
+    from .z3_terms import converter
+
+    class GpuModelCache(ModelCache):
+        """``ModelCache`` whose quick-sat evaluates every cached model in one engine call
+        (module docstring); ``model_cache`` (the LRU) and ``put`` are the reference's own."""
+
+        def __init__(self, previous=None):
+            super().__init__()
+            if previous is not None:   # keep the process's cached models and their order
+                self.model_cache.lru_cache.update(previous.model_cache.lru_cache)
+            self._leaves: Dict[Tuple[int, int], Tuple[object, LeafValues]] = {}
+            self._lock = threading.Lock()
+
+        def _leaf_values(self, model, constraints) -> Optional[LeafValues]:
+            im = internal_for(model, constraints)
+            if im is None:
+                return None
+            key = (id(model), id(im))
+            ent = self._leaves.get(key)
+            if ent is None or ent[0] is not im:
+                ent = (im, LeafValues(leaf_evaluator(z3, im)))
+                self._leaves[key] = ent
+            return ent[1]
+
+        def _prune(self) -> None:
+            live = {id(m) for m in self.model_cache.lru_cache.keys()}
+            if len(self._leaves) > 2 * max(len(live), 1):
+                self._leaves = {k: v for k, v in self._leaves.items() if k[0] in live}
+
+        def _reference_eval(self, model, constraints) -> bool:
+            model_copy = deepcopy(model)
+            return z3.is_true(model_copy.eval(constraints, model_completion=True))
+
+        @functools.lru_cache(maxsize=2 ** 10)
+        def check_quick_sat(self, constraints):
+            models = list(reversed(self.model_cache.lru_cache.keys()))
+            choice = None
+            with self._lock:
+                try:
+                    query = converter(z3).term(constraints)
+                    lvs = [self._leaf_values(m, constraints) for m in models]
+                    choice = choose(query, lvs, lambda i: self._reference_eval(models[i], constraints))
+                    self._prune()
+                except LoweringError as e:
+                    log.debug("quick-sat by the reference loop: %s", e)
+                    with _STATS_LOCK:
+                        STATS.reference_loops += 1
+                    choice = next((i for i, m in enumerate(models) if self._reference_eval(m, constraints)),
+                                  None)
+            if choice is None:
+                return False
+            model = models[choice]
+            self.model_cache.put(model, self.model_cache.get(model) + 1)
+            return model
+
+    _GPU_MODEL_CACHE = GpuModelCache
+    return GpuModelCache
+
+
+def install() -> None:
+    """Rebind the funnel's ``model_cache`` (support/model.py:20, read at call time at :96 and
+    :120) to a GpuModelCache holding the same models; also the class name the
+    ``DelayConstraintStrategy`` instantiates (strategy/constraint_strategy.py:5,13)."""
+    import sys
+
+    import mythril.support.model as funnel
+
+    cls = gpu_model_cache_class()
+    if not isinstance(funnel.model_cache, cls):
+        funnel.model_cache = cls(funnel.model_cache)
+    strat = sys.modules.get("mythril.laser.ethereum.strategy.constraint_strategy")
+    if strat is not None and getattr(strat, "ModelCache", None) is not None:
+        strat.ModelCache = cls

@@ -34,7 +34,7 @@ _OPS = {
     "bvult": 50, "bvule": 51, "bvslt": 52, "bvsle": 53, "bvuadd_noovfl": 54, "bvumul_noovfl": 55,
 }
 OTHER = 99
-HINTS, PROGRAM = 1, 2
+HINTS, PROGRAM, EXPLICIT = 1, 2, 4
 GET_VARS, GET_VAR_TERMS, GET_UF_APPS, GET_READS, GET_CODE, GET_CONSTS, GET_NODES, GET_POOL, \
     GET_ROOTS, GET_FORCED, GET_IN_ROOTS = range(11)
 VT_TERM, VT_SELECT, VT_EXTRACT = 0, 1, 2
@@ -200,6 +200,15 @@ def store() -> Optional[TermStore]:
             if _STORE is None:
                 _STORE = TermStore(L)
     return _STORE
+
+
+def has_explicit() -> bool:
+    """Whether libpflower.so has the explicit-model lowering (PFLT_EXPLICIT)."""
+    st = store()
+    if st is None or not hasattr(st.L, "pflt_features"):
+        return False
+    st.L.pflt_features.restype = ctypes.c_uint32
+    return bool(st.L.pflt_features() & 1)
 
 
 _BLOBS: Dict[tuple, np.ndarray] = {}

@@ -715,6 +715,58 @@ class TermLowering:
         return Lowered(self.dag, self.var_terms, self.uf_apps, arrays)
 
 
+class ExplicitLowering(TermLowering):
+    """Lowering for evaluation under EXPLICIT models — the GPU-resident ``ModelCache``
+    (mythril_amd/model_cache.py; ref support/support_utils.py:57-71 evaluates a query under up
+    to 100 cached models).  A cached model (a z3 model, or a GPU witness) interprets arrays
+    and UFs its own way, so nothing is interpreted by construction here: every read of a
+    base array (``select(A, i)`` at the bottom of a store / ite chain) and every UF
+    application (keccak and its inverse, ``Power``, any other) is a LEAF variable whose value
+    the caller evaluates under each model; only the operators above the leaves are lowered.
+    A leaf wider than 256 bits (``keccak256_512-1``) is one variable per 256-bit chunk, each
+    recorded as its ``extract`` term.  No side constraints, no concrete-``Power`` facts, no
+    ``inv(f(x)) = x`` substitution: the program computes exactly the conjunction's value
+    under whatever leaf values it is given."""
+
+    def __init__(self):
+        super().__init__(UFRegistry())
+        self.reg.actors = ()   # no generator tables: values come from the models
+        self.leaves: Dict[T.Term, int] = {}
+
+    def _leaf(self, term: T.Term, w: int) -> int:
+        node = self.leaves.get(term)
+        if node is None:
+            node = self._var(f"@leaf{len(self.leaves)}", w, term)
+            self.leaves[term] = node
+        return node
+
+    def _select(self, arr: T.Term, idx: T.Term, term: T.Term) -> int:
+        if arr.op == "array":
+            if idx.width > 256:
+                raise LoweringError("array index wider than 256 bits")
+            return self._leaf(T.select(arr, idx), arr.sort[2])
+        return super()._select(arr, idx, term)
+
+    def _apply(self, t: T.Term):
+        if t.width <= 256:
+            return self._leaf(t, t.width)
+        out, lo = [], 0
+        while lo < t.width:
+            cw = min(256, t.width - lo)
+            out.append((self._leaf(T.extract(lo + cw - 1, lo, t), cw), cw))
+            lo += cw
+        return out
+
+    def lower(self, constraints: List[T.Term]) -> Lowered:
+        for c in constraints:
+            if not c.is_bool:
+                raise LoweringError("constraint is not a Bool")
+            if c is T.TRUE:
+                continue
+            self.dag.assert_(self.b(c))
+        return Lowered(self.dag, self.var_terms, [], {})
+
+
 _WBIN = {
     "bvadd": ir.W_ADD, "bvsub": ir.W_SUB, "bvmul": ir.W_MUL, "bvudiv": ir.W_UDIV,
     "bvurem": ir.W_UREM, "bvsdiv": ir.W_SDIV, "bvsrem": ir.W_SREM, "bvsmod": ir.W_SMOD,

@@ -66,6 +66,9 @@ class Z3Converter:
         self._z3 = z3mod
         self.max_entries = max_entries
         self._cache: "OrderedDict[int, Tuple[object, T.Term]]" = OrderedDict()
+        # term -> one z3 AST it was converted from (the GPU-resident ModelCache evaluates a
+        # query's leaf terms under z3 models: mythril_amd/model_cache.py)
+        self._rev: Dict[T.Term, object] = {}
         self._lock = threading.Lock()
         self._kinds: Optional[Dict[int, Tuple[str, str]]] = None
         self.hits = 0
@@ -93,11 +96,37 @@ class Z3Converter:
     def clear(self) -> None:
         with self._lock:
             self._cache.clear()
+            self._rev.clear()
 
     # ---- public -------------------------------------------------------------------------
     def term(self, e) -> T.Term:
         with self._lock:
             return self._convert(e)
+
+    def ast_of(self, t: T.Term):
+        """A z3 AST for a term: the AST it was converted from, else (for the leaf terms the
+        explicit lowering synthesises — a base-array read below a store chain, a 256-bit
+        chunk of a wide UF application — and for bare symbols) one built from its parts."""
+        with self._lock:
+            a = self._rev.get(t)
+        if a is not None:
+            return a
+        z3 = self.z3
+        op = t.op
+        if op == "select":
+            return z3.Select(self.ast_of(t.args[0]), self.ast_of(t.args[1]))
+        if op == "extract":
+            hi, lo = t.val
+            return z3.Extract(hi, lo, self.ast_of(t.args[0]))
+        if op == "var":
+            return z3.BitVec(t.val, t.width)
+        if op == "bvar":
+            return z3.Bool(t.val)
+        if op == "array":
+            return z3.Array(t.val, z3.BitVecSort(t.sort[1]), z3.BitVecSort(t.sort[2]))
+        if op == "bv":
+            return z3.BitVecVal(t.val, t.width)
+        raise LoweringError(f"no z3 AST for a {op} term")
 
     def terms(self, es) -> List[T.Term]:
         with self._lock:
@@ -113,8 +142,11 @@ class Z3Converter:
 
     def _store(self, e, t: T.Term) -> None:
         self._cache[e.get_id()] = (e, t)  # the AST is kept: its id cannot be recycled
+        self._rev[t] = e
         if len(self._cache) > self.max_entries:
-            self._cache.popitem(last=False)
+            _, (old, ot) = self._cache.popitem(last=False)
+            if self._rev.get(ot) is old:
+                del self._rev[ot]
 
     def _convert(self, root) -> T.Term:
         hit = self._lookup(root)

@@ -740,3 +740,212 @@ class Optimize(_Solver):
 
     def maximize(self, e):
         self._objectives.append(("maximize", e))
+
+
+# ---- models -------------------------------------------------------------------------------
+class ModelRef:
+    """A z3 model stand-in: explicit interpretations and ``eval(e, model_completion)``.
+
+    ``interp`` maps a FuncDeclRef to its interpretation: an int / bool for a 0-ary bit-vector
+    / Bool symbol; ``(entries, else)`` for an array (index -> value) or an n-ary function
+    (argument tuple -> value).  ``eval`` is an independent evaluator over this stand-in's
+    ASTs with SMT-LIB2 operator semantics restated below (z3's total division) — the reference
+    check_quick_sat's ``model.eval(C, model_completion=True)`` in the tests.  Like z3, model
+    completion ADDS default interpretations (0 / false / arrays and functions 0 everywhere)
+    to the model it runs on: the reference deep-copies before every eval for that reason."""
+
+    def __init__(self, interp=None):
+        self._interp = dict(interp or {})
+        self.evals = 0
+
+    def __deepcopy__(self, memo):
+        m = ModelRef(self._interp)
+        return m
+
+    def decls(self):
+        return list(self._interp.keys())
+
+    def __getitem__(self, item):
+        if isinstance(item, int):
+            return self.decls()[item]
+        v = self._interp.get(item)
+        if v is None:
+            return None
+        rng = item.range()
+        if item.arity() == 0 and rng.kind() == Z3_BV_SORT:
+            return BitVecVal(v, rng.size())
+        if item.arity() == 0 and rng.kind() == Z3_BOOL_SORT:
+            return BoolVal(v)
+        return v
+
+    def _default(self, d):
+        if d.arity() == 0 and d.range().kind() == Z3_BOOL_SORT:
+            return False
+        if d.arity() == 0 and d.range().kind() == Z3_BV_SORT:
+            return 0
+        return ({}, 0)
+
+    def _lookup(self, d, completion):
+        v = self._interp.get(d)
+        if v is None:
+            if not completion:
+                raise Z3Exception("stand-in: evaluation without completion of an uninterpreted symbol")
+            v = self._interp[d] = self._default(d)
+        return v
+
+    def eval(self, e, model_completion=False):
+        self.evals += 1
+        memo = {}
+
+        def sel(a, i):
+            while True:
+                if a[0] == "st":
+                    if a[2] == i:
+                        return a[3]
+                    a = a[1]
+                elif a[0] == "K":
+                    return a[1]
+                else:
+                    return a[1].get(i, a[2])
+
+        def go(x):
+            r = memo.get(x.get_id())
+            if r is not None:
+                return r
+            d = x.decl()
+            k = d.kind()
+            if k == Z3_OP_ITE:
+                r = go(x.arg(1)) if go(x.arg(0)) else go(x.arg(2))
+                memo[x.get_id()] = r
+                return r
+            a = [go(c) for c in x.children()]
+            ws = [c.sort().size() if c.sort().kind() == Z3_BV_SORT else 0 for c in x.children()]
+            w = x.sort().size() if x.sort().kind() == Z3_BV_SORT else 0
+            if k == Z3_OP_BNUM:
+                r = x._val
+            elif k == Z3_OP_TRUE:
+                r = True
+            elif k == Z3_OP_FALSE:
+                r = False
+            elif k == Z3_OP_UNINTERPRETED:
+                v = self._lookup(d, model_completion)
+                if d.arity() == 0 and x.sort().kind() == Z3_ARRAY_SORT:
+                    r = ("tab", v[0], v[1])
+                elif d.arity() == 0:
+                    r = v
+                else:
+                    r = v[0].get(tuple(a), v[1])
+            elif k == Z3_OP_CONST_ARRAY:
+                r = ("K", a[0])
+            elif k == Z3_OP_STORE:
+                r = ("st", a[0], a[1], a[2])
+            elif k == Z3_OP_SELECT:
+                r = sel(a[0], a[1])
+            elif k in (Z3_OP_EQ, Z3_OP_IFF):
+                r = a[0] == a[1]
+            elif k == Z3_OP_DISTINCT:
+                r = len(set(a)) == len(a)
+            elif k == Z3_OP_AND:
+                r = all(a)
+            elif k == Z3_OP_OR:
+                r = any(a)
+            elif k == Z3_OP_NOT:
+                r = not a[0]
+            elif k == Z3_OP_XOR:
+                r = bool(a[0]) != bool(a[1])
+            elif k == Z3_OP_IMPLIES:
+                r = (not a[0]) or bool(a[1])
+            elif k == Z3_OP_CONCAT:
+                r = 0
+                for v, wv in zip(a, ws):
+                    r = (r << wv) | v
+            elif k == Z3_OP_EXTRACT:
+                hi, lo = d.params()
+                r = (a[0] >> lo) & ((1 << (hi - lo + 1)) - 1)
+            elif k == Z3_OP_ZERO_EXT:
+                r = a[0]
+            elif k == Z3_OP_SIGN_EXT:
+                r = _sg(a[0], ws[0]) % (1 << w)
+            elif k in (Z3_OP_BADD, Z3_OP_BMUL, Z3_OP_BAND, Z3_OP_BOR, Z3_OP_BXOR):
+                f = {Z3_OP_BADD: lambda p, q: p + q, Z3_OP_BMUL: lambda p, q: p * q,
+                     Z3_OP_BAND: lambda p, q: p & q, Z3_OP_BOR: lambda p, q: p | q,
+                     Z3_OP_BXOR: lambda p, q: p ^ q}[k]
+                r = a[0]
+                for v in a[1:]:
+                    r = f(r, v) % (1 << w)
+            elif k in _BIN_SEM:
+                r = _BIN_SEM[k](a[0], a[1], w)
+            elif k == Z3_OP_BNOT:
+                r = ~a[0] % (1 << w)
+            elif k == Z3_OP_BNEG:
+                r = -a[0] % (1 << w)
+            elif k in _CMP_SEM:
+                r = bool(_CMP_SEM[k](a[0], a[1], ws[0]))
+            else:
+                raise Z3Exception(f"stand-in model: cannot evaluate {d.name()}")
+            memo[x.get_id()] = r
+            return r
+
+        v = go(e)
+        if e.sort().kind() == Z3_BOOL_SORT:
+            return BoolVal(bool(v))
+        if e.sort().kind() == Z3_BV_SORT:
+            return BitVecVal(v, e.sort().size())
+        raise Z3Exception("stand-in model: array-valued eval")
+
+
+def _sg(x, w):
+    return x - (1 << w) if (x >> (w - 1)) & 1 else x
+
+
+def _udiv(a, b, w):
+    return (1 << w) - 1 if b == 0 else a // b
+
+
+def _urem(a, b, w):
+    return a if b == 0 else a % b
+
+
+def _sdiv(a, b, w):   # SMT-LIB2: through bvudiv on magnitudes (b == 0 included)
+    m = (1 << w) - 1
+    sa, sb = a >> (w - 1) & 1, b >> (w - 1) & 1
+    q = _udiv((-a) & m if sa else a, (-b) & m if sb else b, w)
+    return (-q) & m if sa != sb else q
+
+
+def _srem(a, b, w):
+    m = (1 << w) - 1
+    sa, sb = a >> (w - 1) & 1, b >> (w - 1) & 1
+    r = _urem((-a) & m if sa else a, (-b) & m if sb else b, w)
+    return (-r) & m if sa else r
+
+
+def _smod(a, b, w):
+    m = (1 << w) - 1
+    sa, sb = a >> (w - 1) & 1, b >> (w - 1) & 1
+    u = _urem((-a) & m if sa else a, (-b) & m if sb else b, w)
+    if u == 0 or (not sa and not sb):
+        return u
+    if sa and not sb:
+        return (b - u) & m
+    if not sa and sb:
+        return (u + b) & m
+    return (-u) & m
+
+
+_BIN_SEM = {
+    Z3_OP_BSUB: lambda a, b, w: (a - b) % (1 << w),
+    Z3_OP_BUDIV: _udiv, Z3_OP_BUDIV_I: _udiv, Z3_OP_BUREM: _urem, Z3_OP_BUREM_I: _urem,
+    Z3_OP_BSDIV: _sdiv, Z3_OP_BSDIV_I: _sdiv, Z3_OP_BSREM: _srem, Z3_OP_BSREM_I: _srem,
+    Z3_OP_BSMOD: _smod, Z3_OP_BSMOD_I: _smod,
+    Z3_OP_BSHL: lambda a, b, w: 0 if b >= w else (a << b) % (1 << w),
+    Z3_OP_BLSHR: lambda a, b, w: 0 if b >= w else a >> b,
+    Z3_OP_BASHR: lambda a, b, w: (_sg(a, w) >> min(b, w)) % (1 << w),
+}
+_CMP_SEM = {
+    Z3_OP_ULT: lambda p, q, w: p < q, Z3_OP_ULEQ: lambda p, q, w: p <= q,
+    Z3_OP_UGT: lambda p, q, w: p > q, Z3_OP_UGEQ: lambda p, q, w: p >= q,
+    Z3_OP_SLT: lambda p, q, w: _sg(p, w) < _sg(q, w), Z3_OP_SLEQ: lambda p, q, w: _sg(p, w) <= _sg(q, w),
+    Z3_OP_SGT: lambda p, q, w: _sg(p, w) > _sg(q, w), Z3_OP_SGEQ: lambda p, q, w: _sg(p, w) >= _sg(q, w),
+    Z3_OP_BUMUL_NO_OVFL: lambda p, q, w: p * q < (1 << w),
+}

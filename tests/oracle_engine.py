@@ -47,6 +47,17 @@ class OracleEngine:
                 found[s] = f
         return CheckResult(found, budget * len(db), budget * len(db), 0, 0.0)
 
+    def eval_assignments(self, db, set_id, soa):
+        """Engine.eval_assignments: the SAT flag of each explicit candidate ([var][limb][cand])."""
+        self.evals = getattr(self, "evals", 0) + 1
+        sv = O.SetView.from_batch(db.batch, int(set_id))
+        nv = len(db.batch.programs[set_id].vars)
+        out = []
+        for c in range(soa.shape[-1]):
+            vals = [O.limbs_to_int(soa[v, :, c]) for v in range(nv)]
+            out.append(bool(sv.evaluate(vals)))
+        return np.array(out, dtype=bool)
+
     def keccak256(self, messages):
         return [O.keccak256(bytes(m)) for m in messages]
 

@@ -1,0 +1,173 @@
+"""The GPU-resident ModelCache (mythril_amd/model_cache.py) against the reference's quick-sat
+loop (support/support_utils.py:57-71, restated in tests/mythril_standin.py).
+
+Both caches hold the same models in the same LRU order; every query of a LASER-shaped
+stream is answered by both and must return the SAME model object, leaving the SAME LRU
+order (the reference bumps the chosen model).  The models mix GPU witnesses, z3-shaped
+models (tests/fake_z3.ModelRef: explicit interpretations, an independent SMT-LIB evaluator)
+and empty ``Model()``s; the stream ends with a query no model satisfies.  The CPU test runs
+the engine call on the C oracle (tests/oracle_engine.py), the ``gpu`` test on the MI355X.
+"""
+
+import numpy as np
+import pytest
+
+import fake_z3 as z3
+import model_cache_workload as W
+import mythril_standin
+import oracle_engine
+from mythril_amd import integration
+from mythril_amd import model_cache as MC
+from mythril_amd.smt import gpu_check
+from mythril_amd.smt import native_terms
+from mythril_amd.smt import terms as T
+from mythril_amd.z3_terms import converter
+
+
+@pytest.fixture
+def standin(monkeypatch):
+    ns = mythril_standin.install(monkeypatch, z3)
+    monkeypatch.setattr(gpu_check.CONFIG, "budget", 4096)
+    integration._BATCH_CACHE.clear()
+    return ns
+
+
+def _lru(cache):
+    return [id(m) for m in cache.model_cache.lru_cache.keys()]
+
+
+def _run_both(ns, models, queries):
+    ref = ns.ModelCache()
+    gpu = MC.gpu_model_cache_class()()
+    for m in models:
+        ref.put(m, 1)
+        gpu.put(m, 1)
+    picks = []
+    for q in queries:
+        a = ref.check_quick_sat(q)
+        b = gpu.check_quick_sat(q)
+        assert a is b, (q, a, b)
+        assert _lru(ref) == _lru(gpu)
+        mru = list(reversed(ref.model_cache.lru_cache.keys()))
+        picks.append(None if a is False else mru.index(a))
+    return picks
+
+
+def _check_stream(ns, models, queries):
+    MC.STATS.__init__()
+    picks = _run_both(ns, models, queries)
+    assert picks[-1] is None                       # the contradiction: no model
+    assert any(p is not None for p in picks)       # some query answered from the cache
+    assert MC.STATS.engine_calls > 0 and MC.STATS.models_engine > 0
+    assert MC.STATS.reference_loops == 0
+    return picks
+
+
+def test_quick_sat_choice_matches_reference_loop(standin, monkeypatch):
+    oracle_engine.install(monkeypatch)
+    models, queries, _, _ = W.build(z3, standin, n_models=100, n_scenarios=6, n_queries=30)
+    assert len(models) == 100
+    picks = _check_stream(standin, models, queries)
+    # both kinds of model answer somewhere in the stream
+    assert len({p for p in picks if p is not None}) >= 1
+
+
+def test_quick_sat_small_caches_and_empty(standin, monkeypatch):
+    oracle_engine.install(monkeypatch)
+    models, queries, _, _ = W.build(z3, standin, n_models=12, n_scenarios=3, n_queries=12)
+    _run_both(standin, models, queries)
+    gpu = MC.gpu_model_cache_class()()
+    assert gpu.check_quick_sat(queries[0]) is False   # no models
+    gpu.put(standin.Model(), 1)                        # an empty Model(): eval is None
+    assert gpu.check_quick_sat(queries[1]) is False
+
+
+def test_quick_sat_literal_true_and_false(standin, monkeypatch):
+    oracle_engine.install(monkeypatch)
+    m1, m2 = standin.Model([z3.ModelRef({})]), standin.Model([z3.ModelRef({})])
+    gpu = MC.gpu_model_cache_class()()
+    gpu.put(m1, 1)
+    gpu.put(m2, 1)
+    assert gpu.check_quick_sat(z3.BoolVal(True)) is m2     # most recent first
+    assert list(gpu.model_cache.lru_cache.values()) == [1, 2]
+    assert gpu.check_quick_sat(z3.BoolVal(False)) is False
+
+
+def test_leaf_values_are_memoised_per_model(standin, monkeypatch):
+    oracle_engine.install(monkeypatch)
+    x = z3.BitVec("x", 256)
+    A = z3.Array("A", z3.BitVecSort(256), z3.BitVecSort(256))
+    zm = z3.ModelRef({x.decl(): 5, A.decl(): ({5: 7}, 1)})
+    gpu = MC.gpu_model_cache_class()()
+    gpu.put(standin.Model([zm]), 1)
+    MC.STATS.__init__()
+    for k in range(6):
+        q = z3.simplify(z3.And(z3.ULT(x, z3.BitVecVal(10 + k, 256)),
+                               z3.Select(A, x) == z3.BitVecVal(7, 256)))
+        assert gpu.check_quick_sat(q) is not False
+    assert MC.STATS.leaf_evals == 2       # x and A[x], once for the whole stream
+    q = z3.simplify(z3.Select(z3.Store(A, x, z3.BitVecVal(3, 256)), z3.BitVecVal(6, 256)) == z3.BitVecVal(1, 256))
+    assert gpu.check_quick_sat(q) is not False   # A[6] is A's else value 1
+
+
+def test_a_model_the_leaves_cannot_value_goes_to_the_reference_statement(standin, monkeypatch):
+    """A z3 model whose eval rejects a leaf is decided by deepcopy + eval in its place."""
+    oracle_engine.install(monkeypatch)
+
+    class Picky(z3.ModelRef):
+        def __deepcopy__(self, memo):
+            return Picky(self._interp)
+
+        def eval(self, e, model_completion=False):
+            if e.decl().kind() == z3.Z3_OP_SELECT:
+                raise z3.Z3Exception("no")
+            return super().eval(e, model_completion)
+
+    x = z3.BitVec("x", 256)
+    A = z3.Array("A", z3.BitVecSort(256), z3.BitVecSort(256))
+    q = z3.simplify(z3.And(z3.ULT(x, z3.BitVecVal(10, 256)), z3.Select(A, x) == z3.BitVecVal(7, 256)))
+    good = standin.Model([z3.ModelRef({x.decl(): 5, A.decl(): ({5: 7}, 1)})])
+    picky = standin.Model([Picky({x.decl(): 5, A.decl(): ({5: 7}, 1)})])
+    gpu = MC.gpu_model_cache_class()()
+    gpu.put(good, 1)
+    gpu.put(picky, 1)
+    MC.STATS.__init__()
+    assert gpu.check_quick_sat(q) is picky    # decided by deepcopy + eval of the whole query
+    assert MC.STATS.models_host == 1 and MC.STATS.models_engine == 1
+
+
+def test_explicit_lowering_native_equals_python(standin, monkeypatch):
+    oracle_engine.install(monkeypatch)
+    if not native_terms.has_explicit():
+        pytest.skip("libpflower.so not built")
+    from mythril_amd import corpus as C
+
+    corp = C.build(n_scenarios=6, txs=2, seed=3)
+    n = 0
+    for q in corp.queries[:80]:
+        conj = [c for c in q.constraints if c is not T.TRUE]
+        lv1, p1 = MC._lower_explicit(conj)
+        lv2, p2 = MC.lower_explicit_py(conj)
+        assert lv1 == lv2
+        assert np.array_equal(np.asarray(p1.words), np.asarray(p2.words))
+        assert list(p1.consts) == list(p2.consts)
+        assert [(v.name, v.width) for v in p1.vars] == [(v.name, v.width) for v in p2.vars]
+        n += 1
+    assert n == min(80, len(corp.queries))
+
+
+def test_install_rebinds_the_funnel_cache(standin):
+    m = standin.Model([z3.ModelRef({})])
+    standin.funnel.model_cache.put(m, 3)
+    MC.install()
+    mc = standin.funnel.model_cache
+    assert type(mc).__name__ == "GpuModelCache"
+    assert list(mc.model_cache.lru_cache.items()) == [(m, 3)]
+    MC.install()                                  # idempotent
+    assert standin.funnel.model_cache is mc
+
+
+@pytest.mark.gpu
+def test_gpu_quick_sat_choice_matches_reference_loop(standin, engine):
+    models, queries, _, _ = W.build(z3, standin, n_models=100, n_scenarios=8, n_queries=60)
+    _check_stream(standin, models, queries)
