@@ -101,13 +101,20 @@ def _lower_explicit(conj: List[T.Term]):
 
     if native_terms.store() is not None and native_terms.has_explicit():
         r = native_terms.lower_native(conj, _EMPTY_REG, None, native_terms.PROGRAM | native_terms.EXPLICIT, 0)
-        return r.lowered().var_terms, native_terms.NativeProgram(r, 0).decode()
+        # the batch is packed from the native result (ir.Batch -> pack_batch): nothing else
+        # of the program is decoded
+        return r.var_terms(), native_terms.NativeProgram(r, 0)
     return lower_explicit_py(conj)
 
 
 def lower_explicit_py(conj: List[T.Term]):
     lo = ExplicitLowering().lower(conj)
     return lo.var_terms, lower(lo.dag, seed=0)
+
+
+def n_vars(program) -> int:
+    r = getattr(program, "native_result", None)
+    return int(r.info[0]) if r is not None else len(program.vars)
 
 
 class _EmptyRegistry:
@@ -123,16 +130,18 @@ _EMPTY_REG = _EmptyRegistry()
 # ---- per-model leaf values --------------------------------------------------------------
 
 class LeafValues:
-    """One cached model's values of leaf terms (term -> int), each computed once."""
+    """One cached model's values of leaf terms, each computed once and kept as the 32 bytes
+    (little-endian) of its row in pf_eval_assignments' input."""
 
     __slots__ = ("evaluate", "vals")
 
     def __init__(self, evaluate: Callable[[T.Term], int]):
         self.evaluate = evaluate
-        self.vals: Dict[T.Term, int] = {}
+        self.vals: Dict[T.Term, bytes] = {}
 
-    def row(self, leaves: Sequence[T.Term]) -> Optional[List[int]]:
-        """The values of ``leaves``; None if the model's evaluator rejects one of them."""
+    def row(self, leaves: Sequence[T.Term]) -> Optional[bytes]:
+        """The values of ``leaves`` as one byte row; None if the model's evaluator rejects
+        one of them."""
         vals = self.vals
         out = []
         new = 0
@@ -140,42 +149,52 @@ class LeafValues:
             v = vals.get(t)
             if v is None:
                 try:
-                    v = int(self.evaluate(t))
+                    x = int(self.evaluate(t))
                 except Exception as e:  # noqa: BLE001 - the reference statement decides then
                     log.debug("leaf %s not evaluated: %s", t.op, e)
                     return None
-                v &= T.M(max(t.width, 1))
-                vals[t] = v
+                v = vals[t] = (x & T.M(max(t.width, 1))).to_bytes(32, "little")
                 new += 1
             out.append(v)
         if new:
             with _STATS_LOCK:
                 STATS.leaf_evals += new
-        return out
+        return b"".join(out)
+
+    def value(self, t: T.Term) -> Optional[int]:
+        v = self.vals.get(t)
+        return None if v is None else int.from_bytes(v, "little")
 
 
-def soa_of(rows: Sequence[Sequence[int]], n_vars: int) -> np.ndarray:
-    """[var][limb][cand] u32 (pf_eval_assignments' layout) from per-candidate value rows."""
-    nv = max(n_vars, 1)
+def soa_of(rows: Sequence[bytes], n_vars: int) -> np.ndarray:
+    """[var][limb][cand] u32 (pf_eval_assignments' layout) from per-candidate byte rows
+    (``n_vars`` x 32 bytes each)."""
     n = len(rows)
     if n_vars == 0:
         return np.zeros((1, 8, n), dtype=np.uint32)
-    buf = b"".join(v.to_bytes(32, "little") for r in rows for v in r)
-    a = np.frombuffer(buf, dtype="<u4").reshape(n, nv, 8)
+    a = np.frombuffer(b"".join(rows), dtype="<u4").reshape(n, n_vars, 8)
     return np.ascontiguousarray(a.transpose(1, 2, 0), dtype=np.uint32)
 
 
-def eval_rows(program, rows: Sequence[Sequence[int]], engine=None) -> np.ndarray:
-    """SAT flag of each explicit assignment: one pf_eval_assignments launch."""
+def rows_of_ints(rows: Sequence[Sequence[int]]) -> List[bytes]:
+    return [b"".join((v & T.M(256)).to_bytes(32, "little") for v in r) for r in rows]
+
+
+def eval_rows(program, rows: Sequence[bytes], engine=None, db=None) -> np.ndarray:
+    """SAT flag of each explicit assignment: one pf_eval_assignments launch (over ``db``, the
+    program already uploaded, when given)."""
     if engine is None:
         from .engine import get_engine
 
         engine = get_engine()
-    db = engine.upload([program])
+    own = db is None
+    if own:
+        db = engine.upload([program])
     try:
-        return engine.eval_assignments(db, 0, soa_of(rows, len(program.vars)))
+        return engine.eval_assignments(db, 0, soa_of(rows, n_vars(program)))
     finally:
-        db.free()
+        if own:
+            db.free()
 
 
 # models evaluated in the first launch: the reference loop stops at the first model that
@@ -210,37 +229,13 @@ def choose(query: T.Term, leaf_values: Sequence[Optional[LeafValues]],
     else:
         leaves, program = explicit_program(query)
     t = lap("lower", t0)
-    choice = None
-    host = launches = on_engine_n = 0
-    lo = 0
     stages = [(0, min(k1, n)), (min(k1, n), n)] if 0 < k1 < n else [(0, n)]
-    for lo, hi in stages:
-        rows = [leaf_values[i].row(leaves) if leaf_values[i] is not None else None for i in range(lo, hi)]
-        t = lap("leaves", t)
-        on_engine = [i for i in range(lo, hi) if rows[i - lo] is not None]
-        flags: Dict[int, bool] = {}
-        if on_engine:
-            if program is None:          # literal True: every model satisfies it
-                flags = {i: True for i in on_engine}
-            else:
-                sat = eval_rows(program, [rows[i - lo] for i in on_engine], engine)
-                flags = dict(zip(on_engine, (bool(x) for x in sat)))
-                launches += 1
-                on_engine_n += len(on_engine)
-        t = lap("eval", t)
-        for i in range(lo, hi):
-            if i in flags:
-                if flags[i]:
-                    choice = i
-                    break
-            else:
-                host += 1
-                if reference(i):
-                    choice = i
-                    break
-        t = lap("host", t)
-        if choice is not None:
-            break
+    if engine is None and program is not None:
+        from .engine import get_engine
+
+        engine = get_engine()
+    choice, host, launches, on_engine_n, t = _stages(stages, leaves, program, leaf_values, reference,
+                                                     engine, lap, t)
     with _STATS_LOCK:
         STATS.queries += 1
         STATS.hits += choice is not None
@@ -250,6 +245,47 @@ def choose(query: T.Term, leaf_values: Sequence[Optional[LeafValues]],
         for k, v in phases.items():
             STATS.phase_s[k] = STATS.phase_s.get(k, 0.0) + v
     return choice
+
+
+def _stages(stages, leaves, program, leaf_values, reference, engine, lap, t):
+    """choose()'s launches: the program is uploaded once for both stages."""
+    choice = None
+    host = launches = on_engine_n = 0
+    db = None
+    try:
+        for lo, hi in stages:
+            rows = [leaf_values[i].row(leaves) if leaf_values[i] is not None else None for i in range(lo, hi)]
+            t = lap("leaves", t)
+            on_engine = [i for i in range(lo, hi) if rows[i - lo] is not None]
+            flags: Dict[int, bool] = {}
+            if on_engine:
+                if program is None:          # literal True: every model satisfies it
+                    flags = {i: True for i in on_engine}
+                else:
+                    if db is None:
+                        db = engine.upload([program])
+                    sat = eval_rows(program, [rows[i - lo] for i in on_engine], engine, db)
+                    flags = dict(zip(on_engine, (bool(x) for x in sat)))
+                    launches += 1
+                    on_engine_n += len(on_engine)
+            t = lap("eval", t)
+            for i in range(lo, hi):
+                if i in flags:
+                    if flags[i]:
+                        choice = i
+                        break
+                else:
+                    host += 1
+                    if reference(i):
+                        choice = i
+                        break
+            t = lap("host", t)
+            if choice is not None:
+                break
+    finally:
+        if db is not None:
+            db.free()
+    return choice, host, launches, on_engine_n, t
 
 
 # ---- the Mythril seam ---------------------------------------------------------------------
@@ -287,8 +323,8 @@ def leaf_evaluator(z3, internal):
     leaf's z3 AST with completion on a private copy (completion adds interpretations to the
     model it runs on, which is why the reference deep-copies before every eval)."""
     w = getattr(getattr(internal, "internal", None), "w", None)
-    if w is not None and hasattr(w, "ev"):
-        return lambda t: int(w.ev(t))
+    if w is not None and hasattr(w, "leaf_value"):
+        return w.leaf_value
     from .z3_terms import converter
 
     conv = converter(z3)

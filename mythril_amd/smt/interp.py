@@ -95,6 +95,7 @@ class Witness:
             w.array_reads.update(p.array_reads)
             w.uf_apps.extend(p.uf_apps)
         w._memo, w._tables, w._pos, w._keccak_tables = {}, None, None, {}
+        w._first = w._building = None
         return w
 
     # ---- array interpretation: first earlier index with an equal value ------------------
@@ -117,12 +118,45 @@ class Witness:
             self._pos[name] = pos
         return pos
 
+    # The scan's answer is the FIRST read of the array, over all of its reads, whose index
+    # evaluates to iv: for a read that is one of the entries, its own entry matches, so the
+    # first match lies at or before it.  Once every index of an array has been evaluated (by
+    # the scan's rules, so nested reads never see an unfinished table) that answer is a dict
+    # lookup — a quick-sat leaf or a later query's read then costs O(1), not O(reads).
+    _first: Optional[Dict[str, object]] = None     # array -> {index value: value} | False
+    _building: Optional[set] = None
+
+    def _first_table(self, name: str, reads):
+        if self._first is None:
+            self._first, self._building = {}, set()
+        tab = self._first.get(name)
+        if tab is not None:
+            return tab
+        if name in self._building:
+            return False          # a nested read while the table is being built: scan
+        self._building.add(name)
+        try:
+            tab = {}
+            for it, sel in reads:
+                v = self._evr(it)
+                if v not in tab:
+                    tab[v] = self.reads.get(sel, 0)
+        except Exception:  # noqa: BLE001 - an index only the scan's early stop avoids: scan
+            tab = False
+        finally:
+            self._building.discard(name)
+        self._first[name] = tab
+        return tab
+
     def _array_read(self, arr: T.Term, idx: Optional[T.Term], iv: int) -> int:
         name = arr.val
         reads = self.array_reads.get(name)
         if not reads:
             tabs = self._tables or {}
             return tabs.get(name, {}).get(iv, 0)     # model completion: 0
+        tab = self._first_table(name, reads)
+        if tab is not False:
+            return tab.get(iv, 0)
         last = len(reads) - 1
         if idx is not None:
             r = self._entry_pos(name).get(T.select(arr, idx))
@@ -227,6 +261,21 @@ class Witness:
         return 1   # model completion outside the set's applications: a positive value
 
     # ---- evaluator ------------------------------------------------------------------------
+    def leaf_value(self, t: T.Term) -> int:
+        """``ev`` of a quick-sat leaf (mythril_amd/model_cache.py: a symbol, a base-array read,
+        a UF application), with the two answers that need no evaluation first: a symbol's own
+        value, and 0 for a read of an array this witness holds no read of (completion)."""
+        op = t.op
+        if op == "var":
+            return self.vars.get(t.val, 0)
+        if op == "bvar":
+            return int(self.bools.get(t.val, False))
+        if op == "select" and t.args[0].op == "array":
+            name = t.args[0].val
+            if not self.array_reads.get(name) and name not in (self._tables or ()):
+                return 0
+        return int(self.ev(t))
+
     def ev(self, t: T.Term):
         """Value of ``t`` under this witness.  A term nested deeper than Python's recursion
         limit (long and / or / ite chains of a large LASER state) is first evaluated bottom-up

@@ -297,6 +297,19 @@ class _Result:
             vs.append(ir.Var(labels[i].decode(), w_, k_, h0, h1, parent))
         return vs
 
+    def var_terms(self) -> List[T.Term]:
+        """The variables' terms alone (the explicit lowering's leaves)."""
+        terms = self.st.terms
+        out = []
+        for typ, a, b, c in self.get(GET_VAR_TERMS, self.info[2], 4).tolist():
+            if typ == VT_TERM:
+                out.append(terms[a])
+            elif typ == VT_SELECT:
+                out.append(T.select(terms[a], terms[b]))
+            else:
+                out.append(T.extract(c, b, terms[a]))
+        return out
+
     def lowered(self) -> Lowered:
         terms = self.st.terms
         vt = self.get(GET_VAR_TERMS, self.info[2], 4)
