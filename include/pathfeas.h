@@ -114,6 +114,15 @@ int pf_materialize(uint64_t handle, uint64_t global_seed, const uint32_t* set_id
 /* Evaluate set `set` on n_cand explicit assignments, SoA limbs [var][limb][cand].          */
 int pf_eval_assignments(uint64_t handle, uint32_t set, const uint32_t* soa, uint32_t n_cand,
                         uint8_t* sat_out);
+/* One program evaluated over explicit assignments in one call (no batch object): validated
+ * and transformed exactly as pf_batch_create does, uploaded with its assignments
+ * ([var][limb][cand] u32, like pf_eval_assignments) through pinned staging, one launch,
+ * verdicts copied back.  Replaces z3 ModelRef.eval(C, model_completion=True) over the <= 100
+ * cached models of check_quick_sat (mythril/support/support_utils.py:57-71), one lane per
+ * model (the GPU-resident ModelCache, mythril_amd/model_cache.py). */
+int pf_eval_program(int device, const uint32_t* code, size_t n_ins, const uint32_t* consts, size_t n_const,
+                    const uint32_t* schema, size_t n_vars, const uint32_t* soa, uint32_t n_cand,
+                    uint8_t* sat_out);
 int pf_eval_assignments_dev(uint64_t handle, uint32_t set, const uint32_t* d_soa,
                             uint32_t n_cand, uint8_t* d_sat_out, void* stream);
 

@@ -663,16 +663,15 @@ int pf_shutdown(void) {
     return 0;
 }
 
-int pf_batch_create_on(int device, const uint32_t* code, size_t n_ins, const uint32_t* consts,
-                       size_t n_const, const uint32_t* schema, size_t n_vars,
-                       const uint32_t* parents, size_t n_parents, const pf_set_desc* descs,
-                       size_t n_sets, uint64_t* handle_out) {
-    std::lock_guard<std::mutex> lk(g_mu);
-    Dev* Dv = use_dev(device);
-    if (!Dv) return -1;
-    if (!handle_out) return fail("pf_batch_create: null handle_out");
-    // host-side shape checks: every kernel index is derived from these
-    uint32_t max_vars = 0;
+// Host-side checks of packed programs and their device form (pf_batch_create and
+// pf_eval_program): every kernel index is derived from these, so nothing the caller packed is
+// trusted.  Fills the device program (device_program), the per-set wide flags and the largest
+// variable count; returns 0 or fail().
+static int prepare_program(const uint32_t* code, size_t n_ins, const uint32_t* consts, size_t n_const,
+                           const uint32_t* schema, size_t n_vars, size_t n_parents, const pf_set_desc* descs,
+                           size_t n_sets, std::vector<uint32_t>& code_out, std::vector<pf_set_desc>& descs_out,
+                           std::vector<uint8_t>& wide, uint32_t& max_vars) {
+    max_vars = 0;
     for (size_t s = 0; s < n_sets; s++) {
         const pf_set_desc& d = descs[s];
         if ((uint64_t)d.code_off + d.n_ins > n_ins || d.n_ins == 0)
@@ -709,7 +708,7 @@ int pf_batch_create_on(int device, const uint32_t* code, size_t n_ins, const uin
     // traffic bits and register def-before-use, recomputed here so the kernel can trust
     // them whatever the caller packed (w0 bits 18..23)
     std::vector<uint32_t> code_fixed(code, code + 4 * n_ins);
-    std::vector<uint8_t> wide(n_sets, 0);
+    wide.assign(n_sets, 0);
     for (size_t s = 0; s < n_sets; s++) {
         const pf_set_desc& d = descs[s];
         uint32_t wdef = 0u, bdef = 0u, max_wreg = 0u;
@@ -745,9 +744,26 @@ int pf_batch_create_on(int device, const uint32_t* code, size_t n_ins, const uin
             if (bres) bdef |= 1u << (rd & 31u);
         }
     }
-    std::vector<uint32_t> code_out;
-    std::vector<pf_set_desc> descs_out(descs, descs + n_sets);
+    descs_out.assign(descs, descs + n_sets);
     device_program(code_fixed, descs_out, code_out, consts, n_const);
+    return 0;
+}
+
+int pf_batch_create_on(int device, const uint32_t* code, size_t n_ins, const uint32_t* consts,
+                       size_t n_const, const uint32_t* schema, size_t n_vars,
+                       const uint32_t* parents, size_t n_parents, const pf_set_desc* descs,
+                       size_t n_sets, uint64_t* handle_out) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    Dev* Dv = use_dev(device);
+    if (!Dv) return -1;
+    if (!handle_out) return fail("pf_batch_create: null handle_out");
+    std::vector<uint32_t> code_out;
+    std::vector<pf_set_desc> descs_out;
+    std::vector<uint8_t> wide;
+    uint32_t max_vars = 0;
+    if (prepare_program(code, n_ins, consts, n_const, schema, n_vars, n_parents, descs, n_sets, code_out,
+                        descs_out, wide, max_vars))
+        return -1;
     code = code_out.data();
     n_ins = code_out.size() / 4;
     descs = descs_out.data();
@@ -1045,6 +1061,71 @@ int pf_eval_assignments(uint64_t handle, uint32_t set, const uint32_t* soa, uint
         if (hipDeviceSynchronize() == hipSuccess) hipFree(dm);
         return fail("pf_eval_assignments: HIP call failed");
     }
+    if (D->pool.size() >= kPoolBlocks) {
+        hipFree(D->pool.front().first);
+        D->pool.erase(D->pool.begin());
+    }
+    D->pool.emplace_back(dm, cap);
+    return 0;
+}
+
+int pf_eval_program(int device, const uint32_t* code, size_t n_ins, const uint32_t* consts, size_t n_const,
+                    const uint32_t* schema, size_t n_vars, const uint32_t* soa, uint32_t n_cand,
+                    uint8_t* sat_out) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    Dev* D = use_dev(device);
+    if (!D) return -1;
+    if (n_cand == 0) return 0;
+    if (!code || !sat_out || (n_vars && !soa)) return fail("pf_eval_program: null argument");
+    const pf_set_desc d0{0u, (uint32_t)n_ins, 0u, (uint32_t)n_const, 0u, (uint32_t)n_vars, 0u, PF_NO_PARENT};
+    std::vector<uint32_t> code_out;
+    std::vector<pf_set_desc> descs_out;
+    std::vector<uint8_t> wide;
+    uint32_t max_vars = 0;
+    if (prepare_program(code, n_ins, consts, n_const, schema, n_vars, 0, &d0, 1, code_out, descs_out, wide,
+                        max_vars))
+        return -1;
+    // one pooled block [code | consts + zero entry | schema | desc | assignments | verdicts] and
+    // one copy each way through the pinned staging buffer; the stream is synchronised, not
+    // the device (no batch object, no events): the quick-sat call of the GPU-resident
+    // ModelCache, once or twice per objective-free query (mythril_amd/model_cache.py)
+    auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+    const size_t nv = std::max<size_t>(n_vars, 1), n_dev = code_out.size() / 4;
+    const size_t soa_bytes = nv * 8 * (size_t)n_cand * 4;
+    const size_t o_code = 0, o_const = al(n_dev * 16), o_schema = o_const + al(n_const * 32 + 32),
+                 o_desc = o_schema + al(nv * 16), o_soa = o_desc + al(sizeof(pf_set_desc)),
+                 o_out = o_soa + al(soa_bytes), total = o_out + n_cand;
+    uint8_t* pin = pinned_staging(std::max<size_t>(o_out, n_cand));
+    if (!pin) return fail("pf_eval_program: no pinned staging buffer");
+    memset(pin, 0, o_out);
+    memcpy(pin + o_code, code_out.data(), n_dev * 16);
+    if (n_const) memcpy(pin + o_const, consts, n_const * 32);
+    if (n_vars) memcpy(pin + o_schema, schema, n_vars * 16);
+    memcpy(pin + o_desc, descs_out.data(), sizeof(pf_set_desc));
+    if (n_vars) memcpy(pin + o_soa, soa, soa_bytes);
+    hipStream_t st = D->stream;
+    if (switch_stream(D, st)) return -1;
+    size_t cap = 0;
+    uint8_t* dm = static_cast<uint8_t*>(pool_acquire(D, total, &cap));
+    if (!dm) return fail("pf_eval_program: hipMalloc(%zu) failed", total);
+    int rc = 0;
+    if (hipMemcpyAsync(dm, pin, o_out, hipMemcpyHostToDevice, st) != hipSuccess) rc = -1;
+    if (!rc) {
+        hipLaunchKernelGGL(pf_eval_soa_kernel, dim3((n_cand + 255) / 256), dim3(256), 0, st,
+                           reinterpret_cast<const pf_set_desc*>(dm + o_desc), 0u,
+                           reinterpret_cast<const uint4*>(dm + o_code), reinterpret_cast<const uint32_t*>(dm + o_const),
+                           reinterpret_cast<const uint4*>(dm + o_schema), static_cast<const uint32_t*>(nullptr),
+                           reinterpret_cast<const uint32_t*>(dm + o_soa), n_cand, dm + o_out);
+        if (hipGetLastError() != hipSuccess ||
+            hipMemcpyAsync(pin, dm + o_out, n_cand, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            rc = -1;
+    }
+    if (rc) {
+        if (hipDeviceSynchronize() == hipSuccess) hipFree(dm);
+        return fail("pf_eval_program: HIP call failed");
+    }
+    memcpy(sat_out, pin, n_cand);
     if (D->pool.size() >= kPoolBlocks) {
         hipFree(D->pool.front().first);
         D->pool.erase(D->pool.begin());

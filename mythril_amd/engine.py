@@ -202,6 +202,29 @@ class Engine:
                                                  n_cand, _lib.ptr_u8(out)), "pf_eval_assignments")
         return out[:n_cand].astype(bool)
 
+    def eval_program(self, program: Program, soa: np.ndarray) -> np.ndarray:
+        """SAT flag of each explicit candidate of one program, in one call (pf_eval_program:
+        no batch object; the GPU-resident ModelCache's launch).  The packed arrays are kept
+        on the program, so a second launch over it packs nothing."""
+        pk = getattr(program, "_eval_pack", None)
+        if pk is None:
+            b = Batch([program])
+            pk = (np.ascontiguousarray(b.code, dtype=np.uint32).reshape(-1),
+                  np.ascontiguousarray(b.consts, dtype=np.uint32).reshape(-1),
+                  np.ascontiguousarray(b.schema, dtype=np.uint32).reshape(-1))
+            program._eval_pack = pk
+        code, consts, schema = pk
+        soa = np.ascontiguousarray(soa, dtype=np.uint32)
+        n_cand = soa.shape[-1]
+        out = np.zeros(max(n_cand, 1), dtype=np.uint8)
+        z = np.zeros(8, dtype=np.uint32)
+        _lib.check(_lib.lib().pf_eval_program(
+            self.device, _lib.ptr_u32(code), code.size // 4,
+            _lib.ptr_u32(consts if consts.size else z), consts.size // 8,
+            _lib.ptr_u32(schema if schema.size else z), schema.size // 4,
+            _lib.ptr_u32(soa.reshape(-1)), n_cand, _lib.ptr_u8(out)), "pf_eval_program")
+        return out[:n_cand].astype(bool)
+
     # ---- keccak -------------------------------------------------------------------
     def keccak256(self, messages: Sequence[bytes]) -> List[bytes]:
         n = len(messages)

@@ -180,21 +180,21 @@ def rows_of_ints(rows: Sequence[Sequence[int]]) -> List[bytes]:
     return [b"".join((v & T.M(256)).to_bytes(32, "little") for v in r) for r in rows]
 
 
-def eval_rows(program, rows: Sequence[bytes], engine=None, db=None) -> np.ndarray:
-    """SAT flag of each explicit assignment: one pf_eval_assignments launch (over ``db``, the
-    program already uploaded, when given)."""
+def eval_rows(program, rows: Sequence[bytes], engine=None) -> np.ndarray:
+    """SAT flag of each explicit assignment: one launch (pf_eval_program; an engine without
+    it — the tests' oracle engine — through upload + eval_assignments)."""
     if engine is None:
         from .engine import get_engine
 
         engine = get_engine()
-    own = db is None
-    if own:
-        db = engine.upload([program])
+    soa = soa_of(rows, n_vars(program))
+    if hasattr(engine, "eval_program"):
+        return engine.eval_program(program, soa)
+    db = engine.upload([program])
     try:
-        return engine.eval_assignments(db, 0, soa_of(rows, n_vars(program)))
+        return engine.eval_assignments(db, 0, soa)
     finally:
-        if own:
-            db.free()
+        db.free()
 
 
 # models evaluated in the first launch: the reference loop stops at the first model that
@@ -248,43 +248,36 @@ def choose(query: T.Term, leaf_values: Sequence[Optional[LeafValues]],
 
 
 def _stages(stages, leaves, program, leaf_values, reference, engine, lap, t):
-    """choose()'s launches: the program is uploaded once for both stages."""
+    """choose()'s launches, newest models first."""
     choice = None
     host = launches = on_engine_n = 0
-    db = None
-    try:
-        for lo, hi in stages:
-            rows = [leaf_values[i].row(leaves) if leaf_values[i] is not None else None for i in range(lo, hi)]
-            t = lap("leaves", t)
-            on_engine = [i for i in range(lo, hi) if rows[i - lo] is not None]
-            flags: Dict[int, bool] = {}
-            if on_engine:
-                if program is None:          # literal True: every model satisfies it
-                    flags = {i: True for i in on_engine}
-                else:
-                    if db is None:
-                        db = engine.upload([program])
-                    sat = eval_rows(program, [rows[i - lo] for i in on_engine], engine, db)
-                    flags = dict(zip(on_engine, (bool(x) for x in sat)))
-                    launches += 1
-                    on_engine_n += len(on_engine)
-            t = lap("eval", t)
-            for i in range(lo, hi):
-                if i in flags:
-                    if flags[i]:
-                        choice = i
-                        break
-                else:
-                    host += 1
-                    if reference(i):
-                        choice = i
-                        break
-            t = lap("host", t)
-            if choice is not None:
-                break
-    finally:
-        if db is not None:
-            db.free()
+    for lo, hi in stages:
+        rows = [leaf_values[i].row(leaves) if leaf_values[i] is not None else None for i in range(lo, hi)]
+        t = lap("leaves", t)
+        on_engine = [i for i in range(lo, hi) if rows[i - lo] is not None]
+        flags: Dict[int, bool] = {}
+        if on_engine:
+            if program is None:          # literal True: every model satisfies it
+                flags = {i: True for i in on_engine}
+            else:
+                sat = eval_rows(program, [rows[i - lo] for i in on_engine], engine)
+                flags = dict(zip(on_engine, (bool(x) for x in sat)))
+                launches += 1
+                on_engine_n += len(on_engine)
+        t = lap("eval", t)
+        for i in range(lo, hi):
+            if i in flags:
+                if flags[i]:
+                    choice = i
+                    break
+            else:
+                host += 1
+                if reference(i):
+                    choice = i
+                    break
+        t = lap("host", t)
+        if choice is not None:
+            break
     return choice, host, launches, on_engine_n, t
 
 

@@ -156,6 +156,31 @@ def test_explicit_lowering_native_equals_python(standin, monkeypatch):
     assert n == min(80, len(corp.queries))
 
 
+def test_explicit_program_holds_under_the_planted_models(monkeypatch):
+    """The explicit program computes the conjunction from its leaves: with every leaf valued
+    by a planted model (the engine's interpretation of arrays and keccak), each SAT-labelled
+    corpus query's program is true, and its value agrees with evaluating the terms
+    directly under that model for every query."""
+    import pyoracle as O
+    from mythril_amd import corpus as C
+    from mythril_amd import ir
+
+    oracle_engine.install(monkeypatch)
+    corp = C.build(n_scenarios=6, txs=2, seed=9)
+    n_sat = 0
+    for q in corp.queries[:120]:
+        if q.planted is None:
+            continue
+        conj = [c for c in q.constraints if c is not T.TRUE]
+        leaves, prog = MC._lower_explicit(conj)
+        ev = C._PlantedEval(q.planted, corp.kfm.registry)
+        vals = [int(ev.ev(t)) & ((1 << max(t.width, 1)) - 1) for t in leaves]
+        got = bool(O.SetView.from_batch(ir.Batch([prog]), 0).evaluate(vals))
+        assert got == all(bool(ev.ev(c)) for c in conj), q.origin
+        n_sat += got
+    assert n_sat > 20
+
+
 def test_install_rebinds_the_funnel_cache(standin):
     m = standin.Model([z3.ModelRef({})])
     standin.funnel.model_cache.put(m, 3)
@@ -171,3 +196,45 @@ def test_install_rebinds_the_funnel_cache(standin):
 def test_gpu_quick_sat_choice_matches_reference_loop(standin, engine):
     models, queries, _, _ = W.build(z3, standin, n_models=100, n_scenarios=8, n_queries=60)
     _check_stream(standin, models, queries)
+
+
+@pytest.mark.gpu
+def test_gpu_eval_program_matches_oracle(engine, monkeypatch):
+    """pf_eval_program (one call: validate, upload, one launch) gives the oracle's verdict on
+    explicit assignments of corpus queries' explicit programs — random values and the
+    planted models' values (SAT by construction under the engine's interpretation)."""
+    import random
+
+    import pyoracle as O
+    from mythril_amd import corpus as C
+    from mythril_amd import ir
+
+    corp = C.build(n_scenarios=4, txs=2, seed=5)
+    rng = random.Random(1)
+    n = 0
+    for q in corp.queries[:40]:
+        leaves, prog = MC._lower_explicit([c for c in q.constraints if c is not T.TRUE])
+        ev = C._PlantedEval(q.planted, corp.kfm.registry) if q.planted is not None else None
+        rows = []
+        for k in range(70):
+            vals = []
+            for t in leaves:
+                if k == 0 and ev is not None:
+                    v = int(ev.ev(t))
+                else:
+                    v = rng.choice([0, 1, rng.getrandbits(max(t.width, 1))])
+                vals.append(v & ((1 << max(t.width, 1)) - 1))
+            rows.append(vals)
+        soa = MC.soa_of(MC.rows_of_ints(rows), MC.n_vars(prog))
+        got = engine.eval_program(prog, soa)
+        sv = O.SetView.from_batch(ir.Batch([prog]), 0)
+        want = [bool(sv.evaluate(r)) for r in rows]
+        assert want[0] or q.label != "sat", q.origin   # the planted model satisfies its query
+        assert list(got) == want, q.origin
+        db = engine.upload([prog])
+        try:
+            assert list(engine.eval_assignments(db, 0, soa)) == want
+        finally:
+            db.free()
+        n += 1
+    assert n == 40
