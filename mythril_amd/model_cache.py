@@ -24,8 +24,10 @@ models are then evaluated in ONE ``pf_eval_assignments`` launch (one lane per mo
 answer is the first model, most recent first, whose lane is true — the model the reference
 loop returns, with the same LRU bump and the same ``lru_cache`` on the method.
 
-A model whose leaves cannot be evaluated (an empty ``Model()``, a leaf its evaluator rejects)
-is evaluated by the reference's own statement for that query, in its place in the order; a
+The newest FIRST_STAGE models go in a first launch (the loop's most frequent answers), the
+others in a second one only if none of those holds.  A model whose leaves cannot be evaluated
+(an empty ``Model()``, a leaf its evaluator rejects) is decided by the reference's own
+statement for that query, in its place in the order; a
 query the converter or the lowering cannot take runs the reference loop unchanged.  The
 decision itself is never approximated: the program computes the conjunction's exact value
 (SMT-LIB bit-vector semantics, GPU-parity-tested against the oracle) from exact leaf values.
@@ -197,21 +199,23 @@ def eval_rows(program, rows: Sequence[bytes], engine=None) -> np.ndarray:
         db.free()
 
 
-# models evaluated in the first launch: the reference loop stops at the first model that
+# Models evaluated in the first launch: the reference loop stops at the first model that
 # holds, and in a live analysis that is most often one of the newest (the parent state's
-# model, bumped to the front by the previous query) — evaluating every model's leaves for
-# such a query would cost more than the loop it replaces; the rest go in a second launch
+# model, bumped to the front by the query before) — computing every model's leaves for such a
+# query would cost more than the loop it replaces.  The others go in a second launch.
+# (Deciding only the newest model on the host first measured slower: it held for 24 of 121
+# profile queries, profiles/r05g_quick_sat.jsonl.)
 FIRST_STAGE = 4
 
 
 def choose(query: T.Term, leaf_values: Sequence[Optional[LeafValues]],
            reference: Callable[[int], bool], engine=None, first_stage: Optional[int] = None) -> Optional[int]:
     """Index (in the given most-recent-first order) of the first model under which ``query``
-    is true, or None.  ``leaf_values[i]`` None, or a leaf it cannot evaluate, sends model i to
-    ``reference(i)`` — the reference statement — in its place in the order.  The models are
-    evaluated in at most two launches: the newest ``first_stage``, then (if none of them
-    holds) all the others.  Raises LoweringError when the query cannot be lowered (the
-    caller runs the reference loop)."""
+    is true, or None.  The models are evaluated in at most two launches: the newest
+    ``first_stage`` (FIRST_STAGE), then, if none of them holds, all the others.  A model whose
+    ``leaf_values[i]`` is None, or that has a leaf its evaluator rejects, is decided by
+    ``reference(i)`` — the reference statement — in its place in the order.  Raises
+    LoweringError when the query cannot be lowered (the caller runs the reference loop)."""
     n = len(leaf_values)
     if n == 0 or query is T.FALSE:
         return None
@@ -229,13 +233,18 @@ def choose(query: T.Term, leaf_values: Sequence[Optional[LeafValues]],
     else:
         leaves, program = explicit_program(query)
     t = lap("lower", t0)
-    stages = [(0, min(k1, n)), (min(k1, n), n)] if 0 < k1 < n else [(0, n)]
+    stages = [(0, k1), (k1, n)] if 0 < k1 < n else [(0, n)]
     if engine is None and program is not None:
         from .engine import get_engine
 
         engine = get_engine()
     choice, host, launches, on_engine_n, t = _stages(stages, leaves, program, leaf_values, reference,
                                                      engine, lap, t)
+    _account(choice, host, launches, on_engine_n, phases)
+    return choice
+
+
+def _account(choice, host, launches, on_engine_n, phases) -> None:
     with _STATS_LOCK:
         STATS.queries += 1
         STATS.hits += choice is not None
@@ -244,7 +253,6 @@ def choose(query: T.Term, leaf_values: Sequence[Optional[LeafValues]],
         STATS.models_host += host
         for k, v in phases.items():
             STATS.phase_s[k] = STATS.phase_s.get(k, 0.0) + v
-    return choice
 
 
 def _stages(stages, leaves, program, leaf_values, reference, engine, lap, t):

@@ -63,8 +63,11 @@ def _check_stream(ns, models, queries):
     return picks
 
 
-def test_quick_sat_choice_matches_reference_loop(standin, monkeypatch):
+@pytest.mark.parametrize("first_stage", [0, 4])
+def test_quick_sat_choice_matches_reference_loop(standin, monkeypatch, first_stage):
+    """first_stage 0: every model in one launch; 4: the production two-launch setting."""
     oracle_engine.install(monkeypatch)
+    monkeypatch.setattr(MC, "FIRST_STAGE", first_stage)
     models, queries, _, _ = W.build(z3, standin, n_models=100, n_scenarios=6, n_queries=30)
     assert len(models) == 100
     picks = _check_stream(standin, models, queries)
@@ -74,6 +77,7 @@ def test_quick_sat_choice_matches_reference_loop(standin, monkeypatch):
 
 def test_quick_sat_small_caches_and_empty(standin, monkeypatch):
     oracle_engine.install(monkeypatch)
+    monkeypatch.setattr(MC, "FIRST_STAGE", 0)
     models, queries, _, _ = W.build(z3, standin, n_models=12, n_scenarios=3, n_queries=12)
     _run_both(standin, models, queries)
     gpu = MC.gpu_model_cache_class()()
@@ -95,6 +99,7 @@ def test_quick_sat_literal_true_and_false(standin, monkeypatch):
 
 def test_leaf_values_are_memoised_per_model(standin, monkeypatch):
     oracle_engine.install(monkeypatch)
+    monkeypatch.setattr(MC, "FIRST_STAGE", 0)
     x = z3.BitVec("x", 256)
     A = z3.Array("A", z3.BitVecSort(256), z3.BitVecSort(256))
     zm = z3.ModelRef({x.decl(): 5, A.decl(): ({5: 7}, 1)})
@@ -113,6 +118,7 @@ def test_leaf_values_are_memoised_per_model(standin, monkeypatch):
 def test_a_model_the_leaves_cannot_value_goes_to_the_reference_statement(standin, monkeypatch):
     """A z3 model whose eval rejects a leaf is decided by deepcopy + eval in its place."""
     oracle_engine.install(monkeypatch)
+    monkeypatch.setattr(MC, "FIRST_STAGE", 0)
 
     class Picky(z3.ModelRef):
         def __deepcopy__(self, memo):
@@ -193,7 +199,9 @@ def test_install_rebinds_the_funnel_cache(standin):
 
 
 @pytest.mark.gpu
-def test_gpu_quick_sat_choice_matches_reference_loop(standin, engine):
+@pytest.mark.parametrize("first_stage", [0, 4])
+def test_gpu_quick_sat_choice_matches_reference_loop(standin, engine, monkeypatch, first_stage):
+    monkeypatch.setattr(MC, "FIRST_STAGE", first_stage)
     models, queries, _, _ = W.build(z3, standin, n_models=100, n_scenarios=8, n_queries=60)
     _check_stream(standin, models, queries)
 
