@@ -54,6 +54,9 @@ def parse(argv=None):
                     help="one waited pf_check_batch call per step instead of all K enqueued at once")
     ap.add_argument("--corpus-scenarios", type=int, default=48,
                     help="LASER-shaped scenarios for the %% discharged half of the metric (0 = skip)")
+    ap.add_argument("--full-pass-dags", type=int, default=1_000_000,
+                    help="config 3 as specified: one pass over this many DAGs (0 = skip; N = 1 only)")
+    ap.add_argument("--full-pass-workers", type=int, default=16)
     ap.add_argument("--quick-sat-queries", type=int, default=120,
                     help="queries of the quick-sat (100 cached models) and funnel legs (0 = skip)")
     return ap.parse_args(argv)
@@ -220,6 +223,27 @@ def discharge(args):
             "queries_per_s_terms_known": n / max(t_rep, 1e-9), "phase_s_terms_known": phase_rep,
             "corpus": f"mythril_amd/corpus.py, {args.corpus_scenarios} planted 2-tx scenarios "
                       f"(config-2 substitute: no z3/solc for --solver-log dumps)"}
+
+
+def full_pass_leg(args, eng):
+    """BASELINE config 3 as specified: ONE pass over the 1,000,000 DAGs ×
+    65,536 candidates, full sweep (plus the planted early-exit pass over the same ids), the
+    host workers generating and lowering the next chunks while the device sweeps
+    (tools/full_pass.py).  Two rates: over the kernel time (inputs resident, the headline's
+    definition) and over the wall time (host generation included)."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import full_pass
+
+    gc.collect()
+    res = full_pass.run_full_pass(eng, dags=args.full_pass_dags, workers=args.full_pass_workers,
+                                  budget=args.budget, seed=args.seed, mp_context="spawn")
+    fs = res["full_sweep"]
+    return {"dags": res["dags"], "candidates_per_dag": res["candidates_per_dag"],
+            "evals": fs["evals_full"], "kernel_s": fs["kernel_s"], "wall_s": res["total_wall_s"],
+            "evals_per_s_kernel": fs["evals_per_s_kernel"], "evals_per_s_wall": fs["evals_per_s_wall"],
+            "sets_with_witness": fs["sets_with_witness"], "chunks": fs["chunks"],
+            "host_wait_s": res["host_wait_s"], "host_workers": res["host_workers"],
+            "planted_early_exit": res["planted_early_exit"], "seeds": res["seeds"]}
 
 
 def quick_sat_leg(args):
@@ -536,6 +560,8 @@ def run(args, rank, world, local, dist, engine=None, cdev="cuda"):
             line["discharge"] = discharge(args)
         if args.quick_sat_queries > 0:
             line["quick_sat"] = quick_sat_leg(args)
+        if args.full_pass_dags > 0 and world == 1:
+            line["full_pass"] = full_pass_leg(args, eng)
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(step_progs[args.warmup], args.budget, args.seed,
                                                 args.cpu_sample_s)

@@ -204,7 +204,7 @@ def eval_rows(program, rows: Sequence[bytes], engine=None) -> np.ndarray:
 # model, bumped to the front by the query before) — computing every model's leaves for such a
 # query would cost more than the loop it replaces.  The others go in a second launch.
 # (Deciding only the newest model on the host first measured slower: it held for 24 of 121
-# profile queries, profiles/r05g_quick_sat.jsonl.)
+# profile queries, profiles/r05g_quick_sat_hostfirst.jsonl.)
 FIRST_STAGE = 4
 
 

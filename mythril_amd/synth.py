@@ -13,6 +13,7 @@ disjunction for the caller, callvalue checks) — used until real --solver-log d
 
 from __future__ import annotations
 
+import bisect
 from typing import List, Optional, Tuple
 
 import numpy as np
@@ -30,6 +31,9 @@ _MIX = [
     ("logic", 0.10), ("shift", 0.05), ("itecmp", 0.10),
 ]
 _BOUNDARY = [0, 1, 2, ir.mask(256), 1 << 255, (1 << 160) - 1]
+_MIX_OPS = [m[0] for m in _MIX]
+_MIX_CDF = [float(x) for x in (lambda c: c / c[-1])(np.cumsum(np.array([m[1] for m in _MIX]) /
+                                                             sum(m[1] for m in _MIX)))]
 
 
 def _boundary(rng) -> int:
@@ -113,9 +117,7 @@ def random_dag_set(dag_id: int, n_interior: int = 48, depth: int = 32, window: i
         c = _leaf_value(rng)
         leaves.append((dag.const(c, 256), c))
     interior: List[Tuple[int, int]] = []
-    ops = [m[0] for m in _MIX]
-    probs = np.array([m[1] for m in _MIX])
-    probs = probs / probs.sum()
+    ops = _MIX_OPS
 
     def pick(first: bool):
         if first and interior and len(interior) <= depth:
@@ -126,7 +128,9 @@ def random_dag_set(dag_id: int, n_interior: int = 48, depth: int = 32, window: i
         return leaves[int(rng.integers(0, len(leaves)))]
 
     for _ in range(n_interior):
-        kind = ops[int(rng.choice(len(ops), p=probs))]
+        # = rng.choice(len(ops), p=probs): numpy draws one double and searches the
+        # normalised cumulative sum (side="right") — the same stream, 20x cheaper per call
+        kind = ops[bisect.bisect_right(_MIX_CDF, rng.random())]
         a, va = pick(True)
         b, vb = pick(False)
         if kind == "div":

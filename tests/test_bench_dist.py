@@ -14,7 +14,7 @@ import numpy as np
 import torch.multiprocessing as mp
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ARGV = ["--sets", "3", "--budget", "64", "--steps", "2", "--warmup", "1", "--keccak-log2", "0", "--quick-sat-queries", "0",
+ARGV = ["--sets", "3", "--budget", "64", "--steps", "2", "--warmup", "1", "--keccak-log2", "0", "--quick-sat-queries", "0", "--full-pass-dags", "0",
         "--corpus-scenarios", "0", "--no-cpu-baseline", "--seed", "5"]
 
 

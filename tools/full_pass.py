@@ -59,41 +59,38 @@ def _arrays_batch(arrs, n):
     return b
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--dags", type=int, default=1_000_000)
-    ap.add_argument("--chunk", type=int, default=65536)
-    ap.add_argument("--piece", type=int, default=2048, help="DAGs per worker task")
-    ap.add_argument("--workers", type=int, default=16)
-    ap.add_argument("--budget", type=int, default=65536)
-    ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--out", default=None)
-    args = ap.parse_args()
+def run_full_pass(eng, dags: int = 1_000_000, chunk: int = 65536, piece: int = 2048, workers: int = 16,
+                  budget: int = 65536, seed: int = 0, progress=None, mp_context=None) -> dict:
+    """The full pass over DAG ids [0, dags) on ``eng``; returns the result dict.  The host
+    workers (``mp_context``: "spawn" when the caller has already initialised the GPU) build
+    the packed batches while the device sweeps the previous chunk."""
+    import multiprocessing as mp
 
     import numpy as np
 
     from mythril_amd import ir
-    from mythril_amd.engine import Engine
 
-    # the workers are forked before this process touches the GPU
-    pool = ProcessPoolExecutor(args.workers)
-    list(pool.map(_build, [(0, 1)] * args.workers))
-    eng = Engine(0)
+    ctx = mp.get_context(mp_context) if mp_context else None
+    pool = ProcessPoolExecutor(workers, mp_context=ctx)
+    list(pool.map(_build, [(0, 1)] * workers))
     t_wall = time.perf_counter()
-    res = {"dags": args.dags, "candidates_per_dag": args.budget,
+    res = {"dags": dags, "candidates_per_dag": budget,
            "seeds": "DAG generator 20260101 (Philox key (seed << 32) | dag_id), candidate key "
                     "0x4D595448 ^ dag_id (global seed 0)"}
     legs = {"full_sweep": (0, 0), "planted_early_exit": (1, ir.FLAG_EARLY_EXIT | ir.FLAG_SHORTCIRCUIT)}
     acc = {k: dict(kernel_ms=0.0, evals=0, decided=0, sat=0) for k in legs}
     chunks = 0
+    t_wait = 0.0   # wall time the device loop spent waiting for the host workers
     with pool:
-        tasks = [(f, min(args.piece, args.dags - f)) for f in range(0, args.dags, args.piece)]
+        tasks = [(f, min(piece, dags - f)) for f in range(0, dags, piece)]
         futs = [pool.submit(_build, t) for t in tasks]
         pending, n_pending = [], 0
         for i, fu in enumerate(futs):
+            tw = time.perf_counter()
             pending.append(fu.result())
+            t_wait += time.perf_counter() - tw
             n_pending += pending[-1][1]
-            if n_pending < args.chunk and i + 1 < len(futs):
+            if n_pending < chunk and i + 1 < len(futs):
                 continue
             chunks += 1
             for leg, (which, flags) in legs.items():
@@ -114,15 +111,16 @@ def main():
                     oc += len(c); ok += len(k); os_ += len(s_); op += len(p)
                 arrs = tuple(np.concatenate(x) for x in (codes, consts, schemas, parents, descs))
                 db = eng.upload(_arrays_batch(arrs, n_pending))
-                r = eng.check(db, budget=args.budget, seed=args.seed, flags=flags)
+                r = eng.check(db, budget=budget, seed=seed, flags=flags)
                 db.free()
                 a = acc[leg]
                 a["kernel_ms"] += r.kernel_ms
                 a["evals"] += r.evals_full
                 a["decided"] += r.cands_decided
                 a["sat"] += int(r.sat.sum())
-                print(json.dumps({"leg": leg, "chunk": chunks, "sets": n_pending,
-                                  "kernel_ms": r.kernel_ms, "sat": int(r.sat.sum())}), flush=True)
+                if progress is not None:
+                    progress({"leg": leg, "chunk": chunks, "sets": n_pending,
+                              "kernel_ms": r.kernel_ms, "sat": int(r.sat.sum())})
             pending, n_pending = [], 0
     for leg, a in acc.items():
         ks = a["kernel_ms"] / 1e3
@@ -130,9 +128,31 @@ def main():
         res[leg] = {"kernel_s": ks, "chunks": chunks, "evals_full": a["evals"],
                     "cands_decided": a["decided"], "sets_with_witness": a["sat"],
                     "evals_per_s_kernel": units / ks if ks else None,
-                    "set_verdicts_per_s_kernel": args.dags / ks if ks else None}
+                    "set_verdicts_per_s_kernel": dags / ks if ks else None}
     res["total_wall_s"] = time.perf_counter() - t_wall
+    res["host_wait_s"] = t_wait
+    res["host_workers"] = workers
     res["full_sweep"]["evals_per_s_wall"] = res["full_sweep"]["evals_full"] / res["total_wall_s"]
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--dags", type=int, default=1_000_000)
+    ap.add_argument("--chunk", type=int, default=65536)
+    ap.add_argument("--piece", type=int, default=2048, help="DAGs per worker task")
+    ap.add_argument("--workers", type=int, default=16)
+    ap.add_argument("--budget", type=int, default=65536)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+
+    from mythril_amd.engine import Engine
+
+    # the workers are started (spawned) by run_full_pass; this process owns the GPU
+    eng = Engine(0)
+    res = run_full_pass(eng, args.dags, args.chunk, args.piece, args.workers, args.budget, args.seed,
+                        progress=lambda d: print(json.dumps(d), flush=True), mp_context="spawn")
     line = json.dumps(res)
     print(line, flush=True)
     if args.out:
