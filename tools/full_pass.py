@@ -80,7 +80,40 @@ def run_full_pass(eng, dags: int = 1_000_000, chunk: int = 65536, piece: int = 2
     legs = {"full_sweep": (0, 0), "planted_early_exit": (1, ir.FLAG_EARLY_EXIT | ir.FLAG_SHORTCIRCUIT)}
     acc = {k: dict(kernel_ms=0.0, evals=0, decided=0, sat=0) for k in legs}
     chunks = 0
-    t_wait = 0.0   # wall time the device loop spent waiting for the host workers
+    t_wait = 0.0   # wall time the packing loop spent waiting for the host workers
+    # the device runs on its own thread (the engine's calls release the GIL): chunk k is
+    # uploaded and swept while this thread waits for and packs chunk k + 1
+    import queue
+    import threading
+
+    todo: "queue.Queue" = queue.Queue(maxsize=2)
+    errors: list = []
+
+    def device_loop():
+        while True:
+            item = todo.get()
+            if item is None:
+                return
+            k, n, packed = item
+            try:
+                for leg, (which, flags) in legs.items():
+                    db = eng.upload(_arrays_batch(packed[which], n))
+                    r = eng.check(db, budget=budget, seed=seed, flags=flags)
+                    db.free()
+                    a = acc[leg]
+                    a["kernel_ms"] += r.kernel_ms
+                    a["evals"] += r.evals_full
+                    a["decided"] += r.cands_decided
+                    a["sat"] += int(r.sat.sum())
+                    if progress is not None:
+                        progress({"leg": leg, "chunk": k, "sets": n, "kernel_ms": r.kernel_ms,
+                                  "sat": int(r.sat.sum())})
+            except Exception as e:  # noqa: BLE001 - reported by the packing thread
+                errors.append(e)
+                return
+
+    dev = threading.Thread(target=device_loop, daemon=True)
+    dev.start()
     with pool:
         tasks = [(f, min(piece, dags - f)) for f in range(0, dags, piece)]
         futs = [pool.submit(_build, t) for t in tasks]
@@ -93,7 +126,8 @@ def run_full_pass(eng, dags: int = 1_000_000, chunk: int = 65536, piece: int = 2
             if n_pending < chunk and i + 1 < len(futs):
                 continue
             chunks += 1
-            for leg, (which, flags) in legs.items():
+            packed = []
+            for which in (0, 1):
                 codes, consts, schemas, parents, descs = [], [], [], [], []
                 oc = ok = os_ = op = 0
                 for (_, nn, both) in pending:
@@ -109,19 +143,20 @@ def run_full_pass(eng, dags: int = 1_000_000, chunk: int = 65536, piece: int = 2
                     s_[sp, 3] += op
                     codes.append(c); consts.append(k); schemas.append(s_); parents.append(p); descs.append(d)
                     oc += len(c); ok += len(k); os_ += len(s_); op += len(p)
-                arrs = tuple(np.concatenate(x) for x in (codes, consts, schemas, parents, descs))
-                db = eng.upload(_arrays_batch(arrs, n_pending))
-                r = eng.check(db, budget=budget, seed=seed, flags=flags)
-                db.free()
-                a = acc[leg]
-                a["kernel_ms"] += r.kernel_ms
-                a["evals"] += r.evals_full
-                a["decided"] += r.cands_decided
-                a["sat"] += int(r.sat.sum())
-                if progress is not None:
-                    progress({"leg": leg, "chunk": chunks, "sets": n_pending,
-                              "kernel_ms": r.kernel_ms, "sat": int(r.sat.sum())})
+                packed.append(tuple(np.concatenate(x) for x in (codes, consts, schemas, parents, descs)))
+            while not errors:
+                try:
+                    todo.put((chunks, n_pending, packed), timeout=1.0)
+                    break
+                except queue.Full:
+                    continue
+            if errors:
+                break
             pending, n_pending = [], 0
+    todo.put(None)
+    dev.join()
+    if errors:
+        raise errors[0]
     for leg, a in acc.items():
         ks = a["kernel_ms"] / 1e3
         units = a["evals"] if leg == "full_sweep" else a["decided"]
