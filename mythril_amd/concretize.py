@@ -15,6 +15,7 @@ replacement — is hashed on demand), so the output string is identical to the r
 
 from __future__ import annotations
 
+import os
 from functools import lru_cache
 from typing import Callable, Dict, List, Optional, Sequence
 
@@ -30,25 +31,21 @@ def _batch_keccak(messages: Sequence[bytes]) -> List[bytes]:
     return get_engine().keccak256(list(messages))
 
 
-def get_concrete_hash_data(kfm: KeccakFunctionManager, model) -> Dict[int, List[int]]:
-    """keccak_function_manager.py:132-148: model values of every symbolic hash, by size."""
-    out: Dict[int, List[int]] = {}
-    for size, vals in kfm.hash_result_store.items():
-        out[size] = []
-        for val in vals:
-            ev = model.eval(val.raw)
-            try:
-                out[size].append(ev.as_long())
-            except AttributeError:
-                continue
-    return out
+def get_concrete_hash_data(kfm, model) -> Dict[int, List[int]]:
+    """keccak_function_manager.py:132-148: model values of every symbolic hash, by size (the
+    manager's own method: Mythril's or the mirror's)."""
+    return kfm.get_concrete_hash_data(model)
 
 
 def replace_with_actual_sha(concrete_transactions: List[Dict[str, str]], model, code=None,
                             kfm: Optional[KeccakFunctionManager] = None,
-                            hasher: Callable[[Sequence[bytes]], List[bytes]] = _batch_keccak) -> None:
-    """Mirror of ``_replace_with_actual_sha`` (analysis/solver.py:129-165), batched."""
+                            hasher: Callable[[Sequence[bytes]], List[bytes]] = _batch_keccak,
+                            bvv=None) -> None:
+    """Mirror of ``_replace_with_actual_sha`` (analysis/solver.py:129-165), batched.  ``kfm``
+    and ``bvv`` (the ``BitVecVal`` constructor its functions take) default to this package's
+    facade; the live seam passes Mythril's own (:func:`live_replace_with_actual_sha`)."""
     kfm = kfm or keccak_function_manager
+    bvv = bvv or symbol_factory.BitVecVal
     concrete_hashes = get_concrete_hash_data(kfm, model)
     inverse_of = {}
 
@@ -62,7 +59,7 @@ def replace_with_actual_sha(concrete_transactions: List[Dict[str, str]], model, 
             if value not in concrete_hashes[size]:
                 continue
             _, inverse = kfm.store_function[size]
-            arg = symbol_factory.BitVecVal(value, 256)
+            arg = bvv(value, 256)
             res = (size, model.eval(inverse(arg).raw).as_long() & ((1 << size) - 1))
         inverse_of[value] = res
         return res
@@ -112,6 +109,30 @@ def replace_with_actual_sha(concrete_transactions: List[Dict[str, str]], model, 
             hex_keccak = table[m].hex().rjust(64, "0")
             tx["input"] = tx["input"][:s_index] + tx["input"][s_index:].replace(
                 tx["input"][i:64 + i], hex_keccak)
+
+
+# preimages per call from which the GPU kernel hashes them (one launch); fewer go to the host
+# Keccak Mythril already uses (eth_hash through support_utils.sha3, keccak_function_manager.py:
+# 57-69): a launch costs tens of microseconds, eth_hash one or two per 64-byte message
+# (profiles/r05_keccak_latency.json)
+GPU_MIN = int(os.environ.get("PF_KECCAK_GPU_MIN", "32"))
+
+
+def live_replace_with_actual_sha(concrete_transactions: List[Dict[str, str]], model, code=None) -> None:
+    """The drop-in for ``mythril.analysis.solver._replace_with_actual_sha`` (installed by
+    integration.install): the batched concretisation over Mythril's own keccak function
+    manager and ``symbol_factory``; the preimages of a call are hashed in one GPU launch
+    when there are ``GPU_MIN`` or more of them, else by Mythril's host ``sha3``."""
+    from mythril.laser.ethereum.function_managers import keccak_function_manager as kfm
+    from mythril.laser.smt import symbol_factory as sf
+    from mythril.support.support_utils import sha3
+
+    def hasher(msgs: Sequence[bytes]) -> List[bytes]:
+        if len(msgs) >= GPU_MIN:
+            return _batch_keccak(msgs)
+        return [bytes(sha3(m)) for m in msgs]
+
+    replace_with_actual_sha(concrete_transactions, model, code, kfm=kfm, hasher=hasher, bvv=sf.BitVecVal)
 
 
 @lru_cache(maxsize=2 ** 10)

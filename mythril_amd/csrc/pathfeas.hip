@@ -1155,19 +1155,44 @@ int pf_keccak256_batch(const uint8_t* data, const uint64_t* offsets, size_t n, u
         if (offsets[i + 1] < offsets[i]) return fail("keccak: offsets not monotone at %zu", i);
     const uint64_t total = offsets[n];
     if (switch_stream(D, st)) return -1;
-    DevBuf b_data, b_off, b_out;
-    HIPCHK(hipMalloc(&b_data.p, total ? total : 8));
-    HIPCHK(hipMalloc(&b_off.p, (n + 1) * 8));
-    HIPCHK(hipMalloc(&b_out.p, n * 32));
-    uint8_t *d_data = b_data.as<uint8_t>(), *d_out = b_out.as<uint8_t>();
-    uint64_t* d_off = b_off.as<uint64_t>();
-    if (total) HIPCHK(hipMemcpyAsync(d_data, data, total, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(d_off, offsets, (n + 1) * 8, hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(pf_keccak_var_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st,
-                       d_data, d_off, (uint64_t)n, d_out);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(out32, d_out, n * 32, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+    // one pooled block [offsets | messages | digests] and one copy each way through the
+    // pinned staging buffer (a concretisation call hashes a handful of preimages: three
+    // hipMalloc / hipFree pairs and pageable copies were most of its latency)
+    auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+    const size_t o_off = 0, o_data = al((n + 1) * 8), o_out = o_data + al(total ? total : 8),
+                 all = o_out + n * 32;
+    size_t cap = 0;
+    uint8_t* dm = static_cast<uint8_t*>(pool_acquire(D, all, &cap));
+    if (!dm) return fail("pf_keccak256_batch: hipMalloc(%zu) failed", all);
+    uint8_t* pin = pinned_staging(std::max<size_t>(o_out, n * 32));
+    int rc = 0;
+    if (pin) {
+        memcpy(pin + o_off, offsets, (n + 1) * 8);
+        if (total) memcpy(pin + o_data, data, total);
+        if (hipMemcpyAsync(dm, pin, o_data + total, hipMemcpyHostToDevice, st) != hipSuccess) rc = -1;
+    } else if (hipMemcpyAsync(dm + o_off, offsets, (n + 1) * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+               (total && hipMemcpyAsync(dm + o_data, data, total, hipMemcpyHostToDevice, st) != hipSuccess)) {
+        rc = -1;
+    }
+    if (!rc) {
+        hipLaunchKernelGGL(pf_keccak_var_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st,
+                           dm + o_data, reinterpret_cast<const uint64_t*>(dm + o_off), (uint64_t)n, dm + o_out);
+        if (hipGetLastError() != hipSuccess ||
+            hipMemcpyAsync(pin ? static_cast<void*>(pin) : static_cast<void*>(out32), dm + o_out, n * 32,
+                           hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            rc = -1;
+    }
+    if (rc) {
+        if (hipDeviceSynchronize() == hipSuccess) hipFree(dm);
+        return fail("pf_keccak256_batch: HIP call failed");
+    }
+    if (pin) memcpy(out32, pin, n * 32);
+    if (D->pool.size() >= kPoolBlocks) {
+        hipFree(D->pool.front().first);
+        D->pool.erase(D->pool.begin());
+    }
+    D->pool.emplace_back(dm, cap);
     return 0;
 }
 

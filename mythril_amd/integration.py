@@ -349,8 +349,9 @@ def discharge_ratio() -> Optional[float]:
 
 
 def install() -> None:
-    """Rebind the funnel's Optimize (support/model.py:13 binds it by value at import) and its
-    ``model_cache`` (support/model.py:20; ``PF_MODEL_CACHE=0`` keeps the reference's).  The
+    """Rebind the funnel's Optimize (support/model.py:13 binds it by value at import), its
+    ``model_cache`` (support/model.py:20; ``PF_MODEL_CACHE=0`` keeps the reference's) and the
+    report's keccak concretisation (``mythril.analysis.solver._replace_with_actual_sha``).  The
     analysis process does not use torch, so the engine is loaded without it (PF_TORCH=0,
     mythril_amd/_lib.py) unless the caller chose otherwise.
 
@@ -365,6 +366,16 @@ def install() -> None:
         os.environ.setdefault("PF_DEVICES", "all")
 
     funnel.Optimize = gpu_optimize_class()
+    try:
+        # keccak concretisation of reported transaction sequences (analysis/solver.py:129-165,
+        # resolved at call time by get_transaction_sequence): batched, GPU for large batches
+        import mythril.analysis.solver as report_solver
+
+        from .concretize import live_replace_with_actual_sha
+
+        report_solver._replace_with_actual_sha = live_replace_with_actual_sha
+    except ImportError:  # pragma: no cover - a Mythril without the analysis package
+        pass
     if os.environ.get("PF_MODEL_CACHE", "1") != "0":
         # the quick-sat loop before every objective-free query (support/model.py:95-98) as
         # one engine call over the cached models (mythril_amd/model_cache.py)

@@ -30,14 +30,17 @@ def keccak256_bytes(data: bytes) -> bytes:
 
 
 class KeccakFunctionManager:
+    hash_matcher = "fffffff"  # :36, the interval prefix as it shows in calldata hex
+
     def __init__(self, registry: UFRegistry = DEFAULT_REGISTRY):
         self.registry = registry
+        self._index_counter = TOTAL_PARTS - 34534
         self.reset()
 
     def reset(self):
+        # as the reference's reset (:48-54): the interval counter keeps counting
         self.store_function: Dict[int, Tuple[Function, Function]] = {}
         self.interval_hook_for_size: Dict[int, int] = {}
-        self._index_counter = TOTAL_PARTS - 34534
         self.hash_result_store: Dict[int, List[BitVec]] = {}
         self.quick_inverse: Dict[BitVec, BitVec] = {}
         self.concrete_hashes: Dict[BitVec, BitVec] = {}
@@ -48,6 +51,18 @@ class KeccakFunctionManager:
     def find_concrete_keccak(data: BitVec) -> BitVec:
         digest = keccak256_bytes(data.value.to_bytes(data.size() // 8, byteorder="big"))
         return symbol_factory.BitVecVal(int.from_bytes(digest, "big"), 256)
+
+    def get_concrete_hash_data(self, model) -> Dict[int, List[int]]:
+        """:132-148: the model's value of every symbolic hash, by input size."""
+        out: Dict[int, List[int]] = {}
+        for size, vals in self.hash_result_store.items():
+            out[size] = []
+            for val in vals:
+                try:
+                    out[size].append(model.eval(val.raw).as_long())
+                except AttributeError:
+                    continue
+        return out
 
     def get_function(self, length: int) -> Tuple[Function, Function]:
         try:

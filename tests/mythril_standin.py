@@ -51,7 +51,14 @@ MODULES = (
     "mythril.laser.ethereum.state.constraints", "mythril.laser.plugin",
     "mythril.laser.plugin.builder", "mythril.laser.plugin.interface",
     "mythril.laser.plugin.loader", "mythril.plugin", "mythril.plugin.interface",
-    "mythril.plugin.discovery", "mythril.plugin.loader")
+    "mythril.plugin.discovery", "mythril.plugin.loader", "mythril.analysis", "mythril.analysis.solver")
+
+
+def host_sha3(value):
+    """support_utils.sha3 (eth_hash) stand-in: the oracle's Keccak-256 (test infrastructure)."""
+    import pyoracle
+
+    return pyoracle.keccak256(bytes(value))
 
 
 def build(z3, installed_plugins=None):
@@ -504,6 +511,49 @@ def build(z3, installed_plugins=None):
                 plugin = PluginDiscovery().build_plugin(
                     plugin_name, self.plugin_args.get(plugin_name, {}))
                 self.load(plugin)
+
+    # ---- analysis/solver.py:129-165 (_replace_with_actual_sha), resolving the keccak
+    # manager and symbol_factory through their modules at call time like the reference's
+    # module globals; get_transaction_sequence calls it by its module-global name ----------
+    def _replace_with_actual_sha(concrete_transactions, model, code=None):
+        keccak_function_manager = mods["mythril.laser.ethereum.function_managers"].keccak_function_manager
+        symbol_factory = mods["mythril.laser.smt"].symbol_factory
+        concrete_hashes = keccak_function_manager.get_concrete_hash_data(model)
+        for tx in concrete_transactions:
+            if keccak_function_manager.hash_matcher not in tx["input"]:
+                continue
+            if code is not None and code.bytecode in tx["input"]:
+                s_index = len(code.bytecode) + 2
+            else:
+                s_index = 10
+            for i in range(s_index, len(tx["input"])):
+                data_slice = tx["input"][i: i + 64]
+                if keccak_function_manager.hash_matcher not in data_slice or len(data_slice) != 64:
+                    continue
+                find_input = symbol_factory.BitVecVal(int(data_slice, 16), 256)
+                input_ = None
+                for size in concrete_hashes:
+                    _, inverse = keccak_function_manager.store_function[size]
+                    if find_input.value not in concrete_hashes[size]:
+                        continue
+                    input_ = symbol_factory.BitVecVal(model.eval(inverse(find_input).raw).as_long(), size)
+                if input_ is None:
+                    continue
+                keccak = keccak_function_manager.find_concrete_keccak(input_)
+                hex_keccak = hex(keccak.value)[2:]
+                if len(hex_keccak) != 64:
+                    hex_keccak = "0" * (64 - len(hex_keccak)) + hex_keccak
+                tx["input"] = tx["input"][:s_index] + tx["input"][s_index:].replace(
+                    tx["input"][i: 64 + i], hex_keccak)
+
+    def get_transaction_sequence_tail(concrete_transactions, model, code=None):
+        """The concretisation step of get_transaction_sequence (analysis/solver.py:96-99)."""
+        mods["mythril.analysis.solver"]._replace_with_actual_sha(concrete_transactions, model, code)
+        return concrete_transactions
+
+    mods["mythril.analysis.solver"]._replace_with_actual_sha = _replace_with_actual_sha
+    mods["mythril.analysis.solver"].get_transaction_sequence_tail = get_transaction_sequence_tail
+    mods["mythril.support.support_utils"].sha3 = host_sha3
 
     mods["mythril.laser.plugin.builder"].PluginBuilder = PluginBuilder
     mods["mythril.laser.plugin.interface"].LaserPlugin = LaserPlugin

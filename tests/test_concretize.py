@@ -69,3 +69,59 @@ def test_gpu_concretisation_and_code_hash(engine):
     assert concretize.get_code_hash(code) == "0x" + O.keccak256(bytes.fromhex(code[2:])).hex()
     assert concretize.code_hashes([code, "0x", "zz"]) == [
         "0x" + O.keccak256(bytes.fromhex(code[2:])).hex(), "0x" + O.keccak256(b"").hex(), ""]
+
+
+def _live_scenario(monkeypatch, gpu_min):
+    """The stand-in Mythril with the report's concretisation step (analysis/solver.py:96-99
+    -> :129-165, restated in tests/mythril_standin.py) over the facade keccak manager."""
+    import copy
+    import sys
+    import types
+
+    import fake_z3
+    import mythril_standin
+    from mythril_amd import integration
+
+    mythril_standin.install(monkeypatch, fake_z3)
+    monkeypatch.setattr(concretize, "GPU_MIN", gpu_min)
+    kfm, model, h = _model_with(4321)
+    kfm2, model2, h2 = _model_with(77)
+    mods = sys.modules
+    monkeypatch.setattr(mods["mythril.laser.ethereum.function_managers"], "keccak_function_manager", kfm)
+    monkeypatch.setattr(mods["mythril.laser.smt"], "symbol_factory", symbol_factory, raising=False)
+    hv = model.eval(h.raw).as_long()
+    code = types.SimpleNamespace(bytecode="6080604052" + f"{hv:064x}")
+    inputs = ["0xa9059cbb" + f"{hv:064x}" + "00" * 32, "0x12345678" + "00" * 32,
+              "0xdeadbeef" + f"{hv:064x}" * 2, "0x" + code.bytecode + f"{hv:064x}"]
+    sol = mods["mythril.analysis.solver"]
+    want = [{"input": s} for s in inputs]
+    sol.get_transaction_sequence_tail(want, model)
+    want_code = [{"input": inputs[3]}]
+    sol.get_transaction_sequence_tail(want_code, model, code)
+    integration.install()
+    assert sol._replace_with_actual_sha is concretize.live_replace_with_actual_sha
+    got = [{"input": s} for s in inputs]
+    sol.get_transaction_sequence_tail(got, model)
+    got_code = [{"input": inputs[3]}]
+    sol.get_transaction_sequence_tail(got_code, model, code)
+    assert got == want and got_code == want_code
+    hx = O.keccak256((4321).to_bytes(32, "big")).hex()
+    assert want[0]["input"] == "0xa9059cbb" + hx + "00" * 32
+    assert want_code[0]["input"] == "0x" + code.bytecode + hx   # the code part is kept
+    return got
+
+
+@pytest.mark.parametrize("gpu_min", [1, 32])
+def test_installed_concretisation_matches_the_reference(monkeypatch, gpu_min):
+    """integration.install() rebinds mythril.analysis.solver._replace_with_actual_sha; the
+    rebound function rewrites calldata exactly as the reference's does — on the batched
+    kernel path (gpu_min 1; the oracle engine here) and on the host path (32)."""
+    import oracle_engine
+
+    oracle_engine.install(monkeypatch)
+    _live_scenario(monkeypatch, gpu_min)
+
+
+@pytest.mark.gpu
+def test_gpu_installed_concretisation_matches_the_reference(monkeypatch, engine):
+    _live_scenario(monkeypatch, 1)
