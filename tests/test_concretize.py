@@ -111,11 +111,11 @@ def _live_scenario(monkeypatch, gpu_min):
     return got
 
 
-@pytest.mark.parametrize("gpu_min", [1, 32])
+@pytest.mark.parametrize("gpu_min", [1, 192])
 def test_installed_concretisation_matches_the_reference(monkeypatch, gpu_min):
     """integration.install() rebinds mythril.analysis.solver._replace_with_actual_sha; the
     rebound function rewrites calldata exactly as the reference's does — on the batched
-    kernel path (gpu_min 1; the oracle engine here) and on the host path (32)."""
+    kernel path (gpu_min 1; the oracle engine here) and on the host path (192)."""
     import oracle_engine
 
     oracle_engine.install(monkeypatch)
