@@ -114,8 +114,9 @@ def replace_with_actual_sha(concrete_transactions: List[Dict[str, str]], model, 
 # preimages per call from which the GPU kernel hashes them (one launch); fewer go to the host
 # Keccak Mythril already uses (eth_hash through support_utils.sha3, keccak_function_manager.py:
 # 57-69): a launch costs tens of microseconds, eth_hash one or two per 64-byte message
-# (profiles/r05_keccak_latency.json)
-GPU_MIN = int(os.environ.get("PF_KECCAK_GPU_MIN", "32"))
+# (profiles/r05j_keccak_latency.json: 43 us per launch against 0.4 us per message on the
+# host, so the launch wins from ~200 messages on)
+GPU_MIN = int(os.environ.get("PF_KECCAK_GPU_MIN", "192"))
 
 
 def live_replace_with_actual_sha(concrete_transactions: List[Dict[str, str]], model, code=None) -> None:
