@@ -199,6 +199,50 @@ class Z3WitnessView:
         return r
 
 
+# A tx-boundary batch whose prune may not come (the end of a prioritised sequence: whether
+# another sequence follows is only known when its first prune query arrives): the states,
+# and their query keys once computed.  Run by the first funnel query that is one of them.
+_DEFERRED: Dict[str, object] = {"states": None, "keys": None}
+
+
+def defer_batch(open_states) -> None:
+    with _BATCH_LOCK:
+        _DEFERRED["states"] = list(open_states)
+        _DEFERRED["keys"] = None
+
+
+def drop_deferred() -> None:
+    with _BATCH_LOCK:
+        _DEFERRED["states"] = _DEFERRED["keys"] = None
+
+
+def run_deferred(terms: List[T.Term]) -> bool:
+    """Run the deferred batch if ``terms`` (a funnel query) is one of its states' queries —
+    the prune it was kept for has started.  True if it ran."""
+    with _BATCH_LOCK:
+        states, keys = _DEFERRED["states"], _DEFERRED["keys"]
+    if states is None:
+        return False
+    if keys is None:
+        keys = set()
+        for st in states:
+            try:
+                keys.add(_query_key(state_terms(st)))
+            except Exception:  # noqa: BLE001 - such a state goes to z3 in the prune
+                pass
+        with _BATCH_LOCK:
+            if _DEFERRED["states"] is states:
+                _DEFERRED["keys"] = keys
+    if _query_key(terms) not in keys:
+        return False
+    with _BATCH_LOCK:
+        if _DEFERRED["states"] is not states:
+            return False
+        _DEFERRED["states"] = _DEFERRED["keys"] = None
+    batch_open_states(states)
+    return True
+
+
 def _query_key(terms: List[T.Term]) -> Tuple[T.Term, ...]:
     return tuple(t for t in terms if t is not T.TRUE)
 
@@ -270,6 +314,7 @@ def gpu_optimize_class():
                 stats.gpu_attempts += 1
                 try:
                     terms = converter(z3).terms(self.raw.assertions())
+                    run_deferred(terms)
                     internal = _lookup_batch(terms)
                     if internal is None:
                         sync_keccak_registry(keccak_function_manager)
@@ -452,7 +497,8 @@ def prune_follows(svm, tx_index: int) -> bool:
       (svm.py:259): after the last transaction's ``stop_sym_trans`` nothing prunes;
     * with a tx prioritiser (svm.py:235-237) every sequence re-enters the loop at i = 0
       (svm.py:248-250), so a batch after any transaction may feed the next sequence's first
-      prune: always batch.
+      prune (the plugin defers the one at a sequence's end until that prune's first query:
+      after the last sequence none comes).
     A stand-in without these attributes counts as the default ordered loop of unknown
     length (batch)."""
     if not getattr(svm, "use_reachability_check", True) or not svm.open_states:
@@ -499,9 +545,19 @@ def _plugin_classes():
             install()
             self.tx_index = 0          # start_sym_trans calls in the current transaction loop
             self.batches = 0
+            self.deferred = 0
 
             def _batch():
                 if not prune_follows(symbolic_vm, self.tx_index):
+                    return
+                tc = getattr(symbolic_vm, "transaction_count", None)
+                if (getattr(symbolic_vm, "tx_strategy", None) is not None and self.tx_index > 0 and tc
+                        and self.tx_index % tc == 0):
+                    # the end of a prioritised sequence: a prune follows only if another
+                    # sequence does, which the strategy's iterator does not tell — the batch
+                    # waits for that prune's first query (run_deferred)
+                    defer_batch(symbolic_vm.open_states)
+                    self.deferred += 1
                     return
                 try:
                     n = batch_open_states(symbolic_vm.open_states)
@@ -519,6 +575,11 @@ def _plugin_classes():
             @symbolic_vm.laser_hook("start_sym_trans")
             def _count():
                 self.tx_index += 1
+                drop_deferred()        # the prune a deferred batch was kept for has passed
+
+            @symbolic_vm.laser_hook("stop_execute_transactions")
+            def _done():
+                drop_deferred()
 
             @symbolic_vm.laser_hook("stop_sym_trans")
             def _before_next_prune():

@@ -204,11 +204,26 @@ def test_transactions_already_executed(standin, monkeypatch):
 
 def test_prioritised_sequences_feed_the_next_sequence(standin, monkeypatch):
     """With a tx prioritiser every sequence re-enters the loop at i = 0 (svm.py:235-237,
-    248-250): the last stop_sym_trans of one sequence feeds the next sequence's first prune,
-    so it batches too."""
-    svm, plugin, _ = _run(standin, monkeypatch, transaction_count=1, tx_strategy=object(),
-                          sequences=2)
-    assert [e[0] for e in svm.events] == ["batch", "prune", "batch", "prune", "batch"]
+    248-250): the batch for the next sequence's first prune is deferred at a sequence's end
+    and run by that prune's first query — and after the last sequence, where no prune
+    follows, it never runs."""
+    svm, plugin, hits = _run(standin, monkeypatch, transaction_count=1, tx_strategy=object(),
+                             sequences=2)
+    assert [e[0] for e in svm.events] == ["batch", "prune", "prune", "batch"]
+    assert plugin.deferred == 2 and plugin.batches == 1
+    # the deferred batch covered the second prune's states and answered its queries
+    assert svm.events[3][1] == svm.events[2][2]
+    assert sum(hits) == 2 + 4
+    assert integration._DEFERRED["states"] is None
+
+
+def test_prioritised_sequences_within_a_sequence_batch_at_once(standin, monkeypatch):
+    """Inside a prioritised sequence (i < transaction_count - 1) the next prune is certain:
+    the batch runs at stop_sym_trans, as in the ordered loop."""
+    svm, plugin, _ = _run(standin, monkeypatch, transaction_count=2, tx_strategy=object(),
+                          sequences=1)
+    assert [e[0] for e in svm.events] == ["batch", "prune", "batch", "prune"]
+    assert plugin.deferred == 1 and plugin.batches == 2
 
 
 def test_prune_follows_rules():
