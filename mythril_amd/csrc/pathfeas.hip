@@ -1214,6 +1214,12 @@ int pf_keccak256_fixed_dev(const uint8_t* d_data, uint32_t len, size_t n, uint8_
                            st, d_data, (uint64_t)n, d_out32);
     } else
 #endif
+#ifdef PF_KECCAK_ILP2
+    if (fast)
+        hipLaunchKernelGGL(pf_keccak_fixed2_kernel, dim3((uint32_t)(((n + 1) / 2 + 255) / 256)), dim3(256), 0,
+                           st, d_data, len, (uint64_t)n, d_out32);
+    else
+#endif
     if (fast)
         hipLaunchKernelGGL(pf_keccak_fixed_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0,
                            st, d_data, len, (uint64_t)n, d_out32);

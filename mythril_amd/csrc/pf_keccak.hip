@@ -267,6 +267,48 @@ pf_keccak_fixed64_persist_kernel(const uint8_t* __restrict__ data, uint64_t n, u
     keccak_persist<4>(data, 64u, n, out32);
 }
 
+#ifdef PF_KECCAK_ILP2
+// Probe (PF_KECCAK_ILP2): two messages per lane, i and i + ceil(n/2), their permutations
+// interleaved round by round — two independent dependency chains per wave instead of one.
+__device__ __forceinline__ void load_fixed(Lane a[25], const uint8_t* __restrict__ data, uint32_t len,
+                                           uint64_t i, bool live) {
+    const uint4* q = (const uint4*)(data + i * (uint64_t)len);
+    const uint32_t nq = len >> 4;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        uint4 v = (live && (uint32_t)k < nq) ? q[k] : make_uint4(0u, 0u, 0u, 0u);
+        a[2 * k] = Lane{v.x, v.y};
+        a[2 * k + 1] = Lane{v.z, v.w};
+    }
+    a[16] = Lane{0u, 0x80000000u};
+#pragma unroll
+    for (int k = 17; k < 25; k++) a[k] = Lane{0u, 0u};
+#pragma unroll
+    for (int k = 0; k < 17; k++)
+        if ((uint32_t)k == (len >> 3)) a[k].lo ^= 0x01u;
+}
+
+extern "C" __global__ void __launch_bounds__(256)
+pf_keccak_fixed2_kernel(const uint8_t* __restrict__ data, uint32_t len, uint64_t n,
+                        uint8_t* __restrict__ out32) {
+    const uint64_t half = (n + 1) / 2;
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= half) return;
+    const uint64_t j = i + half;
+    const bool has_j = j < n;
+    Lane a[25], b[25];
+    load_fixed(a, data, len, i, true);
+    load_fixed(b, data, len, has_j ? j : i, has_j);
+#pragma unroll
+    for (int rnd = 0; rnd < 24; rnd++) {
+        keccak_round(a, kRC[2 * rnd], kRC[2 * rnd + 1]);
+        keccak_round(b, kRC[2 * rnd], kRC[2 * rnd + 1]);
+    }
+    squeeze(a, out32 + 32 * i);
+    if (has_j) squeeze(b, out32 + 32 * j);
+}
+#endif
+
 // fixed-length single-block fast path: the host launches it when len % 16 == 0,
 // len < 136 and the buffer is 16-byte aligned (16-byte vector loads, two 16-byte digest
 // stores, all 24 rounds unrolled).
