@@ -276,6 +276,7 @@ KECCAK_BYTES = 64 + 32
 # not at the §8(d) table's 6,500 ops
 KECCAK_VALU_PER_WAVE = 4340
 VALU_ISSUE_PER_S = 256 * 4 * 2.4e9 / 2   # wave64 VALU instructions per second (2 cycles each)
+KECCAK_CYCLES_PER_WAVE = 2792 * 2.76 + 1352 * 4.69 + (4340 - 2792 - 1352) * 2.76
 
 
 def keccak_leg(args, torch, rank, world):
@@ -315,6 +316,11 @@ def keccak_leg(args, torch, rank, world):
                          "unit": "Tops/s (int32)", "frac": ach / INT32_PEAK_OPS,
                          "hbm_GBps": n * KECCAK_BYTES / t / 1e9,
                          "valu_issue_frac": (n / 64) * KECCAK_VALU_PER_WAVE / t / VALU_ISSUE_PER_S,
+                         # the same instructions priced at their measured issue costs at 8
+                         # waves/SIMD (tools/movbench.hip, profiles/r04c_movbench.log: bitop3
+                         # 2.76, alignbit 4.69 SIMD cycles) and the 2.25 GHz the dense loops
+                         # run at — the rate this instruction mix can reach
+                         "issue_frac_at_measured_rates": (n / 64) * KECCAK_CYCLES_PER_WAVE / (1024 * 2.25e9) / t,
                          "note": "frac prices 6,500 int32 ops per Keccak-f[1600] (SURVEY §8(d) "
                                  "table); valu_issue_frac is the hardware view: the 4,340 VALU "
                                  "instructions per wave the kernel issues over the SIMDs' issue "
