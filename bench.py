@@ -442,7 +442,7 @@ def run(args, rank, world, local, dist, engine=None, cdev="cuda"):
     t_gen = time.perf_counter()
     for k in range(n_steps):
         first = (k * world + rank) * args.sets
-        progs = [synth.random_dag_set(first + i, plant=False)[0] for i in range(args.sets)]
+        progs = synth.random_dag_programs(first, args.sets, plant=False)[0]
         step_progs.append(progs)
         batches.append(eng.upload(progs))
     t_gen = time.perf_counter() - t_gen
@@ -494,7 +494,7 @@ def run(args, rank, world, local, dist, engine=None, cdev="cuda"):
 
     # node evaluations of the timed steps: every instruction of every set runs for every
     # candidate in the full sweep (also report node-evals/s)
-    nodes_per_step = [sum(len(p.code) for p in step_progs[k]) for k in range(args.warmup, n_steps)]
+    nodes_per_step = [len(batches[k].batch.code) for k in range(args.warmup, n_steps)]
     tot_nodes = float(sum(nodes_per_step) * args.budget)
     if dist is not None:
         x = torch.tensor([tot_nodes], dtype=torch.float64, device=cdev)
@@ -510,7 +510,7 @@ def run(args, rank, world, local, dist, engine=None, cdev="cuda"):
     # field, computed on the host for the full sweep (every candidate runs every node)
     s8d = None
     if args.mode == "full":
-        s8d_ops = float(sum(p.node_cost() for k in range(args.warmup, n_steps) for p in step_progs[k])) * args.budget
+        s8d_ops = float(sum(ir.op_cost_words(batches[k].batch.code) for k in range(args.warmup, n_steps))) * args.budget
         ks = sum(kms) / 1e3
         s8d = {"achieved": s8d_ops / ks / 1e12 if ks > 0 else 0.0,
                "frac": s8d_ops / ks / INT32_PEAK_OPS if ks > 0 else 0.0,

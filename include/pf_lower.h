@@ -132,7 +132,16 @@ int pfl_version(void);
 void* pflt_store_new(void);
 /* optional pflt_lower modes this build has (PFLT_FEAT_*) */
 #define PFLT_FEAT_EXPLICIT 1u
+#define PFLT_FEAT_SYNTH 2u
 uint32_t pflt_features(void);
+/* BASELINE config 3's synthetic DAGs natively: results[i] = the lowered program of
+ * mythril_amd.synth.random_dag_set(first_id + i, plant) bit for bit (numpy's Philox4x64
+ * Generator stream restated), for pflt_pack_batch; cdf = the op mix's 8 normalised cumulative
+ * probabilities; witness_limbs (optional, 8 x 8 u32 per DAG) and n_vars_out (optional) get
+ * the planted witness.  0, or -1 with pflt_last_error(); free each result with
+ * pflt_result_free.  Not the reference's: the benchmark's input generator. */
+int pflt_synth(uint32_t first_id, size_t n, uint32_t plant, const double* cdf, void** results,
+               uint32_t* witness_limbs, uint32_t* n_vars_out);
 void pflt_store_free(void* store);
 size_t pflt_store_size(void* store);
 int64_t pflt_add(void* store, uint32_t op, uint32_t sortk, uint32_t w1, uint32_t w2, const uint32_t* args,

@@ -279,7 +279,7 @@ struct Dag {
     std::unordered_map<NodeKey, int32_t, NodeKeyHash> memo;
     std::unordered_map<std::string, int32_t> var_index;
 
-    Dag() { memo.reserve(4096); }
+    explicit Dag(size_t reserve = 4096) { memo.reserve(reserve); }
 
     int32_t add_n(uint32_t kind, uint32_t width, const int32_t* args, uint32_t nargs, uint32_t aux,
                   bool is_bool, const C8* cv = nullptr) {
@@ -339,6 +339,7 @@ struct Dag {
     }
 
     int32_t cnst(const C8& v, uint32_t width) {
+        if (width == 256) return add(K_CONST, width, {}, 0, false, &v);
         C8 m = c8_of(big_of(v), width);
         return add(K_CONST, width, {}, 0, false, &m);
     }
@@ -1480,6 +1481,79 @@ void fill_parents(Parents* P, const char* par_names, const uint32_t* par_name_va
     }
 }
 
+// Register allocation + emission of a finished DAG into R (lower.lower(dag): narrow register
+// file first, wide when the narrow program is spill-heavy and the wide one at least halves
+// its spill code).  Throws TermError like the lowering.
+void emit_program(Dag& d, Result* R) {
+    d.finalize_word_hints();
+    pack(d, &R->packed_nodes, &R->pool);
+    std::vector<uint32_t> forced;
+    for (const C8& c : d.forced) forced.insert(forced.end(), c.l, c.l + 8);
+    std::vector<uint32_t> roots2(d.roots.begin(), d.roots.end());
+    if (roots2.empty()) roots2.push_back(0);
+    const uint32_t tries[2] = {PF_NW_NARROW, PF_NW};
+    int rc = -2;
+    // the narrow program unless its spill code exceeds an eighth of it and the wide
+    // register file at least halves that (lower.py lower(): the same policy)
+    bool have_narrow = false;
+    std::vector<uint32_t> n_code, n_consts;
+    size_t n_spill_narrow = 0;
+    // output scratch per thread, grown but never cleared (pfl_lower writes what it
+    // reports); the result keeps only the words written
+    thread_local std::vector<uint32_t> code_buf, const_buf;
+    for (int ti = 0; ti < 2; ti++) {
+        size_t cap_i = 16 * d.nodes.size() + 64 + 4 * d.roots.size();
+        size_t cap_c = R->pool.size() / 8 + d.forced.size() + 1;
+        size_t ni = 0, nc = 0;
+        for (int attempt = 0; attempt < 4; attempt++) {
+            if (code_buf.size() < 4 * cap_i) code_buf.resize(4 * cap_i);
+            if (const_buf.size() < 8 * cap_c) const_buf.resize(8 * cap_c);
+            rc = pfl_lower(R->packed_nodes.data(), d.nodes.size(), R->pool.data(), R->pool.size() / 8,
+                           roots2.data(), d.roots.size(), forced.empty() ? nullptr : forced.data(),
+                           d.forced.size(), tries[ti], code_buf.data(), cap_i, &ni, const_buf.data(),
+                           cap_c, &nc);
+            if (rc != -3) break;
+            cap_i *= 4;
+            cap_c *= 4;
+        }
+        if (rc == 0) {
+            R->code.assign(code_buf.begin(), code_buf.begin() + 4 * ni);
+            R->consts.assign(const_buf.begin(), const_buf.begin() + 8 * nc);
+            size_t n_spill = 0;
+            for (size_t i = 0; i < ni; i++) {
+                const uint32_t op = R->code[4 * i] & 0xffu;
+                n_spill += op == PF_W_SPILL || op == PF_W_FILL;
+            }
+            R->n_wregs = tries[ti];
+            if (ti == 0 && 8 * n_spill > ni) {  // spill-heavy: try the wide register file
+                have_narrow = true;
+                n_code.swap(R->code);
+                n_consts.swap(R->consts);
+                n_spill_narrow = n_spill;
+                continue;
+            }
+            if (ti == 1 && have_narrow && 2 * n_spill > n_spill_narrow) {
+                R->code.swap(n_code);
+                R->consts.swap(n_consts);
+                R->n_wregs = tries[0];
+            }
+            break;
+        }
+        if (ti == 1 && have_narrow) {  // the wide lowering failed (any rc): keep the narrow one
+            R->code.swap(n_code);
+            R->consts.swap(n_consts);
+            R->n_wregs = tries[0];
+            rc = 0;
+            break;
+        }
+        if (rc != -2) break;
+    }
+    if (rc != 0) {
+        t_err = pfl_last_error();
+        throw TermError{rc};
+    }
+}
+
 // One bucket: terms -> DAG -> hints -> program (pflt_lower).  Reads the store only, so
 // buckets lower concurrently (pflt_lower_many).  Never throws: a failure is R->rc / R->err.
 Result* lower_job(const Store& S, const std::vector<uint32_t>& rs, const Parents& P, const uint32_t* registry,
@@ -1566,73 +1640,7 @@ Result* lower_job(const Store& S, const std::vector<uint32_t>& rs, const Parents
             }
         }
         if (flags & PFLT_PROGRAM) {
-            d.finalize_word_hints();
-            pack(d, &R->packed_nodes, &R->pool);
-            std::vector<uint32_t> forced;
-            for (const C8& c : d.forced) forced.insert(forced.end(), c.l, c.l + 8);
-            std::vector<uint32_t> roots2(d.roots.begin(), d.roots.end());
-            if (roots2.empty()) roots2.push_back(0);
-            const uint32_t tries[2] = {PF_NW_NARROW, PF_NW};
-            int rc = -2;
-            // the narrow program unless its spill code exceeds an eighth of it and the wide
-            // register file at least halves that (lower.py lower(): the same policy)
-            bool have_narrow = false;
-            std::vector<uint32_t> n_code, n_consts;
-            size_t n_spill_narrow = 0;
-            // output scratch per thread, grown but never cleared (pfl_lower writes what it
-            // reports); the result keeps only the words written
-            thread_local std::vector<uint32_t> code_buf, const_buf;
-            for (int ti = 0; ti < 2; ti++) {
-                size_t cap_i = 16 * d.nodes.size() + 64 + 4 * d.roots.size();
-                size_t cap_c = R->pool.size() / 8 + d.forced.size() + 1;
-                size_t ni = 0, nc = 0;
-                for (int attempt = 0; attempt < 4; attempt++) {
-                    if (code_buf.size() < 4 * cap_i) code_buf.resize(4 * cap_i);
-                    if (const_buf.size() < 8 * cap_c) const_buf.resize(8 * cap_c);
-                    rc = pfl_lower(R->packed_nodes.data(), d.nodes.size(), R->pool.data(), R->pool.size() / 8,
-                                   roots2.data(), d.roots.size(), forced.empty() ? nullptr : forced.data(),
-                                   d.forced.size(), tries[ti], code_buf.data(), cap_i, &ni, const_buf.data(),
-                                   cap_c, &nc);
-                    if (rc != -3) break;
-                    cap_i *= 4;
-                    cap_c *= 4;
-                }
-                if (rc == 0) {
-                    R->code.assign(code_buf.begin(), code_buf.begin() + 4 * ni);
-                    R->consts.assign(const_buf.begin(), const_buf.begin() + 8 * nc);
-                    size_t n_spill = 0;
-                    for (size_t i = 0; i < ni; i++) {
-                        const uint32_t op = R->code[4 * i] & 0xffu;
-                        n_spill += op == PF_W_SPILL || op == PF_W_FILL;
-                    }
-                    R->n_wregs = tries[ti];
-                    if (ti == 0 && 8 * n_spill > ni) {  // spill-heavy: try the wide register file
-                        have_narrow = true;
-                        n_code.swap(R->code);
-                        n_consts.swap(R->consts);
-                        n_spill_narrow = n_spill;
-                        continue;
-                    }
-                    if (ti == 1 && have_narrow && 2 * n_spill > n_spill_narrow) {
-                        R->code.swap(n_code);
-                        R->consts.swap(n_consts);
-                        R->n_wregs = tries[0];
-                    }
-                    break;
-                }
-                if (ti == 1 && have_narrow) {  // the wide lowering failed (any rc): keep the narrow one
-                    R->code.swap(n_code);
-                    R->consts.swap(n_consts);
-                    R->n_wregs = tries[0];
-                    rc = 0;
-                    break;
-                }
-                if (rc != -2) break;
-            }
-            if (rc != 0) {
-                t_err = pfl_last_error();
-                throw TermError{rc};
-            }
+            emit_program(d, R);
         } else {
             pack(d, &R->packed_nodes, &R->pool);
         }
@@ -1653,13 +1661,433 @@ Result* lower_job(const Store& S, const std::vector<uint32_t>& rs, const Parents
     return R;
 }
 
+// ---- config-3 synthetic DAGs natively (synth.random_dag_set, bit for bit) ------------------
+// numpy's Philox4x64-10 bit generator and the Generator draws random_dag_set makes: random()
+// (53-bit double from next_uint64), integers(lo, hi) for int64 (Lemire on next_uint32, which
+// uses both halves of a 64-bit output in turn) and integers(0, 2^32, size=8, dtype=uint64)
+// (eight next_uint32).  Checked against numpy draw for draw (tests/test_synth_native.py).
+struct NpPhilox {
+    uint64_t ctr[4] = {0, 0, 0, 0}, key[2], buf[4] = {0, 0, 0, 0};
+    int pos = 4;
+    bool has32 = false;
+    uint32_t u32 = 0;
+
+    explicit NpPhilox(unsigned __int128 k) {
+        key[0] = (uint64_t)k;
+        key[1] = (uint64_t)(k >> 64);
+    }
+    static void mulhilo(uint64_t a, uint64_t b, uint64_t* hi, uint64_t* lo) {
+        const unsigned __int128 p = (unsigned __int128)a * b;
+        *hi = (uint64_t)(p >> 64);
+        *lo = (uint64_t)p;
+    }
+    uint64_t next64() {
+        if (pos < 4) return buf[pos++];
+        if (++ctr[0] == 0 && ++ctr[1] == 0 && ++ctr[2] == 0) ++ctr[3];
+        uint64_t c[4] = {ctr[0], ctr[1], ctr[2], ctr[3]}, k0 = key[0], k1 = key[1];
+        for (int r = 0; r < 10; r++) {
+            uint64_t hi0, lo0, hi1, lo1;
+            mulhilo(0xD2E7470EE14C6C93ull, c[0], &hi0, &lo0);
+            mulhilo(0xCA5A826395121157ull, c[2], &hi1, &lo1);
+            const uint64_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+            c[0] = n0;
+            c[1] = lo1;
+            c[2] = n2;
+            c[3] = lo0;
+            k0 += 0x9E3779B97F4A7C15ull;
+            k1 += 0xBB67AE8584CAA73Bull;
+        }
+        for (int i = 0; i < 4; i++) buf[i] = c[i];
+        pos = 1;
+        return buf[0];
+    }
+    uint32_t next32() {
+        if (has32) {
+            has32 = false;
+            return u32;
+        }
+        const uint64_t v = next64();
+        has32 = true;
+        u32 = (uint32_t)(v >> 32);
+        return (uint32_t)v;
+    }
+    double random() { return (double)(next64() >> 11) * (1.0 / 9007199254740992.0); }
+    int64_t integers(int64_t lo, int64_t hi) {  // [lo, hi), range < 2^32
+        const uint64_t rng = (uint64_t)(hi - lo - 1);
+        if (rng == 0) return lo;
+        if (rng == 0xFFFFFFFFull) return lo + next32();
+        const uint32_t rexcl = (uint32_t)rng + 1u;
+        uint64_t m = (uint64_t)next32() * rexcl;
+        uint32_t left = (uint32_t)m;
+        if (left < rexcl) {
+            const uint32_t thr = (uint32_t)((0xFFFFFFFFull - rng) % rexcl);
+            while (left < thr) {
+                m = (uint64_t)next32() * rexcl;
+                left = (uint32_t)m;
+            }
+        }
+        return lo + (int64_t)(m >> 32);
+    }
+};
+
+// 256-bit values as C8 (little-endian u32 limbs): the planted-value arithmetic of synth._eval
+bool c8_zero(const C8& a) {
+    for (int i = 0; i < 8; i++)
+        if (a.l[i]) return false;
+    return true;
+}
+bool c8_ult(const C8& a, const C8& b) {
+    for (int i = 7; i >= 0; i--)
+        if (a.l[i] != b.l[i]) return a.l[i] < b.l[i];
+    return false;
+}
+C8 c8_add(const C8& a, const C8& b) {
+    C8 r;
+    uint64_t c = 0;
+    for (int i = 0; i < 8; i++) {
+        c += (uint64_t)a.l[i] + b.l[i];
+        r.l[i] = (uint32_t)c;
+        c >>= 32;
+    }
+    return r;
+}
+C8 c8_not(const C8& a) {
+    C8 r;
+    for (int i = 0; i < 8; i++) r.l[i] = ~a.l[i];
+    return r;
+}
+C8 c8_neg(const C8& a) { return c8_add(c8_not(a), c8_small(1, 256)); }
+C8 c8_sub(const C8& a, const C8& b) { return c8_add(a, c8_neg(b)); }
+uint32_t c8_bitlen(const C8& a) {
+    for (int i = 7; i >= 0; i--)
+        if (a.l[i]) return 32u * (uint32_t)i + 32u - (uint32_t)__builtin_clz(a.l[i]);
+    return 0;
+}
+C8 c8_shl(const C8& a, uint32_t k) {  // k < 256
+    C8 r;
+    const uint32_t q = k / 32, s = k % 32;
+    for (int i = 7; i >= 0; i--) {
+        const int j = i - (int)q;
+        uint32_t v = j >= 0 ? a.l[j] << s : 0u;
+        if (s && j - 1 >= 0) v |= a.l[j - 1] >> (32 - s);
+        r.l[i] = v;
+    }
+    return r;
+}
+C8 c8_lshr(const C8& a, uint32_t k, uint32_t fill = 0u) {  // k < 256; fill: 0 or ~0u
+    C8 r;
+    const uint32_t q = k / 32, s = k % 32;
+    for (int i = 0; i < 8; i++) {
+        const uint32_t j = (uint32_t)i + q;
+        const uint32_t lo = j < 8 ? a.l[j] : fill, hi = j + 1 < 8 ? a.l[j + 1] : fill;
+        r.l[i] = s ? (lo >> s) | (hi << (32 - s)) : lo;
+    }
+    return r;
+}
+// a / b and a % b (b != 0): Knuth's algorithm D on 32-bit digits (Hacker's Delight divmnu)
+void c8_divrem(const C8& a, const C8& b, C8* q, C8* r) {
+    memset(q, 0, sizeof(C8));
+    memset(r, 0, sizeof(C8));
+    int m = 8, n = 8;
+    while (m > 0 && a.l[m - 1] == 0) m--;
+    while (n > 0 && b.l[n - 1] == 0) n--;
+    if (m < n) {
+        *r = a;
+        return;
+    }
+    if (n == 1) {
+        uint64_t k = 0;
+        for (int j = m - 1; j >= 0; j--) {
+            const uint64_t cur = (k << 32) | a.l[j];
+            q->l[j] = (uint32_t)(cur / b.l[0]);
+            k = cur - (uint64_t)q->l[j] * b.l[0];
+        }
+        r->l[0] = (uint32_t)k;
+        return;
+    }
+    const int s = __builtin_clz(b.l[n - 1]);
+    uint32_t vn[8], un[9];
+    for (int i = n - 1; i > 0; i--) vn[i] = (b.l[i] << s) | (s ? (uint32_t)((uint64_t)b.l[i - 1] >> (32 - s)) : 0u);
+    vn[0] = b.l[0] << s;
+    un[m] = s ? (uint32_t)((uint64_t)a.l[m - 1] >> (32 - s)) : 0u;
+    for (int i = m - 1; i > 0; i--) un[i] = (a.l[i] << s) | (s ? (uint32_t)((uint64_t)a.l[i - 1] >> (32 - s)) : 0u);
+    un[0] = a.l[0] << s;
+    const uint64_t base = 1ull << 32;
+    for (int j = m - n; j >= 0; j--) {
+        const uint64_t num = ((uint64_t)un[j + n] << 32) | un[j + n - 1];
+        uint64_t qhat = num / vn[n - 1], rhat = num - qhat * vn[n - 1];
+        while (qhat >= base || qhat * vn[n - 2] > ((rhat << 32) | un[j + n - 2])) {
+            qhat--;
+            rhat += vn[n - 1];
+            if (rhat >= base) break;
+        }
+        int64_t borrow = 0;
+        for (int i = 0; i < n; i++) {
+            const uint64_t p = qhat * vn[i];
+            const int64_t t = (int64_t)un[i + j] - borrow - (int64_t)(p & 0xFFFFFFFFull);
+            un[i + j] = (uint32_t)t;
+            borrow = (int64_t)(p >> 32) - (t >> 32);
+        }
+        const int64_t t = (int64_t)un[j + n] - borrow;
+        un[j + n] = (uint32_t)t;
+        q->l[j] = (uint32_t)qhat;
+        if (t < 0) {
+            q->l[j]--;
+            uint64_t c = 0;
+            for (int i = 0; i < n; i++) {
+                c += (uint64_t)un[i + j] + vn[i];
+                un[i + j] = (uint32_t)c;
+                c >>= 32;
+            }
+            un[j + n] += (uint32_t)c;
+        }
+    }
+    for (int i = 0; i < n; i++) r->l[i] = (un[i] >> s) | (s ? (uint32_t)((uint64_t)un[i + 1] << (32 - s)) : 0u);
+}
+// a * b mod 2^256 on 64-bit limbs (10 products)
+C8 c8_mul64(const C8& a, const C8& b) {
+    uint64_t x[4], y[4], r[4] = {0, 0, 0, 0};
+    memcpy(x, a.l, 32);
+    memcpy(y, b.l, 32);
+    for (int i = 0; i < 4; i++) {
+        unsigned __int128 c = 0;
+        for (int j = 0; i + j < 4; j++) {
+            c += (unsigned __int128)x[i] * y[j] + r[i + j];
+            r[i + j] = (uint64_t)c;
+            c >>= 64;
+        }
+    }
+    C8 out;
+    memcpy(out.l, r, 32);
+    return out;
+}
+C8 c8_pow(const C8& b, const C8& e) {  // b^e mod 2^256 (pow(a, b, 1 << 256))
+    const uint32_t n = c8_bitlen(e);
+    if (!(b.l[0] & 1u) && n > 8) return c8_small(0, 256);   // even base, e >= 256: 2^256 | b^e
+    C8 r = c8_small(1, 256), x = b;
+    for (uint32_t i = 0; i < n; i++) {
+        if ((e.l[i / 32] >> (i % 32)) & 1u) r = c8_mul64(r, x);
+        if (i + 1 < n) x = c8_mul64(x, x);
+    }
+    return r;
+}
+bool c8_neg_sign(const C8& a) { return a.l[7] >> 31; }
+C8 c8_abs(const C8& a) { return c8_neg_sign(a) ? c8_neg(a) : a; }
+bool c8_slt(const C8& a, const C8& b) {
+    const bool sa = c8_neg_sign(a), sb = c8_neg_sign(b);
+    if (sa != sb) return sa;
+    return c8_ult(a, b);
+}
+
+C8 synth_eval(uint32_t op, const C8& a, const C8& b) {  // synth._eval at w = 256
+    C8 q, r;
+    switch (op) {
+        case PF_W_ADD: return c8_add(a, b);
+        case PF_W_SUB: return c8_sub(a, b);
+        case PF_W_MUL: return c8_mul64(a, b);
+        case PF_W_UDIV:
+            if (c8_zero(b)) return c8_not(c8_small(0, 256));
+            c8_divrem(a, b, &q, &r);
+            return q;
+        case PF_W_UREM:
+            if (c8_zero(b)) return a;
+            c8_divrem(a, b, &q, &r);
+            return r;
+        case PF_W_SDIV:
+        case PF_W_SREM: {
+            const bool sa = c8_neg_sign(a), sb = c8_neg_sign(b);
+            if (c8_zero(b)) return op == PF_W_SDIV ? (sa ? c8_small(1, 256) : c8_not(c8_small(0, 256))) : a;
+            c8_divrem(c8_abs(a), c8_abs(b), &q, &r);
+            if (op == PF_W_SDIV) return sa == sb ? q : c8_neg(q);
+            return sa ? c8_neg(r) : r;
+        }
+        case PF_W_AND: { C8 z; for (int i = 0; i < 8; i++) z.l[i] = a.l[i] & b.l[i]; return z; }
+        case PF_W_OR: { C8 z; for (int i = 0; i < 8; i++) z.l[i] = a.l[i] | b.l[i]; return z; }
+        case PF_W_XOR: { C8 z; for (int i = 0; i < 8; i++) z.l[i] = a.l[i] ^ b.l[i]; return z; }
+        case PF_W_NOT: return c8_not(a);
+        case PF_W_SHL: return c8_bitlen(b) > 8 ? c8_small(0, 256) : c8_shl(a, b.l[0]);
+        case PF_W_LSHR: return c8_bitlen(b) > 8 ? c8_small(0, 256) : c8_lshr(a, b.l[0]);
+        case PF_W_ASHR: {
+            const uint32_t fill = c8_neg_sign(a) ? ~0u : 0u;
+            if (c8_bitlen(b) > 8) {
+                C8 z;
+                for (int i = 0; i < 8; i++) z.l[i] = fill;
+                return z;
+            }
+            return c8_lshr(a, b.l[0], fill);
+        }
+        case PF_W_EXP: return c8_pow(a, b);
+        default: return a;
+    }
+}
+
+constexpr uint64_t kDagGenSeed = 20260101ull;
+constexpr uint32_t kCandSeedBase = 0x4D595448u;
+// synth._MIX in order (the op kinds) and its normalised cumulative probabilities, the doubles
+// numpy's cumsum / cdf[-1] produces (tests/test_synth_native.py checks the table)
+enum SynthKind { SK_MUL, SK_DIV, SK_REM, SK_EXP, SK_ADDSUB, SK_LOGIC, SK_SHIFT, SK_ITECMP };
+
+C8 synth_leaf_value(NpPhilox& g) {  // synth._leaf_value
+    if (g.random() < 0.5) {  // _rand256: eight u32 draws, the first the most significant
+        C8 v;
+        for (int i = 7; i >= 0; i--) v.l[i] = g.next32();
+        return v;
+    }
+    const int64_t j = g.integers(0, 9);
+    switch (j) {
+        case 0: return c8_small(0, 256);
+        case 1: return c8_small(1, 256);
+        case 2: return c8_small(2, 256);
+        case 3: return c8_not(c8_small(0, 256));
+        case 4: { C8 v = c8_small(0, 256); v.l[7] = 0x80000000u; return v; }
+        case 5: { C8 v = c8_small(0, 256); for (int i = 0; i < 5; i++) v.l[i] = ~0u; return v; }
+        default: {
+            const int64_t k = g.integers(0, 256);
+            C8 p = c8_small(0, 256);
+            p.l[k / 32] = 1u << (k % 32);
+            if (j == 6) return c8_sub(p, c8_small(1, 256));
+            if (j == 8) return c8_add(p, c8_small(1, 256));
+            return p;
+        }
+    }
+}
+
+// One config-3 DAG into R (synth.random_dag_set(dag_id, plant)); the witness into *wit.
+void synth_dag(uint32_t dag_id, bool plant, const double* cdf, Result* R, std::vector<C8>* wit) {
+    NpPhilox g(((unsigned __int128)kDagGenSeed << 32) | dag_id);
+    Dag d(256);
+    const int64_t n_vars = g.integers(4, 9);
+    wit->clear();
+    for (int64_t v = 0; v < n_vars; v++) wit->push_back(synth_leaf_value(g));
+    std::vector<std::pair<int32_t, C8>> leaves, interior;
+    for (int64_t v = 0; v < n_vars; v++) {
+        bool created;
+        leaves.push_back({d.var("x" + std::to_string(v), 256, PF_VK_GENERIC, 0, 0, plant, (*wit)[v], &created),
+                          (*wit)[v]});
+    }
+    for (int k = 0; k < 4; k++) {
+        const C8 c = synth_leaf_value(g);
+        leaves.push_back({d.cnst(c, 256), c});
+    }
+    const int depth = 32, window = 6;
+    auto pick = [&](bool first) -> std::pair<int32_t, C8> {
+        if (first && !interior.empty() && (int)interior.size() <= depth) return interior.back();
+        const size_t np = std::min<size_t>(interior.size(), (size_t)window);
+        if (np && g.random() < 0.6) return interior[interior.size() - np + (size_t)g.integers(0, (int64_t)np)];
+        return leaves[(size_t)g.integers(0, (int64_t)leaves.size())];
+    };
+    for (int it = 0; it < 48; it++) {
+        const double u = g.random();
+        int kind = 0;
+        while (kind < 7 && !(u < cdf[kind])) kind++;   // bisect_right
+        auto A = pick(true);
+        auto B = pick(false);
+        uint32_t op = 0;
+        switch (kind) {
+            case SK_DIV: op = g.random() < 0.5 ? PF_W_UDIV : PF_W_SDIV; break;
+            case SK_REM: op = g.random() < 0.5 ? PF_W_UREM : PF_W_SREM; break;
+            case SK_ADDSUB: op = g.random() < 0.5 ? PF_W_ADD : PF_W_SUB; break;
+            case SK_LOGIC: {
+                static const uint32_t ops[4] = {PF_W_AND, PF_W_OR, PF_W_XOR, PF_W_NOT};
+                op = ops[g.integers(0, 4)];
+                break;
+            }
+            case SK_SHIFT: {
+                static const uint32_t ops[3] = {PF_W_SHL, PF_W_LSHR, PF_W_ASHR};
+                op = ops[g.integers(0, 3)];
+                if (g.random() < 0.5) {
+                    (void)g.integers(0, 256);   // drawn and unused, as in synth.py
+                    B.first = d.op(PF_W_AND, 256, {B.first, d.cnst(0xFF, 256)});
+                    C8 m = c8_small(0, 256);
+                    m.l[0] = B.second.l[0] & 0xFFu;
+                    B.second = m;
+                }
+                break;
+            }
+            case SK_ITECMP: {
+                static const uint32_t ops[3] = {PF_B_ULT, PF_B_SLT, PF_B_EQ};
+                const uint32_t c_op = ops[g.integers(0, 3)];
+                auto C2 = pick(false);
+                const int32_t cond = d.op(c_op, 256, {A.first, C2.first});
+                const bool cv = c_op == PF_B_ULT ? c8_ult(A.second, C2.second)
+                                : c_op == PF_B_EQ ? A.second == C2.second : c8_slt(A.second, C2.second);
+                const int32_t node = d.op(PF_W_ITE, 256, {cond, A.first, B.first});
+                interior.push_back({node, cv ? A.second : B.second});
+                continue;
+            }
+            case SK_MUL: op = PF_W_MUL; break;
+            default: op = PF_W_EXP; break;
+        }
+        int32_t node;
+        C8 val;
+        if (op == PF_W_NOT) {
+            node = d.op(op, 256, {A.first});
+            val = c8_not(A.second);
+        } else {
+            node = d.op(op, 256, {A.first, B.first});
+            val = synth_eval(op, A.second, B.second);
+        }
+        interior.push_back({node, val});
+    }
+    const int64_t n_roots = g.integers(2, 5);
+    const size_t nt = std::min<size_t>(interior.size(), (size_t)std::max<int64_t>(n_roots * 2, 8));
+    const size_t t0 = interior.size() - nt;
+    for (int64_t r = 0; r < n_roots; r++) {
+        const auto& NV = interior[t0 + (size_t)g.integers(0, (int64_t)nt)];
+        const int64_t cmp = g.integers(0, 3);
+        int32_t root;
+        if (cmp == 0) {
+            root = d.op(PF_B_EQ, 256, {NV.first, d.cnst(NV.second, 256)});
+        } else if (cmp == 1) {
+            root = d.op(PF_B_ULE, 256, {NV.first, d.cnst(NV.second, 256)});
+        } else {
+            const int32_t c = d.cnst(NV.second, 256);
+            root = d.op(PF_B_ULE, 256, {c, NV.first});
+        }
+        d.roots.push_back(root);
+    }
+    emit_program(d, R);
+    for (const DVar& v : d.vars) {
+        R->names += v.name;
+        R->names.push_back('\0');
+    }
+    R->parented = plant;
+    R->dag = std::move(d);
+    decltype(R->dag.memo)().swap(R->dag.memo);
+}
+
 }  // namespace
 
 extern "C" {
 
 void* pflt_store_new(void) { return new Store(); }
 
-uint32_t pflt_features(void) { return PFLT_FEAT_EXPLICIT; }
+uint32_t pflt_features(void) { return PFLT_FEAT_EXPLICIT | PFLT_FEAT_SYNTH; }
+
+int pflt_synth(uint32_t first_id, size_t n, uint32_t plant, const double* cdf, void** results,
+               uint32_t* witness_limbs, uint32_t* n_vars_out) {
+    try {
+        std::vector<C8> wit;
+        for (size_t i = 0; i < n; i++) {
+            Result* R = new Result();
+            results[i] = R;
+            try {
+                synth_dag(first_id + (uint32_t)i, plant != 0, cdf, R, &wit);
+            } catch (const TermError& e) {
+                R->rc = e.rc;
+                R->err = t_err;
+                return -1;
+            }
+            if (n_vars_out) n_vars_out[i] = (uint32_t)wit.size();
+            if (witness_limbs)
+                for (size_t v = 0; v < wit.size(); v++) memcpy(witness_limbs + 64 * i + 8 * v, wit[v].l, 32);
+        }
+    } catch (const std::exception& e) {
+        t_err = std::string("pflt_synth: ") + e.what();
+        return -1;
+    }
+    return 0;
+}
 
 void pflt_store_free(void* st) { delete (Store*)st; }
 

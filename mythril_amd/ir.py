@@ -445,6 +445,25 @@ def reach_lut() -> np.ndarray:
     return _REACH_LUT
 
 
+_OP_LUT = None
+
+
+def op_cost_words(words: np.ndarray) -> int:
+    """Sum of ``op_cost`` (the SURVEY §8(d) table) over packed instructions, vectorised."""
+    global _OP_LUT
+    if _OP_LUT is None:
+        lut = np.zeros((256, 1024), dtype=np.int64)
+        for op in range(256):
+            for w in range(1, MAX_WIDTH + 1):
+                try:
+                    lut[op, w] = op_cost(op, w)
+                except Exception:  # noqa: BLE001 - opcodes outside the table cost 0
+                    pass
+        _OP_LUT = lut
+    words = np.asarray(words, dtype=np.uint32).reshape(-1, 4)
+    return int(_OP_LUT[words[:, 0] & 0xFF, (words[:, 0] >> 8) & 0x3FF].sum())
+
+
 def _reach_cost_words(words: np.ndarray) -> np.ndarray:
     """reach_cost of packed instructions, vectorised: a (op, width) lookup table."""
     op = words[:, 0] & 0xFF

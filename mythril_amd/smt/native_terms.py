@@ -202,6 +202,43 @@ def store() -> Optional[TermStore]:
     return _STORE
 
 
+def synth_programs(first_id: int, n: int, plant: bool, cdf) -> Optional[Tuple[list, np.ndarray, np.ndarray]]:
+    """Config-3 DAG programs first_id .. first_id + n - 1 natively (pflt_synth: the programs of
+    synth.random_dag_set bit for bit), as NativePrograms, with the planted witnesses (n x 8 x 8
+    u32 limbs) and variable counts; None when libpflower.so lacks it."""
+    st = store()
+    if st is None or not hasattr(st.L, "pflt_synth") or not (_features(st) & 2):
+        return None
+    L = st.L
+    if not getattr(L, "_synth_bound", False):
+        L.pflt_synth.restype = ctypes.c_int
+        L.pflt_synth.argtypes = [ctypes.c_uint32, ctypes.c_size_t, ctypes.c_uint32,
+                                 ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_void_p), _u32p, _u32p]
+        L._synth_bound = True
+    hs = (ctypes.c_void_p * max(n, 1))()
+    wit = np.zeros((max(n, 1), 8, 8), dtype=np.uint32)
+    nv = np.zeros(max(n, 1), dtype=np.uint32)
+    c = np.ascontiguousarray(cdf, dtype=np.float64)
+    rc = L.pflt_synth(first_id, n, 1 if plant else 0, c.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), hs,
+                      wit.ctypes.data_as(_u32p), nv.ctypes.data_as(_u32p))
+    results = [_Result(st, hs[i]) for i in range(n) if hs[i]]
+    if rc != 0:
+        raise ValueError(L.pflt_last_error().decode(errors="replace"))
+    progs = []
+    for i, r in enumerate(results):
+        p = NativeProgram(r, (0x4D595448 ^ (first_id + i)) & 0xFFFFFFFF)
+        p.name = f"dag{first_id + i}"
+        progs.append(p)
+    return progs, wit[:n], nv[:n]
+
+
+def _features(st) -> int:
+    if not hasattr(st.L, "pflt_features"):
+        return 0
+    st.L.pflt_features.restype = ctypes.c_uint32
+    return int(st.L.pflt_features())
+
+
 def has_explicit() -> bool:
     """Whether libpflower.so has the explicit-model lowering (PFLT_EXPLICIT)."""
     st = store()

@@ -192,6 +192,24 @@ def random_dag_batch(first_id: int, n: int, **kw) -> List[Program]:
     return [random_dag_set(first_id + i, **kw)[0] for i in range(n)]
 
 
+def random_dag_programs(first_id: int, n: int, plant: bool = False) -> Tuple[List[Program], List[List[int]]]:
+    """``random_dag_set(first_id + i, plant=plant)`` for i < n — natively when libpflower.so
+    has the generator (pflt_synth: numpy's Philox Generator stream, the DAG builder, the
+    planted-value arithmetic and the lowering restated in C++, equal program for program:
+    tests/test_synth_native.py), else in Python.  (programs, planted witnesses)."""
+    from .smt import native_terms
+
+    got = native_terms.synth_programs(first_id, n, plant, _MIX_CDF) if n else None
+    if got is None:
+        out = [random_dag_set(first_id + i, plant=plant) for i in range(n)]
+        return [p for p, _ in out], [w for _, w in out]
+    progs, wit, nv = got
+    rows = wit.astype("<u4").tobytes()
+    witnesses = [[int.from_bytes(rows[256 * i + 32 * v:256 * i + 32 * v + 32], "little") for v in range(int(nv[i]))]
+                 for i in range(n)]
+    return progs, witnesses
+
+
 # ---- Mythril-shaped sets ------------------------------------------------------------
 CREATOR = 0xAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFE
 ATTACKER = 0xDEADBEEFDEADBEEFDEADBEEFDEADBEEFDEADBEEF

@@ -28,24 +28,15 @@ sys.path.insert(0, ROOT)
 
 def _build(args):
     """DAGs [first, first+n): packed arrays of the unplanted programs and of the same
-    programs with their planted witness attached as the parent model (identical code)."""
-    import copy
-
+    programs with their planted witness attached as the parent model (identical code) —
+    natively generated when libpflower.so has pflt_synth (synth.random_dag_programs)."""
     first, n = args
     from mythril_amd import ir, synth
 
-    progs, planted = [], []
-    for i in range(n):
-        p, wit = synth.random_dag_set(first + i, plant=False)
-        q = copy.copy(p)
-        q.vars = [copy.copy(v) for v in p.vars]
-        for v, x in zip(q.vars, wit):
-            v.parent = x
-        progs.append(p)
-        planted.append(q)
     out = []
-    for ps in (progs, planted):
-        b = ir.Batch(ps)
+    for plant in (False, True):
+        progs, _ = synth.random_dag_programs(first, n, plant=plant)
+        b = ir.Batch(progs)
         out.append((b.code, b.consts, b.schema, b.parents, b.descs))
     return first, n, out
 
