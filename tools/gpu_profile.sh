@@ -8,8 +8,8 @@ export TMPDIR=/tmp
 TAG=${1:-r02}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-B="python bench.py --steps 5 --warmup 2 --no-cpu-baseline --corpus-scenarios 0"
-P="python bench.py --steps 2 --warmup 1 --no-cpu-baseline --corpus-scenarios 0"
+B="python bench.py --steps 5 --warmup 2 --no-cpu-baseline --corpus-scenarios 0 --full-pass-dags 0 --quick-sat-queries 0"
+P="python bench.py --steps 2 --warmup 1 --no-cpu-baseline --corpus-scenarios 0 --full-pass-dags 0 --quick-sat-queries 0"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run -- $B > $OUT/trace.log 2>&1 || { echo "trace failed"; exit 1; }
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- $P > $OUT/fetch.log 2>&1 || { echo "fetch failed"; exit 1; }
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- $P > $OUT/write.log 2>&1 || { echo "write failed"; exit 1; }
