@@ -55,7 +55,7 @@ def parse(argv=None):
     ap.add_argument("--corpus-scenarios", type=int, default=48,
                     help="LASER-shaped scenarios for the %% discharged half of the metric (0 = skip)")
     ap.add_argument("--full-pass-dags", type=int, default=1_000_000,
-                    help="config 3 as specified: one pass over this many DAGs (0 = skip; N = 1 only)")
+                    help="config 3 as specified: one pass over this many DAGs, split over the ranks (0 = skip)")
     ap.add_argument("--full-pass-workers", type=int, default=16)
     ap.add_argument("--quick-sat-queries", type=int, default=120,
                     help="queries of the quick-sat (100 cached models) and funnel legs (0 = skip)")
@@ -225,25 +225,46 @@ def discharge(args):
                       f"(config-2 substitute: no z3/solc for --solver-log dumps)"}
 
 
-def full_pass_leg(args, eng):
+def full_pass_leg(args, eng, rank=0, world=1, dist=None, cdev="cuda"):
     """BASELINE config 3 as specified: ONE pass over the 1,000,000 DAGs ×
     65,536 candidates, full sweep (plus the planted early-exit pass over the same ids), the
     host workers generating and lowering the next chunks while the device sweeps
     (tools/full_pass.py).  Two rates: over the kernel time (inputs resident, the headline's
-    definition) and over the wall time (host generation included)."""
+    definition) and over the wall time (host generation included).  With N ranks the DAG ids
+    are split into N contiguous shards (strong scaling of the fixed pass: no data-path
+    collective; the per-rank figures are reduced afterwards — evals and witnesses summed,
+    kernel and wall time the slowest rank's)."""
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import full_pass
 
+    D = args.full_pass_dags
+    lo, hi = rank * D // world, (rank + 1) * D // world
     gc.collect()
-    res = full_pass.run_full_pass(eng, dags=args.full_pass_dags, workers=args.full_pass_workers,
+    if dist is not None:
+        dist.barrier()
+    res = full_pass.run_full_pass(eng, dags=hi - lo, first=lo, workers=args.full_pass_workers,
                                   budget=args.budget, seed=args.seed, mp_context="spawn")
-    fs = res["full_sweep"]
-    return {"dags": res["dags"], "candidates_per_dag": res["candidates_per_dag"],
-            "evals": fs["evals_full"], "kernel_s": fs["kernel_s"], "wall_s": res["total_wall_s"],
-            "evals_per_s_kernel": fs["evals_per_s_kernel"], "evals_per_s_wall": fs["evals_per_s_wall"],
-            "sets_with_witness": fs["sets_with_witness"], "chunks": fs["chunks"],
-            "host_wait_s": res["host_wait_s"], "host_workers": res["host_workers"],
-            "planted_early_exit": res["planted_early_exit"], "seeds": res["seeds"]}
+    fs, pe = res["full_sweep"], res["planted_early_exit"]
+    vals = [float(fs["evals_full"]), float(fs["sets_with_witness"]), float(pe["sets_with_witness"]),
+            float(pe["cands_decided"]), fs["kernel_s"], res["total_wall_s"], pe["kernel_s"]]
+    if dist is not None:
+        import torch
+
+        t_sum = torch.tensor(vals[:4], dtype=torch.float64, device=cdev)
+        t_max = torch.tensor(vals[4:], dtype=torch.float64, device=cdev)
+        dist.all_reduce(t_sum, op=dist.ReduceOp.SUM)
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        vals = [float(x) for x in t_sum.cpu().tolist()] + [float(x) for x in t_max.cpu().tolist()]
+    evals, wit, pwit, pdec, ks, wall, pks = vals
+    return {"dags": D, "candidates_per_dag": args.budget, "ranks": world,
+            "evals": evals, "kernel_s": ks, "wall_s": wall,
+            "evals_per_s_kernel": evals / ks if ks else None, "evals_per_s_wall": evals / wall if wall else None,
+            "sets_with_witness": int(wit), "chunks_rank0": fs["chunks"],
+            "host_wait_s_rank0": res["host_wait_s"], "host_workers_per_rank": res["host_workers"],
+            "planted_early_exit": {"kernel_s": pks, "sets_with_witness": int(pwit), "cands_decided": int(pdec),
+                                   "set_verdicts_per_s_kernel": D / pks if pks else None},
+            "seeds": res["seeds"],
+            "scaling": "strong: the 1,000,000 DAG ids split over the ranks" if world > 1 else None}
 
 
 def quick_sat_leg(args):
@@ -517,6 +538,9 @@ def run(args, rank, world, local, dist, engine=None, cdev="cuda"):
                "note": "SURVEY.md §8(d) per-op table (EXP 36,864, UDIV 256, SDIV 280); "
                        "not reachable-work pricing, so frac may exceed 1"}
 
+    # the full pass on every rank (its own shard of the DAG ids), before rank 0's host legs
+    fp = full_pass_leg(args, eng, rank, world, dist, cdev) if args.full_pass_dags > 0 else None
+
     if rank == 0:
         pmc, traffic_src = pmc_traffic(args)
         traffic = pmc.get("traffic_bytes") if pmc else None
@@ -566,8 +590,8 @@ def run(args, rank, world, local, dist, engine=None, cdev="cuda"):
             line["discharge"] = discharge(args)
         if args.quick_sat_queries > 0:
             line["quick_sat"] = quick_sat_leg(args)
-        if args.full_pass_dags > 0 and world == 1:
-            line["full_pass"] = full_pass_leg(args, eng)
+        if fp is not None:
+            line["full_pass"] = fp
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(step_progs[args.warmup], args.budget, args.seed,
                                                 args.cpu_sample_s)

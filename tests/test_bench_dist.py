@@ -90,3 +90,45 @@ def test_bench_multirank_branch_gloo(tmp_path):
     assert line["sets_with_witness"] == want
     ee = line["early_exit"]
     assert ee["unplanted"]["sets"] == 2 * a.sets and ee["planted"]["sets_with_witness"] == 2 * a.sets
+
+
+def _worker_fp(rank, world, port, out_path):
+    import torch.distributed as dist
+
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+
+    argv = [a for a in ARGV]
+    i = argv.index("--full-pass-dags")
+    argv[i + 1] = "21"
+    argv += ["--full-pass-workers", "2"]
+    line = bench.run(bench.parse(argv), rank, world, 0, dist, engine=_engine(), cdev="cpu")
+    if rank == 0:
+        with open(out_path, "w") as f:
+            json.dump(line, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bench_full_pass_sharded_over_ranks(tmp_path):
+    """The full-pass leg at world size 2: each rank sweeps its contiguous shard of the DAG ids
+    (10 + 11 of 21), evals and witnesses summed, times the slowest rank's."""
+    out = str(tmp_path / "line.json")
+    mp.spawn(_worker_fp, args=(2, _free_port(), out), nprocs=2, join=True)
+    fp = json.load(open(out))["full_pass"]
+    import bench
+    import pyoracle as O
+
+    from mythril_amd import ir, synth
+
+    a = bench.parse(ARGV)
+    assert fp["ranks"] == 2 and fp["dags"] == 21 and fp["evals"] == 21 * a.budget
+    progs = [synth.random_dag_set(i, plant=False)[0] for i in range(21)]
+    b = ir.Batch(progs)
+    want = sum(O.SetView.from_batch(b, i).check(a.budget, a.seed)[0] is not None for i in range(21))
+    assert fp["sets_with_witness"] == want
+    assert fp["planted_early_exit"]["sets_with_witness"] == 21
+    assert fp["kernel_s"] > 0 and fp["wall_s"] >= fp["kernel_s"]

@@ -51,8 +51,8 @@ def _arrays_batch(arrs, n):
 
 
 def run_full_pass(eng, dags: int = 1_000_000, chunk: int = 65536, piece: int = 2048, workers: int = 16,
-                  budget: int = 65536, seed: int = 0, progress=None, mp_context=None) -> dict:
-    """The full pass over DAG ids [0, dags) on ``eng``; returns the result dict.  The host
+                  budget: int = 65536, seed: int = 0, progress=None, mp_context=None, first: int = 0) -> dict:
+    """The full pass over DAG ids [first, first + dags) on ``eng``; returns the result dict.  The host
     workers (``mp_context``: "spawn" when the caller has already initialised the GPU) build
     the packed batches while the device sweeps the previous chunk."""
     import multiprocessing as mp
@@ -65,7 +65,7 @@ def run_full_pass(eng, dags: int = 1_000_000, chunk: int = 65536, piece: int = 2
     pool = ProcessPoolExecutor(workers, mp_context=ctx)
     list(pool.map(_build, [(0, 1)] * workers))
     t_wall = time.perf_counter()
-    res = {"dags": dags, "candidates_per_dag": budget,
+    res = {"dags": dags, "first_dag": first, "candidates_per_dag": budget,
            "seeds": "DAG generator 20260101 (Philox key (seed << 32) | dag_id), candidate key "
                     "0x4D595448 ^ dag_id (global seed 0)"}
     legs = {"full_sweep": (0, 0), "planted_early_exit": (1, ir.FLAG_EARLY_EXIT | ir.FLAG_SHORTCIRCUIT)}
@@ -106,7 +106,7 @@ def run_full_pass(eng, dags: int = 1_000_000, chunk: int = 65536, piece: int = 2
     dev = threading.Thread(target=device_loop, daemon=True)
     dev.start()
     with pool:
-        tasks = [(f, min(piece, dags - f)) for f in range(0, dags, piece)]
+        tasks = [(first + f, min(piece, dags - f)) for f in range(0, dags, piece)]
         futs = [pool.submit(_build, t) for t in tasks]
         pending, n_pending = [], 0
         for i, fu in enumerate(futs):
