@@ -246,6 +246,25 @@ void pflt_pack_batch(void* const* results, size_t n, const uint32_t* seeds, cons
  * (not evaluable here: re-check in Python). */
 void pflt_recheck_many(void* store, void* const* results, size_t n, const uint32_t* values,
                        const uint32_t* registry, size_t n_registry, uint32_t n_threads, int8_t* status);
+/* A GPU witness kept for the quick-sat cache (mythril_amd/model_cache.py; replaces the Python
+ * interp.Witness.leaf_value walk behind reference mythril/support/model.py:52-58 model.eval):
+ * the interpretation of n_parts lowering results (the variable-disjoint buckets of one found
+ * set, values back to back as for pflt_recheck_many), with its evaluation memo kept between
+ * calls.  reg_serial names the registry blob's state.  NULL on a malformed registry blob. */
+void* pflt_witness_new(void* store, void* const* results, size_t n_parts, const uint32_t* values,
+                       const uint32_t* registry, size_t n_registry, uint64_t reg_serial);
+void pflt_witness_free(void* witness);
+/* terms[0..n_terms) under each of n_models witnesses (the store locked by the caller), with
+ * the registry's current state (re-parsed by a witness whose reg_serial differs).  slots
+ * (optional): the caller's dense number of each term, under which a witness keeps the value
+ * (forgotten when slot_epoch changes) so that a term read again is a copy:
+ * out_limbs[(m * n_terms + i) * 8 + k] = limb k of the value (masked to the term's width,
+ * at most 256 bits; a Bool is 0 / 1), ok[m * n_terms + i] = 1
+ * where it evaluated (0: not evaluable natively); the witnesses on n_threads threads. */
+void pflt_witness_values(void* const* witnesses, size_t n_models, const uint32_t* terms, size_t n_terms,
+                         const uint32_t* slots, uint64_t slot_epoch,
+                         const uint32_t* registry, size_t n_registry, uint64_t reg_serial,
+                         uint32_t n_threads, uint32_t* out_limbs, uint8_t* ok);
 
 #ifdef __cplusplus
 }

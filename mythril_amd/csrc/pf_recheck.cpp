@@ -79,6 +79,7 @@ class V {
     }
     bool operator==(const V& o) const { return n_ == o.n_ && std::equal(p_, p_ + n_, o.p_); }
     bool operator!=(const V& o) const { return !(*this == o); }
+    bool operator<(const V& o) const { return std::lexicographical_compare(p_, p_ + n_, o.p_, o.p_ + o.n_); }
 
    private:
     static constexpr size_t N = 16;
@@ -548,11 +549,56 @@ struct Ev {
         return vmask(h, width(tv));
     }
 
+    // interp.Witness._first_table: once every index of an array has been evaluated (by the
+    // scan's rules: a nested read of the same array meanwhile scans), the first read whose
+    // index equals iv is a lookup — the scan's answer, as the read's own entry matches
+    struct FirstTable {
+        bool ok = false;
+        std::map<V, V> first;  // index value (trailing zero limbs trimmed) -> value
+    };
+    std::unordered_map<std::string, FirstTable> tables;
+    std::unordered_map<std::string, bool> building;
+
+    static V trimmed(const V& v) {
+        size_t n = v.size();
+        while (n && v[n - 1] == 0) n--;
+        return V(v.begin(), v.begin() + n);
+    }
+
+    const FirstTable* first_table(const std::string& name, const std::vector<std::pair<uint32_t, uint32_t>>& es,
+                                  uint32_t w2) {
+        auto it = tables.find(name);
+        if (it != tables.end()) return it->second.ok ? &it->second : nullptr;
+        if (building[name]) return nullptr;
+        building[name] = true;
+        FirstTable tab;
+        try {
+            for (const auto& e : es) {
+                V key = trimmed(ev(e.second));
+                if (tab.first.count(key)) continue;
+                auto jt = read_vals.find(e);
+                tab.first.emplace(std::move(key), jt != read_vals.end() ? jt->second : vzero(w2));
+            }
+            tab.ok = true;
+        } catch (...) {
+            tab.first.clear();
+            tab.ok = false;
+        }
+        building[name] = false;
+        auto& slot = tables[name] = std::move(tab);
+        return slot.ok ? &slot : nullptr;
+    }
+
     V array_read(uint32_t arr, uint32_t idx, const V& iv) {
         const pflt_term_view A = T(arr);
-        auto it = reads.find(name_of(A));
+        const std::string name = name_of(A);
+        auto it = reads.find(name);
         if (it == reads.end() || it->second.empty()) return vzero(A.w2);
         const auto& es = it->second;
+        if (const FirstTable* tab = first_table(name, es, A.w2)) {
+            auto jt = tab->first.find(trimmed(iv));
+            return jt != tab->first.end() ? jt->second : vzero(A.w2);
+        }
         size_t last = es.size() - 1;
         for (size_t i = 0; i < es.size(); i++)
             if (es[i].first == arr && es[i].second == idx) { last = i; break; }
@@ -580,12 +626,12 @@ struct Ev {
     static bool bool_of(const V& v) { return !vis_zero(v); }
     static V B(bool b) { return V{b ? 1u : 0u}; }
 
-    V ev(uint32_t t) {
+    // memoised: the reference stays valid (node-based map) while later terms are added
+    const V& ev(uint32_t t) {
         auto it = memo.find(t);
         if (it != memo.end()) return it->second;
         V r = ev_(t);
-        memo.emplace(t, r);
-        return r;
+        return memo.emplace(t, std::move(r)).first->second;
     }
 
     V ev_(uint32_t t) {
@@ -643,15 +689,9 @@ struct Ev {
     }
 };
 
-int recheck_core(void* store, const uint32_t* var_desc, size_t n_vars, const uint32_t* values,
-                            const uint32_t* uf_apps, size_t n_uf, const uint32_t* reads, size_t n_reads,
-                            const uint32_t* registry, size_t n_registry, const uint32_t* roots,
-                            size_t n_roots, uint8_t* out) {
-    try {
-        Ev E;
-        E.st = store;
-        // registry blob: as for pflt_lower (actors first, unused here)
-        size_t p = 0;
+// registry blob: as for pflt_lower (actors first, unused here); throws on a short blob
+void parse_registry(Ev& E, const uint32_t* registry, size_t n_registry) {
+    size_t p = 0;
         auto take = [&]() -> uint32_t {
             if (p >= n_registry) throw 2;
             return registry[p++];
@@ -676,7 +716,13 @@ int recheck_core(void* store, const uint32_t* var_desc, size_t n_vars, const uin
             }
             E.kspecs[n] = sp;
         }
-        // the witness (interp.Witness.__init__): var descriptors (type, a, b, c) with values
+}
+
+// one part of a witness (interp.Witness.__init__): var descriptors (type, a, b, c) with values,
+// its UF applications and array reads appended (Witness.union: the parts' arrays and keccak
+// families are disjoint, their uf_apps concatenate in part order)
+void add_part(Ev& E, const uint32_t* var_desc, size_t n_vars, const uint32_t* values, const uint32_t* uf_apps,
+              size_t n_uf, const uint32_t* reads, size_t n_reads) {
         for (size_t i = 0; i < n_vars; i++) {
             const uint32_t* d = var_desc + 4 * i;
             const V val(values + 8 * i, values + 8 * i + 8);
@@ -698,16 +744,39 @@ int recheck_core(void* store, const uint32_t* var_desc, size_t n_vars, const uin
                 cur = binop(PFLT_BVOR, cur, vshl(val, d[2], w), w);
             }
         }
-        E.uf_apps.assign(uf_apps, uf_apps + n_uf);
+        E.uf_apps.insert(E.uf_apps.end(), uf_apps, uf_apps + n_uf);
         for (size_t i = 0; i < n_reads; i++) {
             const uint32_t arr = reads[2 * i], idx = reads[2 * i + 1];
             E.reads[E.name_of(E.T(arr))].push_back({arr, idx});
         }
+}
+
+int recheck_core(void* store, const uint32_t* var_desc, size_t n_vars, const uint32_t* values,
+                 const uint32_t* uf_apps, size_t n_uf, const uint32_t* reads, size_t n_reads,
+                 const uint32_t* registry, size_t n_registry, const uint32_t* roots,
+                 size_t n_roots, uint8_t* out) {
+    try {
+        Ev E;
+        E.st = store;
+        parse_registry(E, registry, n_registry);
+        add_part(E, var_desc, n_vars, values, uf_apps, n_uf, reads, n_reads);
         for (size_t i = 0; i < n_roots; i++) out[i] = Ev::bool_of(E.ev(roots[i])) ? 1u : 0u;
         return 0;
     } catch (...) {
         return -1;
     }
+}
+
+// the witness metadata of one lowering result (pflt_result_get) into E, with its values
+void add_result(Ev& E, void* R, const uint32_t* values) {
+    uint64_t info[17];
+    pflt_result_info(R, info);
+    const size_t nvt = info[2], nuf = info[3], na = info[4], nr = info[5];
+    std::vector<uint32_t> desc(4 * nvt + 1), ufs(nuf + 1), rd(na + 2 * nr + 1);
+    pflt_result_get(R, PFLT_GET_VAR_TERMS, desc.data(), nullptr);
+    pflt_result_get(R, PFLT_GET_UF_APPS, ufs.data(), nullptr);
+    pflt_result_get(R, PFLT_GET_READS, rd.data(), nullptr);
+    add_part(E, desc.data(), std::min<size_t>(nvt, info[0]), values, ufs.data(), nuf, rd.data() + na, nr);
 }
 
 }  // namespace
@@ -754,4 +823,103 @@ extern "C" void pflt_recheck_many(void* store, void* const* results, size_t n, c
         status[j] = ok;
     };
     pfpool::parallel_for(n, n_threads, one);
+}
+
+// ---- GPU witnesses kept natively for the GPU-resident ModelCache (mythril_amd/model_cache.py):
+// a witness's interpretation (interp.Witness, bit for bit: the recheck's evaluator) built
+// once from its parts' lowering results and values, with its evaluation memo kept across
+// calls; pflt_witness_values evaluates the quick-sat leaf terms under many witnesses at once.
+struct WitnessH {
+    Ev E;
+    uint64_t reg_serial = 0;  // the registry state its hash specs were parsed from
+    // the values of the caller's leaf slots (dense: a leaf read again is a 32-byte copy, not a
+    // memo lookup); state 0 unknown, 1 evaluated, 2 not evaluable natively
+    uint64_t slot_epoch = 0;
+    std::vector<uint32_t> slot_vals;
+    std::vector<uint8_t> slot_state;
+};
+
+extern "C" void* pflt_witness_new(void* store, void* const* results, size_t n_parts, const uint32_t* values,
+                                  const uint32_t* registry, size_t n_registry, uint64_t reg_serial) {
+    WitnessH* W = new WitnessH();
+    try {
+        W->E.st = store;
+        parse_registry(W->E, registry, n_registry);
+        W->reg_serial = reg_serial;
+        size_t off = 0;
+        for (size_t j = 0; j < n_parts; j++) {
+            uint64_t info[17];
+            pflt_result_info(results[j], info);
+            add_result(W->E, results[j], values + off);
+            off += 8 * info[0];
+        }
+        return W;
+    } catch (...) {
+        delete W;
+        return nullptr;
+    }
+}
+
+extern "C" void pflt_witness_free(void* w) { delete (WitnessH*)w; }
+
+// values of terms[0..n_terms) under each witness: out_limbs[(m * n_terms + i) * 8 ..], ok = 1
+// where the term evaluated (0: the caller evaluates it another way); the witnesses in parallel
+extern "C" void pflt_witness_values(void* const* witnesses, size_t n_models, const uint32_t* terms, size_t n_terms,
+                                    const uint32_t* slots, uint64_t slot_epoch,
+                                    const uint32_t* registry, size_t n_registry, uint64_t reg_serial,
+                                    uint32_t n_threads, uint32_t* out_limbs, uint8_t* ok) {
+    auto one = [&](size_t m) {
+        WitnessH* W = (WitnessH*)witnesses[m];
+        Ev& E = W->E;
+        if (W->reg_serial != reg_serial) {
+            // hashes registered since (interp.Witness reads its live registry): re-parse; the
+            // memo stays, as the Python witness's does
+            try {
+                std::map<uint32_t, KSpec> old;
+                old.swap(E.kspecs);
+                try {
+                    parse_registry(E, registry, n_registry);
+                } catch (...) {
+                    E.kspecs.swap(old);
+                    throw;
+                }
+                W->reg_serial = reg_serial;
+            } catch (...) {
+                for (size_t i = 0; i < n_terms; i++) ok[m * n_terms + i] = 0;
+                return;
+            }
+        }
+        if (slots && W->slot_epoch != slot_epoch) {
+            W->slot_vals.clear();
+            W->slot_state.clear();
+            W->slot_epoch = slot_epoch;
+        }
+        for (size_t i = 0; i < n_terms; i++) {
+            uint32_t* o = out_limbs + (m * n_terms + i) * 8;
+            const uint32_t s = slots ? slots[i] : 0u;
+            if (slots && s < W->slot_state.size() && W->slot_state[s]) {
+                if (W->slot_state[s] == 1) std::copy(&W->slot_vals[8 * (size_t)s], &W->slot_vals[8 * (size_t)s] + 8, o);
+                ok[m * n_terms + i] = W->slot_state[s] == 1;
+                continue;
+            }
+            uint8_t st = 2;
+            try {
+                const uint32_t w = E.width(E.T(terms[i]));
+                const V v = vmask(E.ev(terms[i]), w ? std::min<uint32_t>(w, 256) : 256);
+                for (size_t k = 0; k < 8; k++) o[k] = k < v.size() ? v[k] : 0u;
+                st = 1;
+            } catch (...) {
+            }
+            ok[m * n_terms + i] = st == 1;
+            if (slots) {
+                if (s >= W->slot_state.size()) {
+                    W->slot_state.resize((size_t)s + 1 + s / 2, 0);
+                    W->slot_vals.resize(8 * W->slot_state.size(), 0);
+                }
+                W->slot_state[s] = st;
+                if (st == 1) std::copy(o, o + 8, &W->slot_vals[8 * (size_t)s]);
+            }
+        }
+    };
+    pfpool::parallel_for(n_models, n_threads, one);
 }

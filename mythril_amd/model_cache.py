@@ -36,6 +36,7 @@ decision itself is never approximated: the program computes the conjunction's ex
 from __future__ import annotations
 
 import logging
+import os
 import threading
 import time
 from collections import OrderedDict
@@ -61,6 +62,7 @@ class QuickSatStats:
     models_host: int = 0      # model evaluations done by the reference statement (fallback)
     reference_loops: int = 0  # queries the converter / lowering could not take (reference loop)
     leaf_evals: int = 0       # (model, leaf) values computed (the rest were memoised)
+    leaf_evals_native: int = 0   # of which by the native witness evaluator (pflt_witness_values)
     phase_s: Dict[str, float] = field(default_factory=dict)
 
 
@@ -168,13 +170,60 @@ class LeafValues:
         return None if v is None else int.from_bytes(v, "little")
 
 
-def soa_of(rows: Sequence[bytes], n_vars: int) -> np.ndarray:
-    """[var][limb][cand] u32 (pf_eval_assignments' layout) from per-candidate byte rows
-    (``n_vars`` x 32 bytes each)."""
+class NativeLeafValues(LeafValues):
+    """LeafValues of a GPU witness held natively (native_terms.NativeWitness): ``native_rows``
+    reads the rows of many such models in one native call (the values memoised in the native
+    witness, not here); a model with a leaf the native evaluator declines goes to ``row`` —
+    the Python witness's ``leaf_value`` — as before."""
+
+    __slots__ = ("native", "reg")
+
+    def __init__(self, evaluate: Callable[[T.Term], int], native, reg):
+        super().__init__(evaluate)
+        self.native, self.reg = native, reg
+
+
+# threads of one native leaf evaluation (the witnesses split across them)
+LEAF_THREADS = max(1, min(8, os.cpu_count() or 1))
+
+
+def native_rows(leaf_values: Sequence[Optional[LeafValues]], leaves: Sequence[T.Term]) -> Dict[int, np.ndarray]:
+    """{position in ``leaf_values``: its row as (len(leaves), 8) u32 limbs} for the natively
+    held models whose every leaf evaluated natively — one pflt_witness_values call per term
+    store (and registry)."""
+    groups: Dict[Tuple[int, int], List[int]] = {}
+    for j, lv in enumerate(leaf_values):
+        if isinstance(lv, NativeLeafValues):
+            groups.setdefault((id(lv.native.st), id(lv.reg)), []).append(j)
+    out: Dict[int, np.ndarray] = {}
+    if not groups or not leaves:
+        return out
+    from .smt import native_terms
+
+    for js in groups.values():
+        lvs = [leaf_values[j] for j in js]
+        vals, ok = native_terms.witness_values_many([lv.native for lv in lvs], list(leaves), lvs[0].reg,
+                                                    min(LEAF_THREADS, len(lvs)))
+        full = ok.all(axis=1)
+        for j, m in zip(js, range(len(js))):
+            if full[m]:
+                out[j] = vals[m]
+        with _STATS_LOCK:
+            STATS.leaf_evals_native += int(full.sum()) * len(leaves)
+    return out
+
+
+def soa_of(rows: Sequence, n_vars: int) -> np.ndarray:
+    """[var][limb][cand] u32 (pf_eval_assignments' layout) from per-candidate rows: byte
+    strings (``n_vars`` x 32 bytes each) or (n_vars, 8) u32 limb arrays."""
     n = len(rows)
     if n_vars == 0:
         return np.zeros((1, 8, n), dtype=np.uint32)
-    a = np.frombuffer(b"".join(rows), dtype="<u4").reshape(n, n_vars, 8)
+    if all(isinstance(r, bytes) for r in rows):
+        a = np.frombuffer(b"".join(rows), dtype="<u4").reshape(n, n_vars, 8)
+    else:
+        a = np.stack([np.frombuffer(r, dtype="<u4").reshape(n_vars, 8) if isinstance(r, bytes) else r
+                      for r in rows])
     return np.ascontiguousarray(a.transpose(1, 2, 0), dtype=np.uint32)
 
 
@@ -260,7 +309,9 @@ def _stages(stages, leaves, program, leaf_values, reference, engine, lap, t):
     choice = None
     host = launches = on_engine_n = 0
     for lo, hi in stages:
-        rows = [leaf_values[i].row(leaves) if leaf_values[i] is not None else None for i in range(lo, hi)]
+        nat = native_rows(leaf_values[lo:hi], leaves)
+        rows = [nat[i - lo] if i - lo in nat else leaf_values[i].row(leaves) if leaf_values[i] is not None
+                else None for i in range(lo, hi)]
         t = lap("leaves", t)
         on_engine = [i for i in range(lo, hi) if rows[i - lo] is not None]
         flags: Dict[int, bool] = {}
@@ -339,6 +390,24 @@ def leaf_evaluator(z3, internal):
     return ev
 
 
+def leaf_values_of(z3, internal) -> LeafValues:
+    """The LeafValues of one internal model: natively held for a GPU witness whose buckets
+    were lowered natively (NativeLeafValues), else over ``leaf_evaluator``."""
+    ev = leaf_evaluator(z3, internal)
+    wm = getattr(internal, "internal", None)
+    parts, reg = getattr(wm, "parts", None), getattr(wm, "reg", None)
+    if parts and reg is not None and NATIVE_LEAVES:
+        from .smt import native_terms
+
+        nw = native_terms.NativeWitness.build(parts, reg)
+        if nw is not None:
+            return NativeLeafValues(ev, nw, reg)
+    return LeafValues(ev)
+
+
+# PF_NATIVE_LEAVES=0 evaluates witness leaves in Python (interp.Witness.leaf_value) instead
+NATIVE_LEAVES = os.environ.get("PF_NATIVE_LEAVES", "1") != "0"
+
 _GPU_MODEL_CACHE = None
 
 
@@ -374,7 +443,7 @@ def gpu_model_cache_class():
             key = (id(model), id(im))
             ent = self._leaves.get(key)
             if ent is None or ent[0] is not im:
-                ent = (im, LeafValues(leaf_evaluator(z3, im)))
+                ent = (im, leaf_values_of(z3, im))
                 self._leaves[key] = ent
             return ent[1]
 

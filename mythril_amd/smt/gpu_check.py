@@ -599,6 +599,7 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
             ok = all(w.ev(c) for c in cs)
         if ok:
             out[i] = WitnessModel(w, list(sets[i]))
+            out[i].parts, out[i].reg = parts, reg    # the native witness's ingredients (model_cache)
             # per bucket: _origin(); the set takes the strongest of its buckets: "search" if
             # some bucket needed a later candidate, else "hint" / "parent" / "first" if such a
             # candidate 0 answered some bucket, else "cache"

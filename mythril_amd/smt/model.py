@@ -107,6 +107,8 @@ class WitnessModel:
         self._w = witness
         self.constraints = constraints
         self.origin = "search"   # set by check_sets: "hint" / "first" / "search" / "cache"
+        self.parts = None        # check_sets: the buckets' (lowering, values), and the registry
+        self.reg = None
 
     @property
     def w(self) -> Witness:

@@ -108,6 +108,13 @@ def _bind(L):
         L.pflt_pack_batch.argtypes = [ctypes.POINTER(vp), sz, _u32p, _u32p, u32, _u32p, _u32p, _u32p, _u32p, _u32p]
         L.pflt_recheck_many.argtypes = [vp, ctypes.POINTER(vp), sz, _u32p, _u32p, sz, u32,
                                         ctypes.POINTER(ctypes.c_int8)]
+    if hasattr(L, "pflt_witness_new"):
+        vp, sz, u32, u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint64
+        L.pflt_witness_new.restype = vp
+        L.pflt_witness_new.argtypes = [vp, ctypes.POINTER(vp), sz, _u32p, _u32p, sz, u64]
+        L.pflt_witness_free.argtypes = [vp]
+        L.pflt_witness_values.argtypes = [ctypes.POINTER(vp), sz, _u32p, sz, _u32p, u64, _u32p, sz, u64, u32,
+                                          _u32p, ctypes.POINTER(ctypes.c_uint8)]
     _SIGNED = True
 
 
@@ -271,14 +278,24 @@ def new_generation(limit: int) -> bool:
 def _registry_blob(reg: UFRegistry) -> np.ndarray:
     """The registry in pflt_lower's layout, cached per registry state (hashes only get added:
     the per-width counts and interval starts identify the state)."""
+    return _registry_blob_serial(reg)[0]
+
+
+_BLOB_SERIAL = [0]
+
+
+def _registry_blob_serial(reg: UFRegistry):
+    """(blob, serial): the serial is new for every blob built, so a native witness re-parses
+    its hash specs exactly when the registry's state moved (pflt_witness_values)."""
     key = (id(reg), tuple(reg.actors),
            tuple((n, s.lo, len(s.concrete)) for n, s in reg.keccak.items()))
-    blob = _BLOBS.get(key)
-    if blob is None:
+    ent = _BLOBS.get(key)
+    if ent is None:
         if len(_BLOBS) > 64:
             _BLOBS.clear()
-        blob = _BLOBS[key] = _registry_blob_build(reg)
-    return blob
+        _BLOB_SERIAL[0] += 1
+        ent = _BLOBS[key] = (_registry_blob_build(reg), _BLOB_SERIAL[0])
+    return ent
 
 
 def _registry_blob_build(reg: UFRegistry) -> np.ndarray:
@@ -788,3 +805,98 @@ def ints_of(limbs: np.ndarray) -> List[int]:
     """Rows of 8 u32 limbs -> ints."""
     raw = np.ascontiguousarray(limbs, dtype="<u4").tobytes()
     return [int.from_bytes(raw[32 * i:32 * i + 32], "little") for i in range(len(raw) // 32)]
+
+
+class NativeWitness:
+    """A GPU witness's interpretation held natively (pflt_witness_new, csrc/pf_recheck.cpp):
+    the bucket parts' lowering results with their values — interp.Witness.union of the parts'
+    witnesses, evaluated by the re-check's evaluator with its memo kept between queries.  The
+    GPU-resident ModelCache (mythril_amd/model_cache.py) reads quick-sat leaves through
+    ``values_many``, all cached witnesses in one call."""
+
+    __slots__ = ("st", "h", "parts", "__weakref__")
+
+    def __init__(self, st: TermStore, h, parts):
+        self.st, self.h, self.parts = st, h, parts   # parts keep the results (and store) alive
+
+    @classmethod
+    def build(cls, parts, reg: UFRegistry) -> Optional["NativeWitness"]:
+        """parts = [(NativeLowered, values as limb rows or ints)] of one store; None when the
+        build has no native witnesses or a part is not native."""
+        if not parts or not all(isinstance(lo, NativeLowered) for lo, _ in parts):
+            return None
+        st = parts[0][0].res.st
+        if any(lo.res.st is not st for lo, _ in parts) or not hasattr(st.L, "pflt_witness_new"):
+            return None
+        rows = []
+        for lo, v in parts:
+            nv = int(lo.res.info[0])
+            r = np.ascontiguousarray(v, dtype=np.uint32).reshape(-1, 8) if isinstance(v, np.ndarray) \
+                else ir.limbs_array(list(v)).reshape(-1, 8) if len(v) else np.zeros((0, 8), dtype=np.uint32)
+            if len(r) != nv:
+                return None
+            rows.append(r)
+        vals = np.concatenate(rows) if rows else np.zeros((0, 8), dtype=np.uint32)
+        if vals.size == 0:
+            vals = np.zeros((1, 8), dtype=np.uint32)
+        vals = np.ascontiguousarray(vals).reshape(-1)
+        blob, serial = _registry_blob_serial(reg)
+        hs = (ctypes.c_void_p * len(parts))(*[lo.res.h for lo, _ in parts])
+        with st.lock:
+            h = st.L.pflt_witness_new(st.h, hs, len(parts), vals.ctypes.data_as(_u32p),
+                                      blob.ctypes.data_as(_u32p), len(blob), serial)
+        if not h:
+            return None
+        return cls(st, h, [lo for lo, _ in parts])
+
+    def __del__(self):
+        try:
+            self.st.L.pflt_witness_free(self.h)
+        except Exception:  # noqa: BLE001
+            pass
+
+
+# leaf slots: a dense number per term read through witness_values_many, under which each
+# native witness keeps the value; renumbered (new epoch) when the table grows past _SLOTS_MAX
+_SLOTS: Dict[T.Term, int] = {}
+_SLOT_EPOCH = [1]
+_SLOTS_MAX = 1 << 16
+
+
+def _slots_of(terms: List[T.Term]) -> Tuple[np.ndarray, int]:
+    """(slots, how many of them are new)."""
+    if len(_SLOTS) + len(terms) > _SLOTS_MAX:
+        _SLOTS.clear()
+        _SLOT_EPOCH[0] += 1
+    out = np.empty(len(terms), dtype=np.uint32)
+    n0 = len(_SLOTS)
+    for i, t in enumerate(terms):
+        s = _SLOTS.get(t)
+        if s is None:
+            s = _SLOTS[t] = len(_SLOTS)
+        out[i] = s
+    return out, len(_SLOTS) - n0
+
+
+def witness_values_many(ws: List[NativeWitness], terms: List[T.Term], reg: UFRegistry, threads: int = 1):
+    """(values [model][term][8] u32 limbs, each masked to its term's width; ok [model][term]
+    bool) of ``terms`` under every witness of ``ws`` (one store), natively in one call."""
+    n, k = len(ws), len(terms)
+    out = np.zeros((n, k, 8), dtype=np.uint32)
+    ok = np.zeros((n, k), dtype=np.uint8)
+    if n == 0 or k == 0:
+        return out, ok.astype(bool)
+    st = ws[0].st
+    blob, serial = _registry_blob_serial(reg)
+    hs = (ctypes.c_void_p * n)(*[w.h for w in ws])
+    with st.lock:
+        ids = np.array([st.export(t) for t in terms], dtype=np.uint32)
+        slots, fresh = _slots_of(terms)
+        if not fresh:
+            # every term was read before: mostly 32-byte copies, cheaper than waking the pool
+            threads = 1
+        st.L.pflt_witness_values(hs, n, ids.ctypes.data_as(_u32p), k, slots.ctypes.data_as(_u32p), _SLOT_EPOCH[0],
+                                 blob.ctypes.data_as(_u32p), len(blob),
+                                 serial, max(1, threads), out.ctypes.data_as(_u32p),
+                                 ok.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))
+    return out, ok.astype(bool)

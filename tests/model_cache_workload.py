@@ -130,6 +130,7 @@ def twin(ns, models):
             w._first = w._building = None
             wm2 = WitnessModel(w, wm.constraints)
             wm2.origin = wm.origin
+            wm2.parts, wm2.reg = wm.parts, wm.reg    # a native witness is built per cache entry
             out.append(ns.Model([integration.Z3WitnessView(wm2)]))
         else:
             out.append(ns.Model([copy.deepcopy(im)]))
@@ -231,6 +232,7 @@ def quick_sat_profile(n_models: int = 100, n_scenarios: int = 16, n_queries: int
                 "speedup_mean": round(sum(t_ref) / max(sum(t_gpu), 1e-9), 2),
                 "engine_calls": st.engine_calls, "models_on_engine": st.models_engine,
                 "models_by_reference_statement": st.models_host, "leaf_evals": st.leaf_evals,
+                "leaf_evals_native": st.leaf_evals_native,
                 "phase_ms_per_query": {k: round(1e3 * v / max(st.queries, 1), 4) for k, v in st.phase_s.items()}}
     finally:
         mp.undo()

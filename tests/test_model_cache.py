@@ -142,6 +142,45 @@ def test_a_model_the_leaves_cannot_value_goes_to_the_reference_statement(standin
     assert MC.STATS.models_host == 1 and MC.STATS.models_engine == 1
 
 
+def test_native_witness_leaves_equal_python_witness(standin, monkeypatch):
+    """pflt_witness_values (csrc/pf_recheck.cpp) gives interp.Witness.leaf_value's value for
+    every quick-sat leaf of the corpus queries under every GPU witness of the workload; a
+    registry that gained hashes since is re-parsed (the Python witness reads it live)."""
+    oracle_engine.install(monkeypatch)
+    if not native_terms.has_explicit():
+        pytest.skip("libpflower.so not built")
+    models, _, qs, reg = W.build(z3, standin, n_models=30, n_scenarios=4, n_queries=40)
+    wms = [m.raw[0].internal for m in models if m.raw and isinstance(m.raw[0], integration.Z3WitnessView)]
+    assert wms and all(wm.parts for wm in wms)
+    lvs = [MC.leaf_values_of(z3, integration.Z3WitnessView(wm)) for wm in wms]
+    assert all(isinstance(lv, MC.NativeLeafValues) for lv in lvs)
+    leaves = {}
+    for q in qs:
+        try:
+            ls, _ = MC.explicit_program(T.and_(*q.constraints) if len(q.constraints) > 1 else q.constraints[0])
+        except Exception:  # noqa: BLE001 - a query the explicit lowering declines
+            continue
+        leaves.update(dict.fromkeys(ls))
+    leaves = list(leaves)
+    assert len(leaves) > 10
+    MC.STATS.__init__()
+    rows = MC.native_rows(lvs, leaves)
+    assert len(rows) >= 0.9 * len(lvs) and MC.STATS.leaf_evals_native == len(rows) * len(leaves)
+    for j, r in rows.items():
+        w = wms[j].w
+        for t, limbs in zip(leaves, r):
+            want = w.leaf_value(t) & T.M(max(t.width, 1))
+            assert native_terms.ints_of(limbs[None])[0] == want, t
+    # a hash registered after the witnesses were built: both evaluators see it
+    k = next(iter(reg.keccak))
+    app = T.apply(f"keccak256_{k}", 256, T.const(12345, k))
+    reg.keccak[k].concrete[12345] = 0xABCDEF
+    rows = MC.native_rows(lvs, [app])
+    assert len(rows) == len(lvs)
+    for j, r in rows.items():
+        assert native_terms.ints_of(r)[0] == wms[j].w.leaf_value(app) == 0xABCDEF
+
+
 def test_explicit_lowering_native_equals_python(standin, monkeypatch):
     oracle_engine.install(monkeypatch)
     if not native_terms.has_explicit():
