@@ -260,7 +260,8 @@ def full_pass_leg(args, eng, rank=0, world=1, dist=None, cdev="cuda"):
             "evals": evals, "kernel_s": ks, "wall_s": wall,
             "evals_per_s_kernel": evals / ks if ks else None, "evals_per_s_wall": evals / wall if wall else None,
             "sets_with_witness": int(wit), "chunks_rank0": fs["chunks"],
-            "host_wait_s_rank0": res["host_wait_s"], "host_workers_per_rank": res["host_workers"],
+            "host_wait_s_rank0": res["host_wait_s"], "upload_s_rank0": res.get("upload_s"),
+            "host_workers_per_rank": res["host_workers"],
             "planted_early_exit": {"kernel_s": pks, "sets_with_witness": int(pwit), "cands_decided": int(pdec),
                                    "set_verdicts_per_s_kernel": D / pks if pks else None},
             "seeds": res["seeds"],

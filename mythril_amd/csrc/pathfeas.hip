@@ -24,6 +24,10 @@ namespace {
 std::mutex g_mu;
 thread_local std::string g_err_tls;
 std::string g_err;
+// host work done outside g_mu (pf_batch_create's program checks) reports into t_err, moved
+// into g_err under the lock afterwards
+thread_local bool t_defer_err = false;
+thread_local std::string t_err;
 
 // One entry per initialised device (pf_init's mask): its library stream, timing events for
 // the Keccak launches and the launch geometry inputs.  Batches live on one device each and
@@ -33,6 +37,7 @@ struct Dev {
     int key = -1;           // what the API calls it: the device id (pf_init) or a context id
                             // >= PF_CONTEXT_BASE (pf_init_contexts: several per device)
     hipStream_t stream = nullptr;
+    hipStream_t up_stream = nullptr;  // batch uploads, issued outside g_mu (pf_batch_create)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     int num_cus = 256;
     hipStream_t last_stream = nullptr;  // see switch_stream
@@ -72,7 +77,10 @@ int fail(const char* fmt, ...) {
     va_start(ap, fmt);
     vsnprintf(buf, sizeof(buf), fmt, ap);
     va_end(ap);
-    g_err = buf;
+    if (t_defer_err)
+        t_err = buf;
+    else
+        g_err = buf;
     return -1;
 }
 
@@ -125,10 +133,14 @@ Dev* find_dev(int key) {
 }
 
 constexpr size_t kPoolBlocks = 8;
+// the device pools have their own lock: pf_batch_create takes and returns blocks without
+// g_mu (a search holds g_mu until its results are back)
+std::mutex g_pool_mu;
 
 // a device block of at least `bytes` from the device's pool (smallest that fits and wastes
 // at most 4x), else a new one
 void* pool_acquire(Dev* D, size_t bytes, size_t* cap) {
+    std::lock_guard<std::mutex> pk(g_pool_mu);
     size_t best = SIZE_MAX;
     for (size_t i = 0; i < D->pool.size(); ++i)
         if (D->pool[i].second >= bytes && D->pool[i].second <= 4 * bytes + (1u << 20) &&
@@ -148,13 +160,19 @@ void* pool_acquire(Dev* D, size_t bytes, size_t* cap) {
 
 // free a batch: its block is kept for reuse (the oldest block is released when the pool is
 // full).  Called with no launch of the batch in flight (pf_batch_free drains the device).
+// a block back into its device's pool (the oldest block is released when the pool is full)
+void pool_release(Dev* D, void* p, size_t cap) {
+    std::lock_guard<std::mutex> pk(g_pool_mu);
+    if (D->pool.size() >= kPoolBlocks) {
+        hipFree(D->pool.front().first);
+        D->pool.erase(D->pool.begin());
+    }
+    D->pool.emplace_back(p, cap);
+}
+
 void release_batch(Dev* D, Batch* B) {
     if (D && B->d_mem) {
-        if (D->pool.size() >= kPoolBlocks) {
-            hipFree(D->pool.front().first);
-            D->pool.erase(D->pool.begin());
-        }
-        D->pool.emplace_back(B->d_mem, B->mem_cap);
+        pool_release(D, B->d_mem, B->mem_cap);
         B->d_mem = nullptr;
     }
     delete B;
@@ -307,6 +325,25 @@ uint8_t* pinned_staging(size_t bytes) {
         t.cap = cap;
     }
     return t.p;
+}
+
+// Pinned host staging for batch uploads (pf_batch_create), separate from pinned_staging and
+// guarded by its own lock: an upload fills and copies it without holding g_mu.
+std::mutex g_up_mu;
+uint8_t* upload_staging(size_t bytes) {
+    static uint8_t* p = nullptr;
+    static size_t cap = 0;
+    if (bytes > cap) {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        const size_t c = std::max<size_t>((bytes + (1u << 20) - 1) & ~size_t((1u << 20) - 1), 1u << 20);
+        void* q = nullptr;
+        if (hipHostMalloc(&q, c, hipHostMallocPortable) != hipSuccess) return nullptr;
+        p = static_cast<uint8_t*>(q);
+        cap = c;
+    }
+    return p;
 }
 
 // Wait for B's last search on stream st and read its counters.
@@ -608,6 +645,7 @@ int pf_init(uint64_t device_mask) {
         D.id = D.key = id;
         D.num_cus = prop.multiProcessorCount;
         HIPCHK(hipStreamCreateWithFlags(&D.stream, hipStreamNonBlocking));
+        HIPCHK(hipStreamCreateWithFlags(&D.up_stream, hipStreamNonBlocking));
         HIPCHK(hipEventCreate(&D.ev0));
         HIPCHK(hipEventCreate(&D.ev1));
         g_devs.push_back(D);
@@ -637,6 +675,7 @@ int pf_init_contexts(const int32_t* devices, size_t n, int32_t* ctx_out) {
         D.key = next++;
         D.num_cus = prop.multiProcessorCount;
         HIPCHK(hipStreamCreateWithFlags(&D.stream, hipStreamNonBlocking));
+        HIPCHK(hipStreamCreateWithFlags(&D.up_stream, hipStreamNonBlocking));
         HIPCHK(hipEventCreate(&D.ev0));
         HIPCHK(hipEventCreate(&D.ev1));
         g_devs.push_back(D);
@@ -652,11 +691,15 @@ int pf_shutdown(void) {
     for (auto& D : g_devs) {
         hipSetDevice(D.id);
         hipDeviceSynchronize();
-        for (auto& b : D.pool) hipFree(b.first);
-        D.pool.clear();
+        {
+            std::lock_guard<std::mutex> pk(g_pool_mu);
+            for (auto& b : D.pool) hipFree(b.first);
+            D.pool.clear();
+        }
         hipEventDestroy(D.ev0);
         hipEventDestroy(D.ev1);
         hipStreamDestroy(D.stream);
+        if (D.up_stream) hipStreamDestroy(D.up_stream);
     }
     g_devs.clear();
     g_default = -1;
@@ -753,17 +796,23 @@ int pf_batch_create_on(int device, const uint32_t* code, size_t n_ins, const uin
                        size_t n_const, const uint32_t* schema, size_t n_vars,
                        const uint32_t* parents, size_t n_parents, const pf_set_desc* descs,
                        size_t n_sets, uint64_t* handle_out) {
-    std::lock_guard<std::mutex> lk(g_mu);
-    Dev* Dv = use_dev(device);
-    if (!Dv) return -1;
-    if (!handle_out) return fail("pf_batch_create: null handle_out");
+    // The host half — checks, the device program, the wave order, the staging copy — touches
+    // no library state and runs before the lock: a caller uploading the next batch from
+    // another thread (tools/full_pass.py) overlaps it with a search in progress, which holds
+    // the lock until its results are back.
     std::vector<uint32_t> code_out;
     std::vector<pf_set_desc> descs_out;
     std::vector<uint8_t> wide;
     uint32_t max_vars = 0;
-    if (prepare_program(code, n_ins, consts, n_const, schema, n_vars, n_parents, descs, n_sets, code_out,
-                        descs_out, wide, max_vars))
+    t_defer_err = true;
+    const int prc = prepare_program(code, n_ins, consts, n_const, schema, n_vars, n_parents, descs, n_sets,
+                                    code_out, descs_out, wide, max_vars);
+    t_defer_err = false;
+    if (prc) {
+        std::lock_guard<std::mutex> lk(g_mu);
+        g_err = t_err;
         return -1;
+    }
     code = code_out.data();
     n_ins = code_out.size() / 4;
     descs = descs_out.data();
@@ -799,50 +848,92 @@ int pf_batch_create_on(int device, const uint32_t* code, size_t n_ins, const uin
                  o_order = o_desc + al(n_sets * sizeof(pf_set_desc)), o_found = o_order + al(n_sets * 4),
                  o_scr = o_found + al(std::max<size_t>(n_sets, 1) * 4),
                  total = o_scr + PF_SCRATCH_BYTES;
-    std::vector<uint8_t> stage(o_found, 0);  // found / scratch are cleared by every search
-    auto put = [&](size_t off, const void* src, size_t bytes) {
-        if (bytes && src) memcpy(stage.data() + off, src, bytes);
+    // found / scratch are cleared by every search: the copy ends at o_found
+    auto fill = [&](uint8_t* stage) {
+        memset(stage, 0, o_found);
+        auto put = [&](size_t off, const void* src, size_t bytes) {
+            if (bytes && src) memcpy(stage + off, src, bytes);
+        };
+        put(o_code, code, n_ins * 16);
+        put(o_const, consts, n_const * 32);
+        put(o_schema, schema, n_vars * 16);
+        put(o_par, parents, n_parents * 32);
+        put(o_desc, descs, n_sets * sizeof(pf_set_desc));
+        put(o_order, order.data(), n_sets * 4);
     };
-    put(o_code, code, n_ins * 16);
-    put(o_const, consts, n_const * 32);
-    put(o_schema, schema, n_vars * 16);
-    put(o_par, parents, n_parents * 32);
-    put(o_desc, descs, n_sets * sizeof(pf_set_desc));
-    put(o_order, order.data(), n_sets * 4);
 
-    Batch* B = new Batch();
-    B->device = Dv->key;
-    B->n_ins = n_ins;
-    B->n_const = n_const;
-    B->n_vars = n_vars;
-    B->n_parents = n_parents;
-    B->n_sets = n_sets;
-    B->max_vars = max_vars;
-    B->n_narrow = (size_t)std::count(wide.begin(), wide.end(), (uint8_t)0);
-    B->all_parented = std::all_of(descs, descs + n_sets, [](const pf_set_desc& d) { return d.parent_off != PF_NO_PARENT; });
-    B->h_descs.assign(descs, descs + n_sets);
-    B->d_mem = pool_acquire(Dv, total, &B->mem_cap);
-    if (!B->d_mem) {
-        delete B;
-        return fail("pf_batch_create: hipMalloc(%zu) failed", total);
+    // No g_mu from here on either: the device lookup reads g_devs (fixed after pf_init), the
+    // block comes from the pool under its own lock, errors go through t_err.
+    Batch* B = nullptr;
+    int dev_id = -1;
+    hipStream_t ups = nullptr;
+    auto report = [](int rc) {
+        t_defer_err = false;
+        std::lock_guard<std::mutex> lk(g_mu);
+        g_err = t_err;
+        return rc;
+    };
+    t_defer_err = true;
+    {
+        Dev* Dv = use_dev(device);
+        if (!Dv) return report(-1);
+        if (!handle_out) return report(fail("pf_batch_create: null handle_out"));
+        B = new Batch();
+        B->device = Dv->key;
+        B->n_ins = n_ins;
+        B->n_const = n_const;
+        B->n_vars = n_vars;
+        B->n_parents = n_parents;
+        B->n_sets = n_sets;
+        B->max_vars = max_vars;
+        B->n_narrow = (size_t)std::count(wide.begin(), wide.end(), (uint8_t)0);
+        B->all_parented = std::all_of(descs, descs + n_sets, [](const pf_set_desc& d) { return d.parent_off != PF_NO_PARENT; });
+        B->h_descs.assign(descs, descs + n_sets);
+        B->d_mem = pool_acquire(Dv, total, &B->mem_cap);
+        if (!B->d_mem) {
+            delete B;
+            return report(fail("pf_batch_create: hipMalloc(%zu) failed", total));
+        }
+        uint8_t* base = static_cast<uint8_t*>(B->d_mem);
+        B->d_code = reinterpret_cast<uint4*>(base + o_code);
+        B->d_consts = reinterpret_cast<uint32_t*>(base + o_const);
+        B->d_schema = reinterpret_cast<uint4*>(base + o_schema);
+        B->d_parents = reinterpret_cast<uint32_t*>(base + o_par);
+        B->d_descs = reinterpret_cast<pf_set_desc*>(base + o_desc);
+        B->d_order = reinterpret_cast<uint32_t*>(base + o_order);
+        B->d_found = reinterpret_cast<uint32_t*>(base + o_found);
+        B->d_scratch = reinterpret_cast<uint32_t*>(base + o_scr);
+        if (hipEventCreate(&B->ev0) != hipSuccess || hipEventCreate(&B->ev1) != hipSuccess) {
+            const int rc = fail("pf_batch_create: hipEventCreate failed");
+            release_batch(Dv, B);
+            return report(rc);
+        }
+        dev_id = Dv->id;
+        ups = Dv->up_stream;
     }
-    uint8_t* base = static_cast<uint8_t*>(B->d_mem);
-    B->d_code = reinterpret_cast<uint4*>(base + o_code);
-    B->d_consts = reinterpret_cast<uint32_t*>(base + o_const);
-    B->d_schema = reinterpret_cast<uint4*>(base + o_schema);
-    B->d_parents = reinterpret_cast<uint32_t*>(base + o_par);
-    B->d_descs = reinterpret_cast<pf_set_desc*>(base + o_desc);
-    B->d_order = reinterpret_cast<uint32_t*>(base + o_order);
-    B->d_found = reinterpret_cast<uint32_t*>(base + o_found);
-    B->d_scratch = reinterpret_cast<uint32_t*>(base + o_scr);
-    int rc = 0;
-    if (hipMemcpy(B->d_mem, stage.data(), stage.size(), hipMemcpyHostToDevice) != hipSuccess)
-        rc = fail("pf_batch_create: hipMemcpy of %zu bytes failed", stage.size());
-    if (!rc && (hipEventCreate(&B->ev0) != hipSuccess || hipEventCreate(&B->ev1) != hipSuccess))
-        rc = fail("pf_batch_create: hipEventCreate failed");
-    if (rc) {
-        release_batch(Dv, B);
-        return -1;
+    t_defer_err = false;
+    // the copy itself outside g_mu, on the device's upload stream through the upload staging
+    // buffer (a search holding g_mu meanwhile runs on the library stream)
+    bool ok = true;
+    {
+        std::lock_guard<std::mutex> lk(g_up_mu);
+        ok = hipSetDevice(dev_id) == hipSuccess;
+        uint8_t* pin = ok ? upload_staging(o_found) : nullptr;
+        if (pin) {
+            fill(pin);
+            ok = hipMemcpyAsync(B->d_mem, pin, o_found, hipMemcpyHostToDevice, ups) == hipSuccess &&
+                 hipStreamSynchronize(ups) == hipSuccess;
+        } else if (ok) {
+            std::vector<uint8_t> stage(o_found);
+            fill(stage.data());
+            ok = hipMemcpy(B->d_mem, stage.data(), o_found, hipMemcpyHostToDevice) == hipSuccess;
+        }
+    }
+    if (!ok) {
+        t_defer_err = true;
+        const int rc = fail("pf_batch_create: hipMemcpy of %zu bytes failed", o_found);
+        release_batch(use_dev(B->device), B);
+        return report(rc);
     }
     *handle_out = (uint64_t)(uintptr_t)B;
     return 0;
@@ -1001,11 +1092,7 @@ int pf_materialize(uint64_t handle, uint64_t global_seed, const uint32_t* set_id
         return fail("pf_materialize: HIP call failed");
     }
     // back to the pool (the stream is drained)
-    if (D->pool.size() >= kPoolBlocks) {
-        hipFree(D->pool.front().first);
-        D->pool.erase(D->pool.begin());
-    }
-    D->pool.emplace_back(dm, cap);
+    pool_release(D, dm, cap);
     return 0;
 }
 
@@ -1061,11 +1148,7 @@ int pf_eval_assignments(uint64_t handle, uint32_t set, const uint32_t* soa, uint
         if (hipDeviceSynchronize() == hipSuccess) hipFree(dm);
         return fail("pf_eval_assignments: HIP call failed");
     }
-    if (D->pool.size() >= kPoolBlocks) {
-        hipFree(D->pool.front().first);
-        D->pool.erase(D->pool.begin());
-    }
-    D->pool.emplace_back(dm, cap);
+    pool_release(D, dm, cap);
     return 0;
 }
 
@@ -1126,11 +1209,7 @@ int pf_eval_program(int device, const uint32_t* code, size_t n_ins, const uint32
         return fail("pf_eval_program: HIP call failed");
     }
     memcpy(sat_out, pin, n_cand);
-    if (D->pool.size() >= kPoolBlocks) {
-        hipFree(D->pool.front().first);
-        D->pool.erase(D->pool.begin());
-    }
-    D->pool.emplace_back(dm, cap);
+    pool_release(D, dm, cap);
     return 0;
 }
 
@@ -1188,11 +1267,7 @@ int pf_keccak256_batch(const uint8_t* data, const uint64_t* offsets, size_t n, u
         return fail("pf_keccak256_batch: HIP call failed");
     }
     if (pin) memcpy(out32, pin, n * 32);
-    if (D->pool.size() >= kPoolBlocks) {
-        hipFree(D->pool.front().first);
-        D->pool.erase(D->pool.begin());
-    }
-    D->pool.emplace_back(dm, cap);
+    pool_release(D, dm, cap);
     return 0;
 }
 

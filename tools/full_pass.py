@@ -77,19 +77,67 @@ def run_full_pass(eng, dags: int = 1_000_000, chunk: int = 65536, piece: int = 2
     import queue
     import threading
 
-    todo: "queue.Queue" = queue.Queue(maxsize=2)
+    # One uploader thread per leg: pf_batch_create's host half (checks, device program,
+    # staging) runs outside the library lock, but its copy is queued behind the search in
+    # progress (the runtime's H2D copy waits for the busy CUs) — one thread per leg keeps the
+    # next chunk's host work from waiting behind the previous leg's blocked copy.
+    todos = {leg: queue.Queue(maxsize=2) for leg in legs}
+    readys = {leg: queue.Queue(maxsize=2) for leg in legs}
     errors: list = []
+    t_upload = [0.0]
+
+    def put_checked(q, item) -> bool:
+        while not errors:
+            try:
+                q.put(item, timeout=0.5)
+                return True
+            except queue.Full:
+                continue
+        return False
+
+    def upload_loop(leg, which):
+        try:
+            while True:
+                item = todos[leg].get()
+                if item is None:
+                    break
+                k, n, packed = item
+                tu = time.perf_counter()
+                db = eng.upload(_arrays_batch(packed[which], n))
+                t_upload[0] += time.perf_counter() - tu
+                if progress is not None:
+                    progress({"upload": leg, "chunk": k, "t0": tu - t_wall, "t1": time.perf_counter() - t_wall})
+                if not put_checked(readys[leg], (k, n, db)):
+                    db.free()
+                    break
+        except Exception as e:  # noqa: BLE001 - reported by the packing thread
+            errors.append(e)
+        finally:
+            readys[leg].put(None)   # the device loop drains until it sees this
+
+    def drain():
+        for leg in legs:
+            while True:
+                it = readys[leg].get()
+                if it is None:
+                    break
+                it[2].free()
 
     def device_loop():
         while True:
-            item = todo.get()
-            if item is None:
+            items = [readys[leg].get() for leg in legs]
+            if any(it is None for it in items):
+                for leg, it in zip(legs, items):
+                    if it is not None:
+                        it[2].free()
+                        while readys[leg].get() is not None:
+                            pass
                 return
-            k, n, packed = item
             try:
-                for leg, (which, flags) in legs.items():
-                    db = eng.upload(_arrays_batch(packed[which], n))
+                for (leg, (which, flags)), (k, n, db) in zip(legs.items(), items):
+                    tc = time.perf_counter()
                     r = eng.check(db, budget=budget, seed=seed, flags=flags)
+                    tc1 = time.perf_counter()
                     db.free()
                     a = acc[leg]
                     a["kernel_ms"] += r.kernel_ms
@@ -98,24 +146,36 @@ def run_full_pass(eng, dags: int = 1_000_000, chunk: int = 65536, piece: int = 2
                     a["sat"] += int(r.sat.sum())
                     if progress is not None:
                         progress({"leg": leg, "chunk": k, "sets": n, "kernel_ms": r.kernel_ms,
-                                  "sat": int(r.sat.sum())})
+                                  "sat": int(r.sat.sum()), "t0": tc - t_wall, "t1": tc1 - t_wall})
             except Exception as e:  # noqa: BLE001 - reported by the packing thread
                 errors.append(e)
+                for _, _, db in items:
+                    db.free()
+                drain()
                 return
 
+    ups = [threading.Thread(target=upload_loop, args=(leg, which), daemon=True) for leg, (which, _) in legs.items()]
+    for t in ups:
+        t.start()
     dev = threading.Thread(target=device_loop, daemon=True)
     dev.start()
     with pool:
         tasks = [(first + f, min(piece, dags - f)) for f in range(0, dags, piece)]
         futs = [pool.submit(_build, t) for t in tasks]
         pending, n_pending = [], 0
+        # the first chunks ramp up (chunk / 8, / 4, / 2, then chunk): the device starts after
+        # a few pieces are built instead of a whole chunk's worth
+        target = max(piece, chunk // 8)
         for i, fu in enumerate(futs):
             tw = time.perf_counter()
             pending.append(fu.result())
             t_wait += time.perf_counter() - tw
+            if progress is not None and i + 1 == len(futs):
+                progress({"built_all": time.perf_counter() - t_wall})
             n_pending += pending[-1][1]
-            if n_pending < chunk and i + 1 < len(futs):
+            if n_pending < target and i + 1 < len(futs):
                 continue
+            target = min(chunk, 2 * target)
             chunks += 1
             packed = []
             for which in (0, 1):
@@ -135,16 +195,18 @@ def run_full_pass(eng, dags: int = 1_000_000, chunk: int = 65536, piece: int = 2
                     codes.append(c); consts.append(k); schemas.append(s_); parents.append(p); descs.append(d)
                     oc += len(c); ok += len(k); os_ += len(s_); op += len(p)
                 packed.append(tuple(np.concatenate(x) for x in (codes, consts, schemas, parents, descs)))
-            while not errors:
-                try:
-                    todo.put((chunks, n_pending, packed), timeout=1.0)
-                    break
-                except queue.Full:
-                    continue
-            if errors:
+            if not all(put_checked(todos[leg], (chunks, n_pending, packed)) for leg in legs):
                 break
             pending, n_pending = [], 0
-    todo.put(None)
+    for leg, t in zip(legs, ups):
+        while t.is_alive():
+            try:
+                todos[leg].put(None, timeout=0.5)
+                break
+            except queue.Full:
+                continue
+    for t in ups:
+        t.join()
     dev.join()
     if errors:
         raise errors[0]
@@ -157,6 +219,7 @@ def run_full_pass(eng, dags: int = 1_000_000, chunk: int = 65536, piece: int = 2
                     "set_verdicts_per_s_kernel": dags / ks if ks else None}
     res["total_wall_s"] = time.perf_counter() - t_wall
     res["host_wait_s"] = t_wait
+    res["upload_s"] = t_upload[0]   # pf_batch_create calls, overlapped with the searches
     res["host_workers"] = workers
     res["full_sweep"]["evals_per_s_wall"] = res["full_sweep"]["evals_full"] / res["total_wall_s"]
     return res
@@ -177,8 +240,16 @@ def main():
 
     # the workers are started (spawned) by run_full_pass; this process owns the GPU
     eng = Engine(0)
+    import threading
+
+    plock = threading.Lock()   # progress comes from the device and uploader threads
+
+    def progress(d):
+        with plock:
+            print(json.dumps(d), flush=True)
+
     res = run_full_pass(eng, args.dags, args.chunk, args.piece, args.workers, args.budget, args.seed,
-                        progress=lambda d: print(json.dumps(d), flush=True), mp_context="spawn")
+                        progress=progress, mp_context="spawn")
     line = json.dumps(res)
     print(line, flush=True)
     if args.out:
