@@ -123,6 +123,15 @@ int pf_eval_assignments(uint64_t handle, uint32_t set, const uint32_t* soa, uint
 int pf_eval_program(int device, const uint32_t* code, size_t n_ins, const uint32_t* consts, size_t n_const,
                     const uint32_t* schema, size_t n_vars, const uint32_t* soa, uint32_t n_cand,
                     uint8_t* sat_out);
+/* Several programs (n_sets descriptors over code / consts / schema, as for pf_batch_create)
+ * over one call's explicit assignments: set s reads its variables from SoA rows
+ * descs[s].var_off .. + n_vars(s) ([var][limb][cand] u32 over all sets' variables); one wave
+ * per (set, 64 candidates), all in one launch; sat_out[s * n_cand + cand].  The quick-sat of
+ * the GPU-resident ModelCache with the query's conjuncts split into groups (the same
+ * reference loop as pf_eval_program: support_utils.py:57-71), the groups side by side. */
+int pf_eval_programs(int device, const uint32_t* code, size_t n_ins, const uint32_t* consts, size_t n_const,
+                     const uint32_t* schema, size_t n_vars, const pf_set_desc* descs, size_t n_sets,
+                     const uint32_t* soa, uint32_t n_cand, uint8_t* sat_out);
 int pf_eval_assignments_dev(uint64_t handle, uint32_t set, const uint32_t* d_soa,
                             uint32_t n_cand, uint8_t* d_sat_out, void* stream);
 

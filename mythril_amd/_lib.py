@@ -68,6 +68,8 @@ SIGNATURES = {
                                            ctypes.c_uint32, _u8p]),
     "pf_eval_program": (ctypes.c_int, [ctypes.c_int, _u32p, _sz, _u32p, _sz, _u32p, _sz, _u32p,
                                        ctypes.c_uint32, _u8p]),
+    "pf_eval_programs": (ctypes.c_int, [ctypes.c_int, _u32p, _sz, _u32p, _sz, _u32p, _sz, _u32p, _sz, _u32p,
+                                        ctypes.c_uint32, _u8p]),
     "pf_eval_assignments_dev": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p,
                                                ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
     "pf_device_program": (ctypes.c_int, [_u32p, _sz, _u32p, _sz, _u32p, _sz, _u32p, ctypes.POINTER(_sz), _u32p]),

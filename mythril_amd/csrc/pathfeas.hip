@@ -1152,65 +1152,83 @@ int pf_eval_assignments(uint64_t handle, uint32_t set, const uint32_t* soa, uint
     return 0;
 }
 
-int pf_eval_program(int device, const uint32_t* code, size_t n_ins, const uint32_t* consts, size_t n_const,
-                    const uint32_t* schema, size_t n_vars, const uint32_t* soa, uint32_t n_cand,
-                    uint8_t* sat_out) {
-    std::lock_guard<std::mutex> lk(g_mu);
+// pf_eval_program / pf_eval_programs: the program(s) validated and rewritten exactly as by
+// pf_batch_create (prepare_program), one pooled block [code | consts + zero entry | schema |
+// descs | assignments | verdicts] and one copy each way through the pinned staging buffer;
+// the stream is synchronised, not the device (no batch object, no events): the quick-sat call
+// of the GPU-resident ModelCache, once or twice per objective-free query
+// (mythril_amd/model_cache.py)
+static int eval_programs(const char* who, int device, const uint32_t* code, size_t n_ins, const uint32_t* consts,
+                         size_t n_const, const uint32_t* schema, size_t n_vars, const pf_set_desc* descs,
+                         size_t n_sets, const uint32_t* soa, uint32_t n_cand, uint8_t* sat_out) {
     Dev* D = use_dev(device);
     if (!D) return -1;
-    if (n_cand == 0) return 0;
-    if (!code || !sat_out || (n_vars && !soa)) return fail("pf_eval_program: null argument");
-    const pf_set_desc d0{0u, (uint32_t)n_ins, 0u, (uint32_t)n_const, 0u, (uint32_t)n_vars, 0u, PF_NO_PARENT};
+    if (n_cand == 0 || n_sets == 0) return 0;
+    if (!code || !sat_out || !descs || (n_vars && !soa)) return fail("%s: null argument", who);
+    if (n_sets > 65535) return fail("%s: %zu programs (at most 65535)", who, n_sets);
     std::vector<uint32_t> code_out;
     std::vector<pf_set_desc> descs_out;
     std::vector<uint8_t> wide;
     uint32_t max_vars = 0;
-    if (prepare_program(code, n_ins, consts, n_const, schema, n_vars, 0, &d0, 1, code_out, descs_out, wide,
+    if (prepare_program(code, n_ins, consts, n_const, schema, n_vars, 0, descs, n_sets, code_out, descs_out, wide,
                         max_vars))
         return -1;
-    // one pooled block [code | consts + zero entry | schema | desc | assignments | verdicts] and
-    // one copy each way through the pinned staging buffer; the stream is synchronised, not
-    // the device (no batch object, no events): the quick-sat call of the GPU-resident
-    // ModelCache, once or twice per objective-free query (mythril_amd/model_cache.py)
     auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
-    const size_t nv = std::max<size_t>(n_vars, 1), n_dev = code_out.size() / 4;
+    const size_t nv = std::max<size_t>(n_vars, 1), n_dev = code_out.size() / 4, n_out = n_sets * (size_t)n_cand;
     const size_t soa_bytes = nv * 8 * (size_t)n_cand * 4;
     const size_t o_code = 0, o_const = al(n_dev * 16), o_schema = o_const + al(n_const * 32 + 32),
-                 o_desc = o_schema + al(nv * 16), o_soa = o_desc + al(sizeof(pf_set_desc)),
-                 o_out = o_soa + al(soa_bytes), total = o_out + n_cand;
-    uint8_t* pin = pinned_staging(std::max<size_t>(o_out, n_cand));
-    if (!pin) return fail("pf_eval_program: no pinned staging buffer");
+                 o_desc = o_schema + al(nv * 16), o_soa = o_desc + al(n_sets * sizeof(pf_set_desc)),
+                 o_out = o_soa + al(soa_bytes), total = o_out + n_out;
+    uint8_t* pin = pinned_staging(std::max<size_t>(o_out, n_out));
+    if (!pin) return fail("%s: no pinned staging buffer", who);
     memset(pin, 0, o_out);
     memcpy(pin + o_code, code_out.data(), n_dev * 16);
     if (n_const) memcpy(pin + o_const, consts, n_const * 32);
     if (n_vars) memcpy(pin + o_schema, schema, n_vars * 16);
-    memcpy(pin + o_desc, descs_out.data(), sizeof(pf_set_desc));
+    memcpy(pin + o_desc, descs_out.data(), n_sets * sizeof(pf_set_desc));
     if (n_vars) memcpy(pin + o_soa, soa, soa_bytes);
     hipStream_t st = D->stream;
     if (switch_stream(D, st)) return -1;
     size_t cap = 0;
     uint8_t* dm = static_cast<uint8_t*>(pool_acquire(D, total, &cap));
-    if (!dm) return fail("pf_eval_program: hipMalloc(%zu) failed", total);
+    if (!dm) return fail("%s: hipMalloc(%zu) failed", who, total);
     int rc = 0;
     if (hipMemcpyAsync(dm, pin, o_out, hipMemcpyHostToDevice, st) != hipSuccess) rc = -1;
     if (!rc) {
-        hipLaunchKernelGGL(pf_eval_soa_kernel, dim3((n_cand + 255) / 256), dim3(256), 0, st,
-                           reinterpret_cast<const pf_set_desc*>(dm + o_desc), 0u,
+        hipLaunchKernelGGL(pf_eval_soa_sets_kernel, dim3((n_cand + 63) / 64, (unsigned)n_sets), dim3(64), 0, st,
+                           reinterpret_cast<const pf_set_desc*>(dm + o_desc),
                            reinterpret_cast<const uint4*>(dm + o_code), reinterpret_cast<const uint32_t*>(dm + o_const),
-                           reinterpret_cast<const uint4*>(dm + o_schema), static_cast<const uint32_t*>(nullptr),
+                           reinterpret_cast<const uint4*>(dm + o_schema),
                            reinterpret_cast<const uint32_t*>(dm + o_soa), n_cand, dm + o_out);
         if (hipGetLastError() != hipSuccess ||
-            hipMemcpyAsync(pin, dm + o_out, n_cand, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipMemcpyAsync(pin, dm + o_out, n_out, hipMemcpyDeviceToHost, st) != hipSuccess ||
             hipStreamSynchronize(st) != hipSuccess)
             rc = -1;
     }
     if (rc) {
         if (hipDeviceSynchronize() == hipSuccess) hipFree(dm);
-        return fail("pf_eval_program: HIP call failed");
+        return fail("%s: HIP call failed", who);
     }
-    memcpy(sat_out, pin, n_cand);
+    memcpy(sat_out, pin, n_out);
     pool_release(D, dm, cap);
     return 0;
+}
+
+int pf_eval_program(int device, const uint32_t* code, size_t n_ins, const uint32_t* consts, size_t n_const,
+                    const uint32_t* schema, size_t n_vars, const uint32_t* soa, uint32_t n_cand,
+                    uint8_t* sat_out) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    const pf_set_desc d0{0u, (uint32_t)n_ins, 0u, (uint32_t)n_const, 0u, (uint32_t)n_vars, 0u, PF_NO_PARENT};
+    return eval_programs("pf_eval_program", device, code, n_ins, consts, n_const, schema, n_vars, &d0, 1, soa,
+                         n_cand, sat_out);
+}
+
+int pf_eval_programs(int device, const uint32_t* code, size_t n_ins, const uint32_t* consts, size_t n_const,
+                     const uint32_t* schema, size_t n_vars, const pf_set_desc* descs, size_t n_sets,
+                     const uint32_t* soa, uint32_t n_cand, uint8_t* sat_out) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    return eval_programs("pf_eval_programs", device, code, n_ins, consts, n_const, schema, n_vars, descs, n_sets,
+                         soa, n_cand, sat_out);
 }
 
 int pf_eval_assignments_dev(uint64_t handle, uint32_t set, const uint32_t* d_soa,

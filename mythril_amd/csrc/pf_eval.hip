@@ -1167,6 +1167,30 @@ pf_eval_soa_kernel(const pf_set_desc* __restrict__ descs, uint32_t set,
     if (active) out[cand] = (uint8_t)sat;
 }
 
+// ---- several programs over one set of explicit assignments ----------------------------
+// grid (ceil(n_cand / 64), n_sets), one wave per block: block (x, s) runs set s's program on
+// candidates 64x .. 64x + 63, its variables at rows descs[s].var_off.. of the SoA; verdicts
+// out[s * n_cand + cand].  The GPU-resident ModelCache splits a query's conjuncts into groups
+// lowered as separate sets, so the groups run side by side instead of one lone wave walking
+// the whole conjunction (mythril_amd/model_cache.py).
+extern "C" __global__ void __launch_bounds__(64)
+pf_eval_soa_sets_kernel(const pf_set_desc* __restrict__ descs, const uint4* __restrict__ code,
+                        const uint32_t* __restrict__ consts, const uint4* __restrict__ schema,
+                        const uint32_t* __restrict__ soa, uint32_t n_cand, uint8_t* __restrict__ out) {
+    const uint32_t set = blockIdx.y;
+    const uint32_t cand = blockIdx.x * 64u + threadIdx.x;
+    const bool active = cand < n_cand;
+    const SetCtx S = make_ctx(descs, set, code, consts, schema, nullptr, 0ull);
+    const uint32_t* soa_s = soa + (size_t)__builtin_amdgcn_readfirstlane(descs[set].var_off) * 8u * n_cand;
+    __shared__ uint2 pf_exp_lds[PF_LDS_ENTRIES * 4 * 64];
+    uint32_t complete = 0;
+    uint64_t ops = 0;
+    UnitProf prof;
+    uint32_t sat = run_program<MODE_SOA, 16>(S, active ? cand : 0u, active, 0u, soa_s, n_cand,
+                                         exp_tbl_of(pf_exp_lds), &complete, &ops, &prof);
+    if (active) out[(size_t)set * n_cand + cand] = (uint8_t)sat;
+}
+
 // ---- materialise witness assignments --------------------------------------------------
 // one thread per (request, variable); out offset per request given by req_off (in vars)
 extern "C" __global__ void __launch_bounds__(256)

@@ -884,12 +884,46 @@ struct Lowering {
         lerr("%u-bit %s", wd, r.name.empty() ? "op" : r.name.c_str());
     }
 
+    // ExplicitLowering._lshr_concat: bvlshr(concat(p0 .. pn-1), k) without the low parts the
+    // shift discards whole — concat(p0 .. pj) >> (k - their width), zero-extended to wd
+    bool lshr_concat(const std::vector<uint32_t>& parts, const Big& kv, uint32_t wd, int32_t* out) {
+        uint64_t k = (uint64_t)limb(kv, 0) | ((uint64_t)limb(kv, 1) << 32);
+        for (size_t i = 2; i < kv.size(); i++)
+            if (kv[i]) k = UINT64_MAX;  // past any width
+        size_t j = parts.size();
+        uint64_t drop = 0;
+        while (j > 1 && drop + width(parts[j - 1]) <= k) {
+            drop += width(parts[j - 1]);
+            j--;
+        }
+        if (j == parts.size()) return false;
+        int32_t hi = node(parts[0]);
+        uint32_t hw = width(parts[0]);
+        for (size_t i = 1; i < j; i++) {
+            const uint32_t pw = width(parts[i]);
+            hi = d.op(PF_W_CONCAT, hw + pw, {hi, node(parts[i])}, pw);
+            hw += pw;
+        }
+        const uint64_t rem = k - drop;
+        if (rem >= hw) {
+            *out = d.cnst((uint64_t)0, wd);
+            return true;
+        }
+        if (rem) hi = d.op(PF_W_LSHR, hw, {hi, d.cnst(rem, hw)});
+        *out = d.op(PF_W_MOV, wd, {hi});
+        return true;
+    }
+
     Val lower_bv(uint32_t t) {
         const TermRec& r = T(t);
         const uint32_t wd = width(t);
         if (wd > 256) return lower_wide(t);
         if (r.op == T_BV) return V(d.cnst(c8_of(r.val, wd), wd));
         if (r.op == T_VAR) return V(mkvar(r.name, wd, VarTerm{PFLT_VT_TERM, t, 0, 0}, nullptr, nullptr));
+        if (explicit_ && r.op == PFLT_BVLSHR && T(r.args[1]).op == T_BV && T(r.args[0]).op == T_CONCAT) {
+            int32_t nd;
+            if (lshr_concat(T(r.args[0]).args, T(r.args[1]).val, wd, &nd)) return V(nd);
+        }
         if (const uint32_t opc = wbin_op(r.op)) return V(d.op(opc, wd, {node(r.args[0]), node(r.args[1])}));
         if (r.op == T_BVNOT) return V(d.op(PF_W_NOT, wd, {node(r.args[0])}));
         if (r.op == T_BVNEG) return V(d.op(PF_W_NEG, wd, {node(r.args[0])}));

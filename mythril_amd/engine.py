@@ -225,6 +225,26 @@ class Engine:
             _lib.ptr_u32(soa.reshape(-1)), n_cand, _lib.ptr_u8(out)), "pf_eval_program")
         return out[:n_cand].astype(bool)
 
+    def eval_programs(self, pack, soa: np.ndarray) -> np.ndarray:
+        """SAT flags [program][candidate] of several programs over one call's explicit
+        candidates (pf_eval_programs: one launch, a wave per program and 64 candidates).
+        ``pack`` = the flat (code, consts, schema, descs) u32 arrays of an ir.Batch over the
+        programs; ``soa`` = [var][limb][cand] over all programs' variables, program after
+        program (their descriptors' var_off)."""
+        code, consts, schema, descs = pack
+        n_sets = descs.size // 8
+        soa = np.ascontiguousarray(soa, dtype=np.uint32)
+        n_cand = soa.shape[-1]
+        out = np.zeros(max(n_sets * n_cand, 1), dtype=np.uint8)
+        z = np.zeros(8, dtype=np.uint32)
+        _lib.check(_lib.lib().pf_eval_programs(
+            self.device, _lib.ptr_u32(code), code.size // 4,
+            _lib.ptr_u32(consts if consts.size else z), consts.size // 8,
+            _lib.ptr_u32(schema if schema.size else z), schema.size // 4,
+            _lib.ptr_u32(descs), n_sets,
+            _lib.ptr_u32(soa.reshape(-1) if soa.size else z), n_cand, _lib.ptr_u8(out)), "pf_eval_programs")
+        return out[:n_sets * n_cand].reshape(n_sets, n_cand).astype(bool)
+
     # ---- keccak -------------------------------------------------------------------
     def keccak256(self, messages: Sequence[bytes]) -> List[bytes]:
         n = len(messages)

@@ -117,8 +117,133 @@ def lower_explicit_py(conj: List[T.Term]):
 
 
 def n_vars(program) -> int:
+    if isinstance(program, ExplicitGroups):
+        return len(program.gather)
     r = getattr(program, "native_result", None)
     return int(r.info[0]) if r is not None else len(program.vars)
+
+
+# ---- conjunct groups: a long query as several programs side by side ----------------------
+# One quick-sat launch is a lone wave walking the whole conjunction (~0.45 us per bytecode
+# instruction, §3 of DESIGN.md; LASER's queries lower to ~500 instructions).  With
+# SPLIT_NODES > 0, a query whose (flattened) conjuncts add up to more than SPLIT_NODES term
+# nodes is lowered as up to MAX_GROUPS programs over balanced groups of its conjuncts
+# (largest first onto the lightest group), all run in one launch (pf_eval_programs: one wave
+# per group and 64 models); a model satisfies the query iff it satisfies every group.
+# Shared subterms are lowered once per group.  Off by default: measured on the quick-sat
+# workload (profiles/r05t_quick_sat_split.md) the launches got 0.09 ms cheaper per query and
+# the lowering 0.3 ms dearer (one native lowering per group, the shared keccak terms lowered
+# again in each).  PF_QS_SPLIT_NODES turns it on.
+MAX_GROUPS = 8
+SPLIT_NODES = int(os.environ.get("PF_QS_SPLIT_NODES", "0"))
+
+
+class ExplicitGroups:
+    """The programs of one query's conjunct groups: ``gather`` lists, group after group,
+    the position in the query's leaf list of each program variable (the SoA rows the
+    programs read, in pf_eval_programs' order); ``pack`` the packed arrays, made once."""
+
+    __slots__ = ("programs", "gather", "offsets", "_pack")
+
+    def __init__(self, programs, gather: np.ndarray, offsets: List[int]):
+        self.programs, self.gather, self.offsets = programs, gather, offsets
+        self._pack = None
+
+    def pack(self):
+        if self._pack is None:
+            from .ir import Batch
+
+            b = Batch(list(self.programs))
+            self._pack = tuple(np.ascontiguousarray(a, dtype=np.uint32).reshape(-1)
+                               for a in (b.code, b.consts, b.schema, b.descs))
+        return self._pack
+
+
+def _term_nodes(t: T.Term) -> int:
+    seen = set()
+    stack = [t]
+    while stack:
+        x = stack.pop()
+        if x in seen:
+            continue
+        seen.add(x)
+        stack.extend(x.args)
+    return len(seen)
+
+
+def flat_conjuncts(conj: List[T.Term]) -> List[T.Term]:
+    """The conjuncts with nested ``and``s opened (the keccak manager's conditions arrive as
+    one conjunct of nested ands), in order."""
+    out: List[T.Term] = []
+    stack = list(reversed(conj))
+    while stack:
+        c = stack.pop()
+        if c.op == "and":
+            stack.extend(reversed(c.args))
+        else:
+            out.append(c)
+    return out
+
+
+def conjunct_groups(conj: List[T.Term]) -> List[List[T.Term]]:
+    """The (flattened) conjuncts in balanced groups (one group when the query is short)."""
+    conj = flat_conjuncts(conj)
+    if len(conj) < 2:
+        return [conj]
+    sizes = [_term_nodes(c) for c in conj]
+    total = sum(sizes)
+    g = min(len(conj), MAX_GROUPS, -(-total // SPLIT_NODES))
+    if g < 2:
+        return [conj]
+    groups: List[List[int]] = [[] for _ in range(g)]
+    load = [0] * g
+    for i in sorted(range(len(conj)), key=lambda i: -sizes[i]):
+        k = min(range(g), key=load.__getitem__)
+        groups[k].append(i)
+        load[k] += sizes[i]
+    # each group keeps the conjuncts' query order
+    return [[conj[i] for i in sorted(gr)] for gr in groups if gr]
+
+
+_GROUPS: "OrderedDict[T.Term, object]" = OrderedDict()
+
+
+def explicit_groups(query: T.Term):
+    """(leaf terms, ExplicitGroups or a single program) of a Bool query term: a long
+    conjunction split by ``conjunct_groups``, each group lowered as explicit_program does;
+    raises LoweringError as explicit_program does."""
+    if SPLIT_NODES <= 0 or query.op != "and":
+        return explicit_program(query)
+    with _PROG_LOCK:
+        hit = _GROUPS.get(query)
+        if hit is not None:
+            _GROUPS.move_to_end(query)
+    if hit is None:
+        groups = conjunct_groups(list(query.args) if query.op == "and" else [query])
+        try:
+            if len(groups) == 1:
+                hit = explicit_program(query)
+            else:
+                lowered = [_lower_explicit(gr) for gr in groups]
+                pos: Dict[T.Term, int] = {}
+                gather, offsets = [], []
+                for vt, prog in lowered:
+                    if len(vt) != n_vars(prog):
+                        raise LoweringError("explicit group: variables and leaves differ")
+                    offsets.append(len(gather))
+                    for t in vt:
+                        gather.append(pos.setdefault(t, len(pos)))
+                hit = (list(pos), ExplicitGroups([p for _, p in lowered], np.array(gather, dtype=np.int64),
+                                                 offsets))
+        except (LoweringError, ValueError, OverflowError, RecursionError) as e:
+            hit = f"{type(e).__name__}: {e}"
+        with _PROG_LOCK:
+            _GROUPS[query] = hit
+            while len(_GROUPS) > _PROGRAMS_MAX:
+                _GROUPS.popitem(last=False)
+    if isinstance(hit, str):
+        raise LoweringError(hit)
+    return hit
 
 
 class _EmptyRegistry:
@@ -232,13 +357,27 @@ def rows_of_ints(rows: Sequence[Sequence[int]]) -> List[bytes]:
 
 
 def eval_rows(program, rows: Sequence[bytes], engine=None) -> np.ndarray:
-    """SAT flag of each explicit assignment: one launch (pf_eval_program; an engine without
-    it — the tests' oracle engine — through upload + eval_assignments)."""
+    """SAT flag of each explicit assignment: one launch (pf_eval_program, or pf_eval_programs
+    for conjunct groups; an engine without them — the tests' oracle engine — through upload +
+    eval_assignments per program)."""
     if engine is None:
         from .engine import get_engine
 
         engine = get_engine()
-    soa = soa_of(rows, n_vars(program))
+    if isinstance(program, ExplicitGroups):
+        n_leaves = int(program.gather.max()) + 1 if len(program.gather) else 0
+        soa = soa_of(rows, n_leaves)[program.gather] if n_leaves else soa_of(rows, 0)
+        if hasattr(engine, "eval_programs"):
+            return engine.eval_programs(program.pack(), soa).all(axis=0)
+        ends = program.offsets[1:] + [len(program.gather)]
+        out = np.ones(soa.shape[-1], dtype=bool)
+        for prog, lo, hi in zip(program.programs, program.offsets, ends):
+            out &= _eval_one(prog, np.ascontiguousarray(soa[lo:hi]) if hi > lo else soa_of(rows, 0), engine)
+        return out
+    return _eval_one(program, soa_of(rows, n_vars(program)), engine)
+
+
+def _eval_one(program, soa: np.ndarray, engine) -> np.ndarray:
     if hasattr(engine, "eval_program"):
         return engine.eval_program(program, soa)
     db = engine.upload([program])
@@ -280,7 +419,7 @@ def choose(query: T.Term, leaf_values: Sequence[Optional[LeafValues]],
     if query is T.TRUE:
         leaves, program = [], None
     else:
-        leaves, program = explicit_program(query)
+        leaves, program = explicit_groups(query)
     t = lap("lower", t0)
     stages = [(0, k1), (k1, n)] if 0 < k1 < n else [(0, n)]
     if engine is None and program is not None:

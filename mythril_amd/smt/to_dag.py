@@ -757,6 +757,37 @@ class ExplicitLowering(TermLowering):
             lo += cw
         return out
 
+    def _lower_bv(self, t: T.Term):
+        if t.op == "bvlshr" and t.width <= 256 and t.args[1].op == "bv" and t.args[0].op == "concat":
+            r = self._lshr_concat(t.args[0].args, t.args[1].val, t.width)
+            if r is not None:
+                return r
+        return super()._lower_bv(t)
+
+    def _lshr_concat(self, parts, k: int, wd: int) -> Optional[int]:
+        """``bvlshr(concat(p0 .. pn-1), k)``: the low parts the shift discards whole are not
+        lowered — their bits never reach the result (LASER's selector test shifts a 32-byte
+        calldata word right by 224: 4 of its 32 guarded byte reads matter).  The kept parts
+        ``concat(p0 .. pj)`` shifted by what is left of k, zero-extended back to ``wd``; None
+        when no part is dropped.  Mirrored by pf_terms.cpp (PFLT_EXPLICIT)."""
+        j, drop = len(parts), 0
+        while j > 1 and drop + parts[j - 1].width <= k:
+            drop += parts[j - 1].width
+            j -= 1
+        if j == len(parts):
+            return None
+        d = self.dag
+        hi, hw = self.node(parts[0]), parts[0].width
+        for p in parts[1:j]:
+            hi = d.op(ir.W_CONCAT, hw + p.width, hi, self.node(p), aux=p.width)
+            hw += p.width
+        rem = k - drop
+        if rem >= hw:
+            return d.const(0, wd)
+        if rem:
+            hi = d.op(ir.W_LSHR, hw, hi, d.const(rem, hw))
+        return d.op(ir.W_MOV, wd, hi)
+
     def lower(self, constraints: List[T.Term]) -> Lowered:
         for c in constraints:
             if not c.is_bool:

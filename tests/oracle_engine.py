@@ -58,6 +58,23 @@ class OracleEngine:
             out.append(bool(sv.evaluate(vals)))
         return np.array(out, dtype=bool)
 
+    def eval_programs(self, pack, soa):
+        """Engine.eval_programs: flags [program][cand] of the packed programs, program s
+        reading SoA rows descs[s].var_off .. + n_vars (mythril_amd/model_cache.py groups)."""
+        self.evals = getattr(self, "evals", 0) + 1
+        code, consts, schema, descs = pack
+        b = ir.Batch.__new__(ir.Batch)
+        b.code, b.consts = code.reshape(-1, 4), consts.reshape(-1, 8)
+        b.schema, b.descs = schema.reshape(-1, 4), descs.reshape(-1, 8)
+        b.parents = np.zeros((0, 8), dtype=np.uint32)
+        out = np.zeros((len(b.descs), soa.shape[-1]), dtype=bool)
+        for s in range(len(b.descs)):
+            sv = O.SetView.from_batch(b, s)
+            off, nv = int(b.descs[s][4]), int(b.descs[s][5])
+            for c in range(soa.shape[-1]):
+                out[s, c] = bool(sv.evaluate([O.limbs_to_int(soa[off + v, :, c]) for v in range(nv)]))
+        return out
+
     def keccak256(self, messages):
         return [O.keccak256(bytes(m)) for m in messages]
 

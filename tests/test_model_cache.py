@@ -285,3 +285,90 @@ def test_gpu_eval_program_matches_oracle(engine, monkeypatch):
             db.free()
         n += 1
     assert n == 40
+
+
+def _group_case(corp, rng, q, n_rows=70):
+    """(query term, leaves, groups, rows) of one corpus query split into conjunct groups."""
+    from mythril_amd import corpus as C
+
+    cs = [c for c in q.constraints if c is not T.TRUE]
+    query = T.and_(*cs) if len(cs) > 1 else cs[0]
+    leaves, groups = MC.explicit_groups(query)
+    ev = C._PlantedEval(q.planted, corp.kfm.registry) if q.planted is not None else None
+    rows = []
+    for k in range(n_rows):
+        vals = []
+        for t in leaves:
+            v = int(ev.ev(t)) if k == 0 and ev is not None else rng.choice([0, 1, rng.getrandbits(max(t.width, 1))])
+            vals.append(v & ((1 << max(t.width, 1)) - 1))
+        rows.append(vals)
+    return query, leaves, groups, rows
+
+
+def test_conjunct_groups_equal_the_whole_program(standin, monkeypatch):
+    """A long query split into conjunct groups (explicit_groups, evaluated per group and
+    and-ed) gives the whole-conjunction program's verdict on every explicit assignment —
+    random values and the planted model; and the quick-sat choices stay the reference's."""
+    import random
+
+    import pyoracle as O
+    from mythril_amd import corpus as C
+    from mythril_amd import ir
+
+    eng = oracle_engine.install(monkeypatch)
+    if not native_terms.has_explicit():
+        pytest.skip("libpflower.so not built")
+    monkeypatch.setattr(MC, "SPLIT_NODES", 24)    # split small queries too
+    MC._GROUPS.clear()
+    corp = C.build(n_scenarios=4, txs=2, seed=5)
+    rng = random.Random(3)
+    split = 0
+    for q in corp.queries[:40]:
+        query, leaves, groups, rows = _group_case(corp, rng, q, n_rows=12)
+        if not isinstance(groups, MC.ExplicitGroups):
+            continue
+        split += 1
+        assert len(groups.programs) >= 2 and sorted(set(groups.gather.tolist())) == list(range(len(leaves)))
+        whole_leaves, whole = MC.explicit_program(query)
+        sv = O.SetView.from_batch(ir.Batch([whole]), 0)
+        idx = [leaves.index(t) for t in whole_leaves]
+        want = [bool(sv.evaluate([r[i] for i in idx])) for r in rows]
+        got = MC.eval_rows(groups, MC.rows_of_ints(rows), eng)
+        assert list(got) == want, q.origin
+    assert split >= 10
+    models, queries, _, _ = W.build(z3, standin, n_models=30, n_scenarios=4, n_queries=20)
+    _check_stream(standin, models, queries)
+    MC._GROUPS.clear()
+
+
+@pytest.mark.gpu
+def test_gpu_eval_programs_match_per_group_programs(engine, monkeypatch):
+    """pf_eval_programs (every group of a query in one launch) gives each group's
+    pf_eval_program verdicts, and their conjunction the whole program's."""
+    import random
+
+    from mythril_amd import corpus as C
+
+    monkeypatch.setattr(MC, "SPLIT_NODES", 24)
+    MC._GROUPS.clear()
+    corp = C.build(n_scenarios=4, txs=2, seed=5)
+    rng = random.Random(4)
+    split = 0
+    for q in corp.queries[:40]:
+        query, leaves, groups, rows = _group_case(corp, rng, q)
+        if not isinstance(groups, MC.ExplicitGroups):
+            continue
+        split += 1
+        soa = MC.soa_of(MC.rows_of_ints(rows), len(leaves))[groups.gather]
+        got = engine.eval_programs(groups.pack(), soa)
+        ends = groups.offsets[1:] + [len(groups.gather)]
+        for s, (prog, lo, hi) in enumerate(zip(groups.programs, groups.offsets, ends)):
+            part = np.ascontiguousarray(soa[lo:hi]) if hi > lo else MC.soa_of(MC.rows_of_ints(rows), 0)
+            assert list(got[s]) == list(engine.eval_program(prog, part)), (q.origin, s)
+        whole_leaves, whole = MC.explicit_program(query)
+        idx = [leaves.index(t) for t in whole_leaves]
+        want = engine.eval_program(whole, MC.soa_of(MC.rows_of_ints([[r[i] for i in idx] for r in rows]),
+                                                    MC.n_vars(whole)))
+        assert list(got.all(axis=0)) == list(want), q.origin
+    assert split >= 10
+    MC._GROUPS.clear()
