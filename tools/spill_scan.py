@@ -41,7 +41,8 @@ def main():
         max_slot.append(ms)
     ms = np.array(max_slot)
     print(json.dumps({"dags": args.dags, "sets_spilling": float((ms >= 0).mean()),
-                      "sets_by_highest_slot": {str(k): int(v) for k, v in enumerate(np.bincount(ms + 1)) if v},
+                      "sets_by_highest_slot": {("none" if k == 0 else str(k - 1)): int(v)
+                                              for k, v in enumerate(np.bincount(ms + 1)) if v},
                       "fills": fills, "fills_per_set": fills / args.dags,
                       "ranges_crossing_exp_table_users": crossing,
                       "crossing_frac": crossing / max(fills, 1)}))
