@@ -131,6 +131,13 @@ enum pf_opcode {
 #define PF_I_KA (1u << 25)
 #define PF_I_KB (1u << 26)
 
+/* aux of a W/B SPILL or FILL: PF_SPILL_LDS | e keeps the value in LDS entry e (1..3) of the
+ * lane's EXP window table instead of private scratch slot aux.  Set only by pf_batch_create's
+ * spill peephole, for a spill whose fills all come before the next W_EXP (which rewrites
+ * entries 1..3) and, for entry 1, the next B_UMUL_NOOVF (which parks an operand there):
+ * scratch traffic is dirty L2 lines of every resident wave. */
+#define PF_SPILL_LDS 0x100u
+
 /* operand traffic bits (w0 >> 18): reads W[a], reads W[b], writes W[d] */
 #define PF_TR_RA 1u
 #define PF_TR_RB 2u

@@ -551,6 +551,55 @@ void device_program(const std::vector<uint32_t>& code_fixed, std::vector<pf_set_
             for (uint32_t r = 0; r <= PF_NW; r++) settle(r);
         }
 #endif
+#ifndef PF_NO_LDS_SPILL
+        // ---- 4. spill slots -> LDS entries 1..3 of EXP's window table (PF_SPILL_LDS)
+        // A segment is a SPILL of slot k and the FILLs of k before its next SPILL.  One whose
+        // range holds no W_EXP takes entry 2 or 3 when free (entry 1 too if no B_UMUL_NOOVF
+        // runs in it): the value never touches scratch.  Entries are handed out in program
+        // order; a segment without a FILL stays (a dead store costs nothing more).
+        {
+            struct Seg {
+                uint32_t spill, last;
+                std::vector<uint32_t> fills;
+            };
+            std::vector<Seg> segs;
+            int64_t open[PF_MAX_SPILL];
+            for (int k = 0; k < PF_MAX_SPILL; k++) open[k] = -1;
+            std::vector<uint32_t> exp_at, umul_at;
+            for (uint32_t i = 0; i < n; i++) {
+                if (drop[i]) continue;
+                const uint32_t op = P[4 * i] & 0xffu, k = P[4 * i + 2] & (PF_MAX_SPILL - 1u);
+                if (op == PF_END) break;
+                if (op == PF_W_EXP) exp_at.push_back(i);
+                if (op == PF_B_UMUL_NOOVF) umul_at.push_back(i);
+                if (op == PF_W_SPILL || op == PF_B_SPILL) {
+                    open[k] = (int64_t)segs.size();
+                    segs.push_back(Seg{i, i, {}});
+                } else if ((op == PF_W_FILL || op == PF_B_FILL) && open[k] >= 0) {
+                    Seg& g = segs[(size_t)open[k]];
+                    g.fills.push_back(i);
+                    g.last = i;
+                }
+            }
+            auto any_in = [](const std::vector<uint32_t>& at, uint32_t lo, uint32_t hi) {
+                const auto it = std::upper_bound(at.begin(), at.end(), lo);
+                return it != at.end() && *it < hi;
+            };
+            int64_t busy_until[4] = {-1, -1, -1, -1};
+            static const uint32_t order[3] = {2u, 3u, 1u};
+            for (const Seg& g : segs) {
+                if (g.fills.empty() || any_in(exp_at, g.spill, g.last)) continue;
+                const bool umul = any_in(umul_at, g.spill, g.last);
+                for (uint32_t e : order) {
+                    if ((e == 1u && umul) || busy_until[e] >= (int64_t)g.spill) continue;
+                    busy_until[e] = g.last;
+                    P[4 * (size_t)g.spill + 2] = PF_SPILL_LDS | e;
+                    for (uint32_t f : g.fills) P[4 * (size_t)f + 2] = PF_SPILL_LDS | e;
+                    break;
+                }
+            }
+        }
+#endif
         const size_t first = code_out.size() / 4;
         for (uint32_t i = 0; i < n; i++)
             if (!drop[i]) code_out.insert(code_out.end(), P.begin() + 4 * (size_t)i, P.begin() + 4 * (size_t)i + 4);

@@ -829,10 +829,19 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
                     case PF_B_NOT: BSET(d, BGET(a) ^ 1u); break;
                     case PF_B_ITE: BSET(d, BGET(c) ? BGET(a) : BGET(b)); break;
                     case PF_B_FILL:
-                        BSET(d, spill[PF_SLOT(aux) * 8u]);
+                        if (aux & PF_SPILL_LDS) {  // uniform: pf_batch_create's LDS slots
+                            BSET(d, exp_tbl[(aux & 3u) * 4u * 64u].x);
+                        } else {
+                            BSET(d, spill[PF_SLOT(aux) * 8u]);
+                        }
                         PF_WAIT_ALL();
                         break;
-                    case PF_B_SPILL: spill[PF_SLOT(aux) * 8u] = BGET(a); break;
+                    case PF_B_SPILL:
+                        if (aux & PF_SPILL_LDS)
+                            exp_tbl[(aux & 3u) * 4u * 64u] = make_uint2(BGET(a), 0u);
+                        else
+                            spill[PF_SLOT(aux) * 8u] = BGET(a);
+                        break;
                     default:  // PF_ASSERT
                         PF_DO_ASSERT(BGET(a));
                         PF_NEXT();
@@ -864,14 +873,22 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
                     }
                     case PF_W_MOV: z = x; break;
                     case PF_W_SPILL:
+                        if (aux & PF_SPILL_LDS) {  // uniform: pf_batch_create's LDS slots
+                            pf::tbl_put(exp_tbl, 64u, aux & 3u, x);
+                        } else {
 #pragma unroll
-                        for (int i = 0; i < 8; i++) spill[PF_SLOT(aux) * 8u + i] = x.l[i];
+                            for (int i = 0; i < 8; i++) spill[PF_SLOT(aux) * 8u + i] = x.l[i];
+                        }
                         if (NREG == 8) PF_NEXT();  // no W result (the wide kernels write the sink)
                         z = x;
                         break;
                     case PF_W_FILL:
+                        if (aux & PF_SPILL_LDS) {
+                            z = pf::tbl_get(exp_tbl, 64u, aux & 3u);
+                        } else {
 #pragma unroll
-                        for (int i = 0; i < 8; i++) z.l[i] = spill[PF_SLOT(aux) * 8u + i];
+                            for (int i = 0; i < 8; i++) z.l[i] = spill[PF_SLOT(aux) * 8u + i];
+                        }
                         PF_WAIT_ALL();
                         break;
                     case PF_W_NOT: z = pf::not256(x); break;
