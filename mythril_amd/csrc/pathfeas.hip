@@ -979,9 +979,13 @@ int pf_batch_create_on(int device, const uint32_t* code, size_t n_ins, const uin
         }
     }
     if (!ok) {
+        // the copy may still be in flight: drain the device and free the block rather than
+        // pool it (the next pool_acquire would hand out memory still being written)
         t_defer_err = true;
         const int rc = fail("pf_batch_create: hipMemcpy of %zu bytes failed", o_found);
-        release_batch(use_dev(B->device), B);
+        if (hipDeviceSynchronize() == hipSuccess) hipFree(B->d_mem);
+        B->d_mem = nullptr;
+        delete B;
         return report(rc);
     }
     *handle_out = (uint64_t)(uintptr_t)B;
