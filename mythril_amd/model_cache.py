@@ -389,18 +389,39 @@ def _eval_one(program, soa: np.ndarray, engine) -> np.ndarray:
 
 # Models evaluated in the first launch: the reference loop stops at the first model that
 # holds, and in a live analysis that is most often one of the newest (the parent state's
-# model, bumped to the front by the query before) — computing every model's leaves for such a
-# query would cost more than the loop it replaces.  The others go in a second launch.
+# model, bumped to the front by the query before) — computing every z3 model's leaves for
+# such a query would cost more than the loop it replaces.  The first launch therefore covers
+# the newest models up to (not including) the (FIRST_STAGE + 1)-th whose leaves are dear —
+# a z3 model, evaluated per leaf through its own eval; a natively held GPU witness costs a
+# copy per leaf — and the rest go in a second launch only if none of those holds (0: one
+# launch for all).  Measured (profiles/r05x_quick_sat_stages.md): a cache of GPU witnesses
+# in one launch 0.98 -> 0.86 ms mean per query; z3-heavy caches keep the two stages.
 # (Deciding only the newest model on the host first measured slower: it held for 24 of 121
 # profile queries, profiles/r05g_quick_sat_hostfirst.jsonl.)
-FIRST_STAGE = 4
+FIRST_STAGE = int(os.environ.get("PF_QS_FIRST_STAGE", "4"))
+
+
+def first_stage_end(leaf_values: Sequence[Optional[LeafValues]], k: int) -> int:
+    """End of the first launch's models: the longest prefix holding at most k models whose
+    leaves are dear (everything but NativeLeafValues; an unvaluable model counts as dear —
+    the reference statement decides it in its place)."""
+    if k <= 0:
+        return len(leaf_values)
+    dear = 0
+    for i, lv in enumerate(leaf_values):
+        if not isinstance(lv, NativeLeafValues):
+            dear += 1
+            if dear > k:
+                return i
+    return len(leaf_values)
 
 
 def choose(query: T.Term, leaf_values: Sequence[Optional[LeafValues]],
            reference: Callable[[int], bool], engine=None, first_stage: Optional[int] = None) -> Optional[int]:
     """Index (in the given most-recent-first order) of the first model under which ``query``
-    is true, or None.  The models are evaluated in at most two launches: the newest
-    ``first_stage`` (FIRST_STAGE), then, if none of them holds, all the others.  A model whose
+    is true, or None.  The models are evaluated in at most two launches: the newest up to the
+    (``first_stage`` + 1)-th with dear leaves (FIRST_STAGE, ``first_stage_end``), then, if none
+    of them holds, all the others.  A model whose
     ``leaf_values[i]`` is None, or that has a leaf its evaluator rejects, is decided by
     ``reference(i)`` — the reference statement — in its place in the order.  Raises
     LoweringError when the query cannot be lowered (the caller runs the reference loop)."""
@@ -421,7 +442,8 @@ def choose(query: T.Term, leaf_values: Sequence[Optional[LeafValues]],
     else:
         leaves, program = explicit_groups(query)
     t = lap("lower", t0)
-    stages = [(0, k1), (k1, n)] if 0 < k1 < n else [(0, n)]
+    e1 = first_stage_end(leaf_values, k1)
+    stages = [(0, e1), (e1, n)] if 0 < e1 < n else [(0, n)]
     if engine is None and program is not None:
         from .engine import get_engine
 

@@ -181,6 +181,18 @@ def test_native_witness_leaves_equal_python_witness(standin, monkeypatch):
         assert native_terms.ints_of(r)[0] == wms[j].w.leaf_value(app) == 0xABCDEF
 
 
+def test_first_stage_counts_only_dear_models():
+    """The first launch takes the newest models up to the (k + 1)-th whose leaves are dear
+    (z3 models, unvaluable ones); natively held witnesses ride along."""
+    nat = MC.NativeLeafValues.__new__(MC.NativeLeafValues)
+    z = MC.LeafValues(lambda t: 0)
+    assert MC.first_stage_end([nat] * 10, 4) == 10
+    assert MC.first_stage_end([z] * 10, 4) == 4
+    assert MC.first_stage_end([nat, z, nat, None, z, z, nat, z, nat], 4) == 7
+    assert MC.first_stage_end([z] * 10, 0) == 10
+    assert MC.first_stage_end([], 4) == 0
+
+
 def test_explicit_lowering_native_equals_python(standin, monkeypatch):
     oracle_engine.install(monkeypatch)
     if not native_terms.has_explicit():
