@@ -127,6 +127,9 @@ class TermStore:
         self.h = lib.pflt_store_new()
         self.ids: Dict[T.Term, int] = {}
         self.terms: List[T.Term] = []
+        # (array id, index id) -> select term: var_terms' base-array reads, built once per
+        # store (the quick-sat leaves of successive queries repeat most of them)
+        self.selects: Dict[Tuple[int, int], T.Term] = {}
         # guards Store::t and the recent tables: pflt_add (export) may reallocate the term
         # vector that a concurrent recheck / recent-parent / lowering reads through pointers
         # (ctypes drops the GIL), so every call into the store holds it
@@ -359,10 +362,18 @@ class _Result:
             if typ == VT_TERM:
                 out.append(terms[a])
             elif typ == VT_SELECT:
-                out.append(T.select(terms[a], terms[b]))
+                out.append(self._select(a, b))
             else:
                 out.append(T.extract(c, b, terms[a]))
         return out
+
+    def _select(self, a: int, b: int) -> T.Term:
+        sel = self.st.selects
+        t = sel.get((a, b))
+        if t is None:
+            terms = self.st.terms
+            t = sel[(a, b)] = T.select(terms[a], terms[b])
+        return t
 
     def lowered(self) -> Lowered:
         terms = self.st.terms
@@ -372,7 +383,7 @@ class _Result:
             if typ == VT_TERM:
                 var_terms.append(terms[a])
             elif typ == VT_SELECT:
-                var_terms.append(T.select(terms[a], terms[b]))
+                var_terms.append(self._select(a, b))
             else:
                 var_terms.append(T.extract(c, b, terms[a]))
         uf_apps = []
@@ -386,8 +397,8 @@ class _Result:
         k = 0
         for cnt in counts:
             for _ in range(cnt):
-                arr, idx = terms[pairs[2 * k]], terms[pairs[2 * k + 1]]
-                reads.setdefault(arr.val, []).append((idx, T.select(arr, idx)))
+                a, b = pairs[2 * k], pairs[2 * k + 1]
+                reads.setdefault(terms[a].val, []).append((terms[b], self._select(a, b)))
                 k += 1
         return Lowered(None, var_terms, uf_apps, reads)
 
