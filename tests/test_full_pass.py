@@ -30,3 +30,38 @@ def test_full_pass_chunks_match_per_dag_search(monkeypatch):
     # the planted pass: every DAG's witness is candidate 0
     assert res["planted_early_exit"]["sets_with_witness"] == 40
     assert res["full_sweep"]["evals_per_s_wall"] > 0
+
+
+def test_full_pass_reports_a_device_error_without_hanging():
+    """An engine that fails mid-pass: the error comes back from run_full_pass (the uploader
+    and device threads drain and stop) instead of a hang on the bounded queues."""
+    import pytest
+
+    class Failing(oracle_engine.OracleEngine):
+        def check(self, db, budget=65536, seed=0, flags=0, timeout_ms=0):
+            if self.launches >= 3:
+                raise RuntimeError("device lost")
+            return super().check(db, budget, seed, flags, timeout_ms)
+
+    with pytest.raises(RuntimeError, match="device lost"):
+        full_pass.run_full_pass(Failing(), dags=60, chunk=8, piece=4, workers=2, budget=64, seed=0,
+                                mp_context="spawn")
+
+
+def test_full_pass_reports_an_upload_error_without_hanging():
+    import pytest
+
+    class Failing(oracle_engine.OracleEngine):
+        def __init__(self):
+            super().__init__()
+            self.uploads = 0
+
+        def upload(self, programs):
+            self.uploads += 1
+            if self.uploads >= 4:
+                raise ValueError("bad batch")
+            return super().upload(programs)
+
+    with pytest.raises(ValueError, match="bad batch"):
+        full_pass.run_full_pass(Failing(), dags=60, chunk=8, piece=4, workers=2, budget=64, seed=0,
+                                mp_context="spawn")
