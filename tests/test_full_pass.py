@@ -19,7 +19,7 @@ def test_full_pass_chunks_match_per_dag_search(monkeypatch):
     res = full_pass.run_full_pass(eng, dags=40, chunk=16, piece=6, workers=2, budget=256, seed=0,
                                   mp_context="spawn")
     fs = res["full_sweep"]
-    # chunks ramp up from chunk / 8 (at least one piece): 6 + 12 + 18 + 4 DAGs
+    # chunks ramp up from chunk / 32 (at least one piece): 6 + 12 + 18 + 4 DAGs
     assert fs["evals_full"] == 40 * 256 and fs["chunks"] == 4
     want = 0
     for i in range(40):

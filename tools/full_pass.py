@@ -163,9 +163,9 @@ def run_full_pass(eng, dags: int = 1_000_000, chunk: int = 65536, piece: int = 2
         tasks = [(first + f, min(piece, dags - f)) for f in range(0, dags, piece)]
         futs = [pool.submit(_build, t) for t in tasks]
         pending, n_pending = [], 0
-        # the first chunks ramp up (chunk / 8, / 4, / 2, then chunk): the device starts after
-        # a few pieces are built instead of a whole chunk's worth
-        target = max(piece, chunk // 8)
+        # the first chunks ramp up (chunk / 32, / 16, ... then chunk): the device starts after
+        # one piece is built instead of a whole chunk's worth
+        target = max(piece, chunk // 32)
         for i, fu in enumerate(futs):
             tw = time.perf_counter()
             pending.append(fu.result())
