@@ -889,9 +889,9 @@ extern "C" void pflt_witness_values(void* const* witnesses, size_t n_models, con
                 return;
             }
         }
-        if (slots && W->slot_epoch != slot_epoch) {
-            W->slot_vals.clear();
-            W->slot_state.clear();
+        if (slots && W->slot_epoch != slot_epoch) {  // renumbered: drop the old slots' memory
+            std::vector<uint32_t>().swap(W->slot_vals);
+            std::vector<uint8_t>().swap(W->slot_state);
             W->slot_epoch = slot_epoch;
         }
         for (size_t i = 0; i < n_terms; i++) {

@@ -868,10 +868,11 @@ class NativeWitness:
 
 
 # leaf slots: a dense number per term read through witness_values_many, under which each
-# native witness keeps the value; renumbered (new epoch) when the table grows past _SLOTS_MAX
+# native witness keeps the value (33 bytes per slot per witness: at most ~0.5 MB each, ~50 MB
+# for a full 100-model cache); renumbered (new epoch) when the table grows past _SLOTS_MAX
 _SLOTS: Dict[T.Term, int] = {}
 _SLOT_EPOCH = [1]
-_SLOTS_MAX = 1 << 16
+_SLOTS_MAX = 1 << 14
 
 
 def _slots_of(terms: List[T.Term]) -> Tuple[np.ndarray, int]:
