@@ -208,23 +208,57 @@ def conjunct_groups(conj: List[T.Term]) -> List[List[T.Term]]:
 _GROUPS: "OrderedDict[T.Term, object]" = OrderedDict()
 
 
+# PF_QS_CONJ=1: every (flattened) conjunct of a query is its own program, lowered once and
+# cached by conjunct across queries — LASER's queries along a path share all but their newest
+# conjuncts, so a query lowers only those — and all of a query's conjunct programs run in one
+# launch (pf_eval_programs).
+CONJ_PROGRAMS = os.environ.get("PF_QS_CONJ", "0") != "0"
+_CONJ: "OrderedDict[T.Term, object]" = OrderedDict()
+_CONJ_MAX = 8192
+
+
+def _conj_program(c: T.Term):
+    with _PROG_LOCK:
+        hit = _CONJ.get(c)
+        if hit is not None:
+            _CONJ.move_to_end(c)
+    if hit is None:
+        try:
+            hit = _lower_explicit([c])
+        except (LoweringError, ValueError, OverflowError, RecursionError) as e:
+            hit = f"{type(e).__name__}: {e}"
+        with _PROG_LOCK:
+            _CONJ[c] = hit
+            while len(_CONJ) > _CONJ_MAX:
+                _CONJ.popitem(last=False)
+    if isinstance(hit, str):
+        raise LoweringError(hit)
+    return hit
+
+
 def explicit_groups(query: T.Term):
     """(leaf terms, ExplicitGroups or a single program) of a Bool query term: a long
-    conjunction split by ``conjunct_groups``, each group lowered as explicit_program does;
-    raises LoweringError as explicit_program does."""
-    if SPLIT_NODES <= 0 or query.op != "and":
+    conjunction split by ``conjunct_groups`` (or, with CONJ_PROGRAMS, one cached program per
+    conjunct), each group lowered as explicit_program does; raises LoweringError as
+    explicit_program does."""
+    if (SPLIT_NODES <= 0 and not CONJ_PROGRAMS) or query.op != "and":
         return explicit_program(query)
     with _PROG_LOCK:
         hit = _GROUPS.get(query)
         if hit is not None:
             _GROUPS.move_to_end(query)
     if hit is None:
-        groups = conjunct_groups(list(query.args) if query.op == "and" else [query])
+        if CONJ_PROGRAMS:
+            conj = [c for c in dict.fromkeys(flat_conjuncts(list(query.args))) if c is not T.TRUE]
+            groups = [[c] for c in conj] or [[T.TRUE]]
+        else:
+            groups = conjunct_groups(list(query.args))
         try:
-            if len(groups) == 1:
+            if len(groups) == 1 and not CONJ_PROGRAMS:
                 hit = explicit_program(query)
             else:
-                lowered = [_lower_explicit(gr) for gr in groups]
+                lowered = [_conj_program(gr[0]) for gr in groups] if CONJ_PROGRAMS else \
+                    [_lower_explicit(gr) for gr in groups]
                 pos: Dict[T.Term, int] = {}
                 gather, offsets = [], []
                 for vt, prog in lowered:

@@ -361,6 +361,27 @@ def test_conjunct_groups_equal_the_whole_program(standin, monkeypatch):
     MC._GROUPS.clear()
 
 
+def test_conjunct_programs_cached_across_queries(standin, monkeypatch):
+    """CONJ_PROGRAMS: one cached program per flattened conjunct, every query's conjuncts in
+    one pf_eval_programs call — the same choices as the reference loop, and a conjunct shared
+    by later queries is lowered once."""
+    oracle_engine.install(monkeypatch)
+    if not native_terms.has_explicit():
+        pytest.skip("libpflower.so not built")
+    monkeypatch.setattr(MC, "CONJ_PROGRAMS", True)
+    MC._GROUPS.clear()
+    MC._CONJ.clear()
+    lowered = []
+    real = MC._lower_explicit
+    monkeypatch.setattr(MC, "_lower_explicit", lambda conj: (lowered.append(conj[0]), real(conj))[1])
+    models, queries, _, _ = W.build(z3, standin, n_models=30, n_scenarios=4, n_queries=30)
+    _check_stream(standin, models, queries)
+    assert len(lowered) == len(set(lowered))          # every conjunct lowered once
+    assert len(MC._CONJ) == len(lowered)
+    MC._GROUPS.clear()
+    MC._CONJ.clear()
+
+
 @pytest.mark.gpu
 def test_gpu_eval_programs_match_per_group_programs(engine, monkeypatch):
     """pf_eval_programs (every group of a query in one launch) gives each group's
