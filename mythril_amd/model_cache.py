@@ -208,11 +208,14 @@ def conjunct_groups(conj: List[T.Term]) -> List[List[T.Term]]:
 _GROUPS: "OrderedDict[T.Term, object]" = OrderedDict()
 
 
-# PF_QS_CONJ=1: every (flattened) conjunct of a query is its own program, lowered once and
-# cached by conjunct across queries — LASER's queries along a path share all but their newest
+# Every (flattened) conjunct of a query is its own program, lowered once and cached by
+# conjunct across queries — LASER's queries along a path share all but their newest
 # conjuncts, so a query lowers only those — and all of a query's conjunct programs run in one
-# launch (pf_eval_programs).
-CONJ_PROGRAMS = os.environ.get("PF_QS_CONJ", "0") != "0"
+# launch (pf_eval_programs), side by side: the launch lasts as long as the longest conjunct,
+# not the whole conjunction.  Measured (profiles/r05z_quick_sat_conj.md): witness cache 0.93
+# -> 0.67 ms mean per query (lowering 0.26 -> 0.13, launch 0.43 -> 0.34).  PF_QS_CONJ=0 lowers
+# each query whole.
+CONJ_PROGRAMS = os.environ.get("PF_QS_CONJ", "1") != "0"
 _CONJ: "OrderedDict[T.Term, object]" = OrderedDict()
 _CONJ_MAX = 8192
 
