@@ -402,10 +402,15 @@ def eval_rows(program, rows: Sequence[bytes], engine=None) -> np.ndarray:
 
         engine = get_engine()
     if isinstance(program, ExplicitGroups):
+        t0 = time.perf_counter()
         n_leaves = int(program.gather.max()) + 1 if len(program.gather) else 0
         soa = soa_of(rows, n_leaves)[program.gather] if n_leaves else soa_of(rows, 0)
         if hasattr(engine, "eval_programs"):
-            return engine.eval_programs(program.pack(), soa).all(axis=0)
+            pack = program.pack()
+            dt = time.perf_counter() - t0
+            with _STATS_LOCK:   # the host share of the "eval" phase: SoA gather + packing
+                STATS.phase_s["eval_host"] = STATS.phase_s.get("eval_host", 0.0) + dt
+            return engine.eval_programs(pack, soa).all(axis=0)
         ends = program.offsets[1:] + [len(program.gather)]
         out = np.ones(soa.shape[-1], dtype=bool)
         for prog, lo, hi in zip(program.programs, program.offsets, ends):
