@@ -367,12 +367,26 @@ def native_rows(leaf_values: Sequence[Optional[LeafValues]], leaves: Sequence[T.
         vals, ok = native_terms.witness_values_many([lv.native for lv in lvs], list(leaves), lvs[0].reg,
                                                     min(LEAF_THREADS, len(lvs)))
         full = ok.all(axis=1)
-        for j, m in zip(js, range(len(js))):
-            if full[m]:
-                out[j] = vals[m]
+        if len(groups) == 1 and len(js) == len(leaf_values) and full.all():
+            # every model native and complete (a cache of GPU witnesses): the block itself,
+            # models in order — eval_rows takes it as the SoA source without restacking
+            out = _NativeBlock(vals)
+        else:
+            for j, m in zip(js, range(len(js))):
+                if full[m]:
+                    out[j] = vals[m]
         with _STATS_LOCK:
             STATS.leaf_evals_native += int(full.sum()) * len(leaves)
     return out
+
+
+class _NativeBlock(dict):
+    """native_rows' answer when every model of the stage is native and complete: the rows
+    as one (models, leaves, 8) array (``block``), still indexable per model."""
+
+    def __init__(self, block: np.ndarray):
+        super().__init__((j, block[j]) for j in range(len(block)))
+        self.block = block
 
 
 def soa_of(rows: Sequence, n_vars: int) -> np.ndarray:
@@ -381,6 +395,8 @@ def soa_of(rows: Sequence, n_vars: int) -> np.ndarray:
     n = len(rows)
     if n_vars == 0:
         return np.zeros((1, 8, n), dtype=np.uint32)
+    if isinstance(rows, np.ndarray):   # a (models, vars, 8) block (native_rows)
+        return np.ascontiguousarray(rows.transpose(1, 2, 0), dtype=np.uint32)
     if all(isinstance(r, bytes) for r in rows):
         a = np.frombuffer(b"".join(rows), dtype="<u4").reshape(n, n_vars, 8)
     else:
@@ -404,7 +420,12 @@ def eval_rows(program, rows: Sequence[bytes], engine=None) -> np.ndarray:
     if isinstance(program, ExplicitGroups):
         t0 = time.perf_counter()
         n_leaves = int(program.gather.max()) + 1 if len(program.gather) else 0
-        soa = soa_of(rows, n_leaves)[program.gather] if n_leaves else soa_of(rows, 0)
+        if not n_leaves:
+            soa = soa_of(rows, 0)
+        elif isinstance(rows, np.ndarray):   # (models, leaves, 8): gather, then one transpose copy
+            soa = np.ascontiguousarray(rows[:, program.gather].transpose(1, 2, 0), dtype=np.uint32)
+        else:
+            soa = soa_of(rows, n_leaves)[program.gather]
         if hasattr(engine, "eval_programs"):
             pack = program.pack()
             dt = time.perf_counter() - t0
@@ -513,16 +534,21 @@ def _stages(stages, leaves, program, leaf_values, reference, engine, lap, t):
     host = launches = on_engine_n = 0
     for lo, hi in stages:
         nat = native_rows(leaf_values[lo:hi], leaves)
-        rows = [nat[i - lo] if i - lo in nat else leaf_values[i].row(leaves) if leaf_values[i] is not None
-                else None for i in range(lo, hi)]
+        block = getattr(nat, "block", None)
+        if block is not None:
+            rows, on_engine = None, list(range(lo, hi))
+        else:
+            rows = [nat[i - lo] if i - lo in nat else leaf_values[i].row(leaves) if leaf_values[i] is not None
+                    else None for i in range(lo, hi)]
+            on_engine = [i for i in range(lo, hi) if rows[i - lo] is not None]
         t = lap("leaves", t)
-        on_engine = [i for i in range(lo, hi) if rows[i - lo] is not None]
         flags: Dict[int, bool] = {}
         if on_engine:
             if program is None:          # literal True: every model satisfies it
                 flags = {i: True for i in on_engine}
             else:
-                sat = eval_rows(program, [rows[i - lo] for i in on_engine], engine)
+                sat = eval_rows(program, block if block is not None else [rows[i - lo] for i in on_engine],
+                                engine)
                 flags = dict(zip(on_engine, (bool(x) for x in sat)))
                 launches += 1
                 on_engine_n += len(on_engine)

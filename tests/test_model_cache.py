@@ -75,6 +75,20 @@ def test_quick_sat_choice_matches_reference_loop(standin, monkeypatch, first_sta
     assert len({p for p in picks if p is not None}) >= 1
 
 
+def test_quick_sat_witness_only_cache(standin, monkeypatch):
+    """A cache of GPU witnesses only — the live case: every model's leaves native, one
+    launch from the (models, leaves, 8) block — same choices as the reference loop."""
+    oracle_engine.install(monkeypatch)
+    models, queries, _, _ = W.build(z3, standin, n_models=40, n_scenarios=4, n_queries=20, gpu_frac=1.0,
+                                    empty_frac=0.0)
+    models = [m for m in models if m.raw and isinstance(m.raw[0], integration.Z3WitnessView)]
+    assert len(models) >= 10
+    MC.STATS.__init__()
+    picks = _run_both(standin, models, queries)
+    assert picks[-1] is None and any(p is not None for p in picks)
+    assert MC.STATS.models_host == 0 and MC.STATS.leaf_evals == 0 and MC.STATS.leaf_evals_native > 0
+
+
 def test_quick_sat_small_caches_and_empty(standin, monkeypatch):
     oracle_engine.install(monkeypatch)
     monkeypatch.setattr(MC, "FIRST_STAGE", 0)
