@@ -422,8 +422,8 @@ def eval_rows(program, rows: Sequence[bytes], engine=None) -> np.ndarray:
         n_leaves = int(program.gather.max()) + 1 if len(program.gather) else 0
         if not n_leaves:
             soa = soa_of(rows, 0)
-        elif isinstance(rows, np.ndarray):   # (models, leaves, 8): gather, then one transpose copy
-            soa = np.ascontiguousarray(rows[:, program.gather].transpose(1, 2, 0), dtype=np.uint32)
+        elif isinstance(rows, np.ndarray):   # (models, leaves, 8): transpose once, gather rows
+            soa = soa_of(rows, n_leaves)[program.gather]
         else:
             soa = soa_of(rows, n_leaves)[program.gather]
         if hasattr(engine, "eval_programs"):
