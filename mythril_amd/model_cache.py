@@ -40,6 +40,7 @@ import os
 import threading
 import time
 from collections import OrderedDict
+from collections.abc import Mapping
 from copy import deepcopy
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
@@ -349,7 +350,7 @@ class NativeLeafValues(LeafValues):
 LEAF_THREADS = max(1, min(8, os.cpu_count() or 1))
 
 
-def native_rows(leaf_values: Sequence[Optional[LeafValues]], leaves: Sequence[T.Term]) -> Dict[int, np.ndarray]:
+def native_rows(leaf_values: Sequence[Optional[LeafValues]], leaves: Sequence[T.Term]) -> Mapping:
     """{position in ``leaf_values``: its row as (len(leaves), 8) u32 limbs} for the natively
     held models whose every leaf evaluated natively — one pflt_witness_values call per term
     store (and registry)."""
@@ -357,7 +358,7 @@ def native_rows(leaf_values: Sequence[Optional[LeafValues]], leaves: Sequence[T.
     for j, lv in enumerate(leaf_values):
         if isinstance(lv, NativeLeafValues):
             groups.setdefault((id(lv.native.st), id(lv.reg)), []).append(j)
-    out: Dict[int, np.ndarray] = {}
+    out: Mapping = {}
     if not groups or not leaves:
         return out
     from .smt import native_terms
@@ -380,13 +381,26 @@ def native_rows(leaf_values: Sequence[Optional[LeafValues]], leaves: Sequence[T.
     return out
 
 
-class _NativeBlock(dict):
+class _NativeBlock(Mapping):
     """native_rows' answer when every model of the stage is native and complete: the rows
-    as one (models, leaves, 8) array (``block``), still indexable per model."""
+    as one (models, leaves, 8) array (``block``), readable per model like the dict
+    native_rows returns otherwise (no per-model views made unless asked for)."""
+
+    __slots__ = ("block",)
 
     def __init__(self, block: np.ndarray):
-        super().__init__((j, block[j]) for j in range(len(block)))
         self.block = block
+
+    def __getitem__(self, j: int) -> np.ndarray:
+        if not 0 <= j < len(self.block):
+            raise KeyError(j)
+        return self.block[j]
+
+    def __iter__(self):
+        return iter(range(len(self.block)))
+
+    def __len__(self) -> int:
+        return len(self.block)
 
 
 def soa_of(rows: Sequence, n_vars: int) -> np.ndarray:

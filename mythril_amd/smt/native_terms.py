@@ -894,7 +894,7 @@ def witness_values_many(ws: List[NativeWitness], terms: List[T.Term], reg: UFReg
     """(values [model][term][8] u32 limbs, each masked to its term's width; ok [model][term]
     bool) of ``terms`` under every witness of ``ws`` (one store), natively in one call."""
     n, k = len(ws), len(terms)
-    out = np.zeros((n, k, 8), dtype=np.uint32)
+    out = np.empty((n, k, 8), dtype=np.uint32)   # every (model, term) the call marks ok is written
     ok = np.zeros((n, k), dtype=np.uint8)
     if n == 0 or k == 0:
         return out, ok.astype(bool)
