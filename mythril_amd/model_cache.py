@@ -218,7 +218,7 @@ _GROUPS: "OrderedDict[T.Term, object]" = OrderedDict()
 # each query whole.
 CONJ_PROGRAMS = os.environ.get("PF_QS_CONJ", "1") != "0"
 _CONJ: "OrderedDict[T.Term, object]" = OrderedDict()
-_CONJ_MAX = 8192
+_CONJ_MAX = 4096   # lowering results of a few KB each
 
 
 def _conj_program(c: T.Term):
