@@ -211,3 +211,27 @@ def test_out_of_width_constant_is_not_folded(monkeypatch):
         if tried >= 12:
             break
     assert tried > 0 and kept > 0, (tried, kept)
+
+
+def test_spill_heavy_device_programs_keep_their_values():
+    """Three W registers: the LDS spill peephole under heavy pressure (entries reused, spills
+    across EXPs left in scratch) — the device form, with EXP / UMUL_NOOVF clobbering the LDS
+    entries, still computes the lowered program's verdict."""
+    import sys
+    sys.path.insert(0, __file__.rsplit("/", 1)[0])
+    from test_gpu_parity import _spill_heavy_programs
+
+    batch = ir.Batch(_spill_heavy_programs(n=16))
+    code, descs = device_program(batch)
+    ops = code[:, 0] & 0xFF
+    spills = np.isin(ops, [ir.W_SPILL, ir.B_SPILL])
+    lds = spills & ((code[:, 2] & SPILL_LDS) != 0)
+    assert lds.sum() > 10 and (spills & ~lds).sum() > 10
+    rng = random.Random(9)
+    for s in range(len(batch.descs)):
+        sv = O.SetView.from_batch(batch, s)
+        d = descs[s]
+        rows = [tuple(int(x) for x in r) for r in code[d[0]:d[0] + d[1]]]
+        cands = sv.gen_assignments(np.arange(16, dtype=np.uint64), 3)
+        for vals in cands + [[rng.getrandbits(sv.var_width(v)) for v in range(len(sv.schema))]]:
+            assert eval_device(sv, rows, vals) == sv.evaluate(vals), s

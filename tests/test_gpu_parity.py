@@ -454,3 +454,40 @@ def test_candidate0_limbs_match_device_materialize(engine):
     for seed in (0, 7, 0xDEAD_BEEF):
         got = engine.materialize_limbs(db, list(range(len(progs))), [0] * len(progs), seed=seed)
         assert np.array_equal(got, np.concatenate(rows)), seed
+
+
+def _spill_heavy_programs(n=24, nw=4):
+    """Config-3 DAGs lowered over only ``nw`` W registers (those that fit): spills
+    everywhere, many of them across an EXP (scratch) and many not (pf_batch_create's LDS
+    slots, PF_SPILL_LDS)."""
+    from mythril_amd import lower as L
+
+    real = synth.lower
+    out, i = [], 0
+    try:
+        synth.lower = lambda dag, seed=0, name="": L.lower(dag, seed, name, nw)
+        while len(out) < n and i < 20 * n:
+            try:
+                out.append(synth.random_dag_set(300 + i, plant=(i % 3 == 0))[0])
+            except L.LoweringError:
+                pass
+            i += 1
+    finally:
+        synth.lower = real
+    return out
+
+
+@pytest.mark.parametrize("flags", [0, ir.FLAG_EARLY_EXIT | ir.FLAG_SHORTCIRCUIT])
+def test_spill_heavy_programs_match_oracle(engine, flags):
+    """Programs at three W registers (spill code in most instructions, both kinds of spill
+    slot): the smallest witness equals the oracle's, which evaluates the program as lowered."""
+    budget, seed = 512, 0x5EED
+    progs = _spill_heavy_programs()
+    n_spill = sum(int(((p.words[:, 0] & 0xFF) == ir.W_SPILL).sum()) for p in progs if hasattr(p, "words"))
+    db = engine.upload(progs)
+    res = engine.check(db, budget=budget, seed=seed, flags=flags)
+    for i, p in enumerate(progs):
+        want = _oracle_first(p, budget, seed)
+        got = None if res.found[i] == 0xFFFFFFFF else int(res.found[i])
+        assert got == want, (i, p.name, got, want)
+    assert n_spill == 0 or n_spill > len(progs)
