@@ -427,3 +427,43 @@ def test_gpu_eval_programs_match_per_group_programs(engine, monkeypatch):
         assert list(got.all(axis=0)) == list(want), q.origin
     assert split >= 10
     MC._GROUPS.clear()
+
+
+@pytest.mark.gpu
+def test_gpu_eval_programs_edge_shapes(engine):
+    """pf_eval_programs over sets of unlike shapes in one call — no variables (always true /
+    always false), config-3 DAG programs (16 registers' worth in the wide kernel), LASER-like
+    sets — and 130 candidates (three waves per set): each set's verdicts equal the oracle's
+    on its own SoA rows."""
+    import random
+
+    import pyoracle as O
+    from mythril_amd import ir, synth
+    from mythril_amd.lower import Dag, lower
+
+    progs = []
+    for b in (True, False):
+        d = Dag()
+        d.assert_(d.bconst(b))
+        progs.append(lower(d))
+    progs += [synth.random_dag_set(700 + i, plant=False)[0] for i in range(3)]
+    progs += [synth.mythril_like_set(i) for i in range(2)]
+    b = ir.Batch(progs)
+    pack = tuple(np.ascontiguousarray(a, dtype=np.uint32).reshape(-1) for a in (b.code, b.consts, b.schema, b.descs))
+    n_vars = len(b.schema)
+    n_cand = 130
+    rng = random.Random(11)
+    soa = np.zeros((max(n_vars, 1), 8, n_cand), dtype=np.uint32)
+    for v in range(n_vars):
+        w = (int(b.schema[v][0]) >> 8) & 0x3FF
+        for c in range(n_cand):
+            x = rng.choice([0, 1, rng.getrandbits(w)])
+            soa[v, :, c] = [(x >> (32 * k)) & 0xFFFFFFFF for k in range(8)]
+    got = engine.eval_programs(pack, soa[:n_vars] if n_vars else soa)
+    assert got.shape == (len(progs), n_cand)
+    for s in range(len(progs)):
+        sv = O.SetView.from_batch(b, s)
+        off, nv = int(b.descs[s][4]), int(b.descs[s][5])
+        want = [bool(sv.evaluate([O.limbs_to_int(soa[off + v, :, c]) for v in range(nv)])) for c in range(n_cand)]
+        assert list(got[s]) == want, s
+    assert got[0].all() and not got[1].any()
