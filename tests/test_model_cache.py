@@ -467,3 +467,27 @@ def test_gpu_eval_programs_edge_shapes(engine):
         want = [bool(sv.evaluate([O.limbs_to_int(soa[off + v, :, c]) for v in range(nv)])) for c in range(n_cand)]
         assert list(got[s]) == want, s
     assert got[0].all() and not got[1].any()
+
+
+@pytest.mark.gpu
+def test_gpu_witness_leaves_native_equal_python(standin, engine):
+    """The same equality as the CPU test, on witnesses the MI355X found: every corpus leaf's
+    value from pflt_witness_values equals interp.Witness.leaf_value."""
+    models, _, qs, reg = W.build(z3, standin, n_models=30, n_scenarios=4, n_queries=40)
+    wms = [m.raw[0].internal for m in models if m.raw and isinstance(m.raw[0], integration.Z3WitnessView)]
+    assert wms and all(wm.parts for wm in wms)
+    lvs = [MC.leaf_values_of(z3, integration.Z3WitnessView(wm)) for wm in wms]
+    leaves = {}
+    for q in qs:
+        try:
+            ls, _ = MC.explicit_program(T.and_(*q.constraints) if len(q.constraints) > 1 else q.constraints[0])
+        except Exception:  # noqa: BLE001 - a query the explicit lowering declines
+            continue
+        leaves.update(dict.fromkeys(ls))
+    leaves = list(leaves)
+    rows = MC.native_rows(lvs, leaves)
+    assert len(rows) >= 0.9 * len(lvs)
+    for j, r in rows.items():
+        w = wms[j].w
+        for t, limbs in zip(leaves, r):
+            assert native_terms.ints_of(limbs[None])[0] == w.leaf_value(t) & T.M(max(t.width, 1)), t
