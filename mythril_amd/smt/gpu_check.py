@@ -67,6 +67,14 @@ class GpuConfig:
     # 95 % of the corpus' wall time on one core
     workers: int = int(os.environ.get("PF_LOWER_WORKERS", "0")) or min(16, os.cpu_count() or 1)
     parallel_min: int = 48
+    # candidate 0 of a long bucket program first as the bucket's conjuncts side by side: a
+    # bucket whose program has at least this many instructions and whose every variable
+    # carries a parent / hint value (so candidate 0 is known on the host) is evaluated at
+    # that assignment by its cached per-conjunct explicit programs in one launch, a wave per
+    # conjunct (model_cache, pf_eval_programs) — the search is a lone wave walking the whole
+    # program, ~0.45 us per instruction.  A bucket that holds there skips the search; the
+    # host re-check runs as for any witness.  0 turns it off.
+    probe_min_ins: int = int(os.environ.get("PF_PROBE_SPLIT_MIN", "400"))
 
 
 CONFIG = GpuConfig()
@@ -82,6 +90,8 @@ class GpuStats:
     lowering_failures: Dict[str, int] = field(default_factory=dict)
     bucket_origin: Dict[str, int] = field(default_factory=dict)  # witness provenance per bucket
     recheck_failures: int = 0  # GPU witnesses the host re-check rejected (must stay 0)
+    probe_split: int = 0       # long buckets whose candidate 0 went through the conjunct probe
+    probe_split_sat: int = 0   # ... and held there (no search launch for them)
     kernel_ms: float = 0.0
     evals: int = 0
     host_s: float = 0.0      # lowering + hints + witness re-checks
@@ -249,6 +259,54 @@ def _witness_limbs(eng, db, mine: List[int], base: int, progs, found, seed_: int
         else:
             return np.concatenate(parts) if parts else np.zeros((0, 8), dtype=np.uint32)
     return eng.materialize_limbs(db, [k - base for k in mine], [int(found[k]) for k in mine], seed=seed_)
+
+
+def _probe_candidate0(eng, progs, lows, keys, reg, cfg) -> Dict[int, np.ndarray]:
+    """{program index: candidate-0 limb rows} for the long programs whose every variable
+    carries a parent value and whose bucket holds at that assignment — decided on the device
+    by the bucket's per-conjunct explicit programs (mythril_amd/model_cache.py, cached across
+    queries) in one pf_eval_programs launch, the leaves valued by the native witness
+    interpretation of the assignment (the one the host re-check uses).  A bucket whose
+    explicit form is out of reach (lowering, a leaf the native evaluator declines, an engine
+    without pf_eval_programs) is left to the search."""
+    from .. import model_cache as MC
+    from . import native_terms
+
+    if not hasattr(eng, "eval_programs"):
+        return {}
+    out: Dict[int, np.ndarray] = {}
+    for k, prog in enumerate(progs):
+        r = getattr(prog, "native_result", None)
+        if r is None or int(r.info[6]) < cfg.probe_min_ins:
+            continue
+        rows = native_terms.candidate0_limbs(prog)
+        if rows is None:
+            continue
+        cs = [c for c in keys[k][0] if c is not T.TRUE]
+        if not cs:
+            continue
+        try:
+            leaves, program = MC.explicit_groups(T.and_(*cs) if len(cs) > 1 else cs[0])
+        except LoweringError:
+            continue
+        nw = native_terms.NativeWitness.build([(lows[k], rows)], reg)
+        if nw is None:
+            continue
+        if leaves:
+            vals, ok = native_terms.witness_values_many([nw], list(leaves), reg, 1)
+            if not ok.all():
+                continue
+            block = vals
+        else:
+            block = np.zeros((1, 0, 8), dtype=np.uint32)
+        sat = MC.eval_rows(program, block if leaves else [b""], eng)
+        with _lock:
+            STATS.probe_split += 1
+        if bool(sat[0]):
+            out[k] = rows
+            with _lock:
+                STATS.probe_split_sat += 1
+    return out
 
 
 def _native_batch() -> bool:
@@ -488,42 +546,61 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
     res = None
     if progs:
         eng = get_engine()
-        # one batch per device of the engine (cost-balanced shards), searched concurrently
-        dbs = eng.upload_sharded(progs) if hasattr(eng, "upload_sharded") else [eng.upload(progs)]
-        lap("upload")
-        if len(dbs) == 1:
-            res = eng.check(dbs[0], budget=cfg.budget, seed=cfg.seed, flags=cfg.flags,
-                            timeout_ms=cfg.timeout_ms)
-        else:
-            res = eng.check_many(dbs, budget=cfg.budget, seed=cfg.seed, flags=cfg.flags,
-                                 timeout_ms=cfg.timeout_ms)
-        lap("search")
-        sat = [k for k in range(len(progs)) if res.found[k] != 0xFFFFFFFF]
+        # long hinted buckets: candidate 0 by their conjuncts side by side first
+        pre: Dict[int, np.ndarray] = {}
+        if nat and cfg.probe_min_ins > 0:
+            pre = _probe_candidate0(eng, progs, lows, keys, reg, cfg)
+            if pre:
+                lap("probe")
+        search = [k for k in range(len(progs)) if k not in pre]
+        found_all = np.full(len(progs), 0xFFFFFFFF, dtype=np.uint32)
+        for k in pre:
+            found_all[k] = 0
+        timed_out = False
         vals_of = {}
-        base = 0
         limb_rows = []   # native: the witnesses' variables as limbs, in `sat` order
-        for db in dbs:
-            mine = [k for k in sat if base <= k < base + len(db)]
-            if mine:
-                sids, cids = [k - base for k in mine], [int(res.found[k]) for k in mine]
-                if nat:
-                    if hasattr(eng, "materialize_limbs"):
-                        rows = _witness_limbs(eng, db, mine, base, progs, res.found, cfg.seed)
+        if search:
+            sprogs = [progs[k] for k in search]
+            # one batch per device of the engine (cost-balanced shards), searched concurrently
+            dbs = eng.upload_sharded(sprogs) if hasattr(eng, "upload_sharded") else [eng.upload(sprogs)]
+            lap("upload")
+            if len(dbs) == 1:
+                res = eng.check(dbs[0], budget=cfg.budget, seed=cfg.seed, flags=cfg.flags,
+                                timeout_ms=cfg.timeout_ms)
+            else:
+                res = eng.check_many(dbs, budget=cfg.budget, seed=cfg.seed, flags=cfg.flags,
+                                     timeout_ms=cfg.timeout_ms)
+            timed_out = bool(res.timed_out)
+            lap("search")
+            for i, k in enumerate(search):
+                found_all[k] = res.found[i]
+            ssat = [i for i in range(len(search)) if res.found[i] != 0xFFFFFFFF]
+            base = 0
+            for db in dbs:
+                mine = [i for i in ssat if base <= i < base + len(db)]
+                if mine:
+                    sids, cids = [i - base for i in mine], [int(res.found[i]) for i in mine]
+                    if nat:
+                        if hasattr(eng, "materialize_limbs"):
+                            rows = _witness_limbs(eng, db, mine, base, sprogs, res.found, cfg.seed)
+                        else:
+                            rows = ir.limbs_array([x for vs in eng.materialize(db, sids, cids, seed=cfg.seed)
+                                                   for x in vs])
+                        o = 0
+                        for i in mine:
+                            nv = int(db.batch.descs[i - base][5])
+                            vals_of[search[i]] = rows[o:o + nv]
+                            o += nv
                     else:
-                        rows = ir.limbs_array([x for vs in eng.materialize(db, sids, cids, seed=cfg.seed)
-                                               for x in vs])
-                    limb_rows.append(rows)
-                    o = 0
-                    for k in mine:
-                        nv = int(db.batch.descs[k - base][5])
-                        vals_of[k] = rows[o:o + nv]
-                        o += nv
-                else:
-                    got = eng.materialize(db, sids, cids, seed=cfg.seed)
-                    vals_of.update(zip(mine, got))
-            base += len(db)
-            db.free()
+                        got = eng.materialize(db, sids, cids, seed=cfg.seed)
+                        vals_of.update(zip([search[i] for i in mine], got))
+                base += len(db)
+                db.free()
+        vals_of.update(pre)
+        sat = [k for k in range(len(progs)) if found_all[k] != 0xFFFFFFFF]
         vals = [vals_of[k] for k in sat]
+        if nat:
+            limb_rows = [np.asarray(v, dtype=np.uint32).reshape(-1, 8) for v in vals]
         lap("materialize")
         status = None
         if nat and sat:
@@ -532,7 +609,7 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
                                                _host_threads(cfg, len(sat)))
         for k in range(len(progs)):
             found[keys[k]] = None
-        if not res.timed_out:  # a deadline-cut search is not a complete answer
+        if not timed_out:  # a deadline-cut search is not a complete answer
             sat_set = set(sat)
             with _lock:
                 for k in range(len(progs)):
@@ -544,7 +621,7 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
             key = keys[k]
             # provenance of the witness: candidate 0 of a hinted program is the host's
             # constraint-directed hint model itself; any other index was found by the search
-            idx = int(res.found[k])
+            idx = int(found_all[k])
             origin[key] = _origin(idx, progs[k], cfg.hints, parented[k])
             # re-check on the host under the same interpretation before trusting it:
             # natively (pflt_recheck, the Witness interpretation bit for bit) when built
@@ -567,7 +644,7 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
                 with _lock:
                     STATS.recheck_failures += 1
                     prog = progs[k].decode() if hasattr(progs[k], "decode") else progs[k]
-                    _RECHECK_DEBUG.append((key[0], lows[k], v, prog, int(res.found[k])))
+                    _RECHECK_DEBUG.append((key[0], lows[k], v, prog, int(found_all[k])))
                     del _RECHECK_DEBUG[:-8]
             else:
                 found[key] = (lows[k], v)
