@@ -279,6 +279,12 @@ def _probe_candidate0(eng, progs, lows, keys, reg, cfg) -> Dict[int, np.ndarray]
         r = getattr(prog, "native_result", None)
         if r is None or int(r.info[6]) < cfg.probe_min_ins:
             continue
+        # only where the host's hint solver left every (distinct) root true under its model
+        # (info[13] n_sat): a probe that fails costs its launch on top of the search (the
+        # hint is a guess; the device decides)
+        n_roots = int(r.info[10])
+        if n_roots == 0 or int(r.info[13]) < len(set(r.get(native_terms.GET_ROOTS, n_roots, 1).tolist())):
+            continue
         rows = native_terms.candidate0_limbs(prog)
         if rows is None:
             continue
@@ -550,8 +556,7 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
         pre: Dict[int, np.ndarray] = {}
         if nat and cfg.probe_min_ins > 0:
             pre = _probe_candidate0(eng, progs, lows, keys, reg, cfg)
-            if pre:
-                lap("probe")
+            lap("probe")
         search = [k for k in range(len(progs)) if k not in pre]
         found_all = np.full(len(progs), 0xFFFFFFFF, dtype=np.uint32)
         for k in pre:
