@@ -75,6 +75,9 @@ class GpuConfig:
     # program, ~0.45 us per instruction.  A bucket that holds there skips the search; the
     # host re-check runs as for any witness.  0 turns it off.
     probe_min_ins: int = int(os.environ.get("PF_PROBE_SPLIT_MIN", "400"))
+    # ... for calls of at most this many programs (a single query's buckets: latency); a
+    # batch's search runs its long programs side by side anyway
+    probe_max_progs: int = 4
 
 
 CONFIG = GpuConfig()
@@ -554,7 +557,9 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
         eng = get_engine()
         # long hinted buckets: candidate 0 by their conjuncts side by side first
         pre: Dict[int, np.ndarray] = {}
-        if nat and cfg.probe_min_ins > 0:
+        if nat and 0 < cfg.probe_min_ins and len(progs) <= cfg.probe_max_progs and any(
+                int(getattr(getattr(p, "native_result", None), "info", [0] * 7)[6]) >= cfg.probe_min_ins
+                for p in progs):
             pre = _probe_candidate0(eng, progs, lows, keys, reg, cfg)
             lap("probe")
         search = [k for k in range(len(progs)) if k not in pre]
