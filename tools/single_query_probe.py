@@ -39,6 +39,7 @@ def main():
     # warm: the corpus in one call, as the bench runs it before the sample
     gpu_check.check_sets([q.constraints for q in c.queries], registry=c.kfm.registry)
     sample = [q for q in c.queries if q.label == "sat"][:96]
+    gpu_check.STATS.probe_split = gpu_check.STATS.probe_split_sat = 0
     rows = []
     for i, q in enumerate(sample):
         gpu_check.reset_cache()
@@ -51,7 +52,8 @@ def main():
         rows.append((ms, i, q.origin, ph, list(calls)))
     lat = np.array([r[0] for r in rows])
     print(f"median {np.median(lat):.3f} mean {lat.mean():.3f} p95 {np.percentile(lat, 95):.3f} "
-          f"max {lat.max():.3f} ms")
+          f"max {lat.max():.3f} ms  split probe {gpu_check.STATS.probe_split} buckets, "
+          f"{gpu_check.STATS.probe_split_sat} answered")
     for ms, i, origin, ph, cl in sorted(rows, key=lambda r: -r[0])[:top]:
         print(f"{ms:8.3f} ms  query {i} {origin}  phases {ph}")
         for cc in cl:
