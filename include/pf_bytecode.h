@@ -131,6 +131,14 @@ enum pf_opcode {
 #define PF_I_KA (1u << 25)
 #define PF_I_KB (1u << 26)
 
+/* w0 bits 27 / 28: operand a / b is the W result of the instruction right before (its
+ * traffic bit cleared: no register read).  Set only by pf_batch_create's forwarding
+ * peephole, which also clears the previous instruction's PF_TR_WW when nothing else reads
+ * that result before its register's next write (no write-back).  Never set by the host
+ * lowering. */
+#define PF_I_FA (1u << 27)
+#define PF_I_FB (1u << 28)
+
 /* aux of a W/B SPILL or FILL: PF_SPILL_LDS | e keeps the value in LDS entry e (1..3) of the
  * lane's EXP window table instead of private scratch slot aux.  Set only by pf_batch_create's
  * spill peephole, for a spill whose fills all come before the next W_EXP (which rewrites

@@ -600,6 +600,45 @@ void device_program(const std::vector<uint32_t>& code_fixed, std::vector<pf_set_
             }
         }
 #endif
+#ifndef PF_NO_FORWARD
+        // ---- 5. back-to-back forwarding: an instruction reading the W register the kept
+        // instruction right before it wrote takes that result directly (PF_I_FA / PF_I_FB,
+        // traffic bit cleared), and the writer skips its write-back (PF_TR_WW cleared) when
+        // no later instruction reads the register before its next write
+        {
+            int64_t prev = -1;
+            for (uint32_t q = 0; q < n; q++) {
+                if (drop[q]) continue;
+                const int64_t p = prev;
+                prev = q;
+                uint32_t& qw0 = P[4 * q];
+                const uint32_t qop = qw0 & 0xffu;
+                if (qop == PF_END) break;
+                if (p < 0) continue;
+                uint32_t& pw0 = P[4 * (size_t)p];
+                const uint32_t ptr = (pw0 >> 18) & 7u, pd = P[4 * (size_t)p + 1] & 0xffu;
+                if (!(ptr & PF_TR_WW) || PF_OP_WRITES_B(pw0 & 0xffu) || pd > PF_NW) continue;
+                const uint32_t qtr = (qw0 >> 18) & 7u, qw1 = P[4 * q + 1];
+                const bool fa = (qtr & PF_TR_RA) && ((qw1 >> 8) & 0xffu) == pd;
+                const bool fb = (qtr & PF_TR_RB) && ((qw1 >> 16) & 0xffu) == pd;
+                if (!fa && !fb) continue;
+                qw0 &= ~(((fa ? PF_TR_RA : 0u) | (fb ? PF_TR_RB : 0u)) << 18);
+                qw0 |= (fa ? PF_I_FA : 0u) | (fb ? PF_I_FB : 0u);
+                bool live = false;
+                if (!((qtr & PF_TR_WW) && (qw1 & 0xffu) == pd)) {
+                    for (uint32_t r = q + 1; r < n && !live; r++) {
+                        if (drop[r]) continue;
+                        const uint32_t rw0 = P[4 * r], rw1 = P[4 * r + 1], rtr = (rw0 >> 18) & 7u;
+                        if ((rw0 & 0xffu) == PF_END) break;
+                        live = ((rtr & PF_TR_RA) && ((rw1 >> 8) & 0xffu) == pd) ||
+                               ((rtr & PF_TR_RB) && ((rw1 >> 16) & 0xffu) == pd);
+                        if ((rtr & PF_TR_WW) && (rw1 & 0xffu) == pd) break;
+                    }
+                }
+                if (!live) pw0 &= ~(PF_TR_WW << 18);
+            }
+        }
+#endif
         const size_t first = code_out.size() / 4;
         for (uint32_t i = 0; i < n; i++)
             if (!drop[i]) code_out.insert(code_out.end(), P.begin() + 4 * (size_t)i, P.begin() + 4 * (size_t)i + 4);

@@ -615,6 +615,20 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
     // the pipelined scalar load
     const pf_code_t* ip = (const pf_code_t*)S.code;
     uint4 In = fetch_ins(ip);
+    // the last W result (PF_I_FA / PF_I_FB operands: pf_batch_create's forwarding peephole
+    // sets them only on the instruction right after a W write)
+#ifndef PF_NO_FORWARD
+    u256 last;
+#define PF_FWD_A() else if (I.x & PF_I_FA) x = last
+#define PF_FWD_B() else if (I.x & PF_I_FB) y = last
+#define PF_FWD_KEEP() last = z
+#define PF_FWD_WB(tr) __builtin_expect(((tr) & PF_TR_WW) != 0u, 1)
+#else
+#define PF_FWD_A() else {}
+#define PF_FWD_B() else {}
+#define PF_FWD_KEEP() (void)0
+#define PF_FWD_WB(tr) true
+#endif
     for (;;) {
 #ifdef PF_PROFILE_UNITS
         {
@@ -652,10 +666,14 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
         // against the register file of the kernel that runs the set
         if (NREG == 8) {
             if (__builtin_expect((tr & PF_TR_RA) != 0u, 1)) RDN_SW(x, Wn, a, exp_tbl);
+            PF_FWD_A();
             if (__builtin_expect((tr & PF_TR_RB) != 0u, 1)) RDN_SW(y, Wn, b, exp_tbl);
+            PF_FWD_B();
         } else {
             if (__builtin_expect((tr & PF_TR_RA) != 0u, 1)) RD_W(x, W, a, LPB);
+            PF_FWD_A();
             if (__builtin_expect((tr & PF_TR_RB) != 0u, 1)) RD_W(y, W, b, LPB);
+            PF_FWD_B();
         }
         // constant operands (pf_batch_create's peephole deleted their W_CONST): one scalar
         // load of const[a] / const[b] each
@@ -914,11 +932,14 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
             // W write-back of every op that reaches here (ops without a W result other than
             // the B ops above — W_SPILL — write the sink register PF_W_SINK)
             maskw(z, w);
+            PF_FWD_KEEP();
             const uint32_t dd = (tr & PF_TR_WW) ? d : (uint32_t)(NREG - 1);
             // keep the 8 indexed moves one s_set_gpr_idx block: the scheduler otherwise
             // interleaves the B update into it and re-enters indexing mode per move
             if (NREG == 8) {
-                WRN_SW(Wn, d, z, exp_tbl);  // only W results reach here (W_SPILL leaves above)
+                // only W results reach here (W_SPILL leaves above); PF_TR_WW clear = a result
+                // only the next instruction reads (forwarded), no write-back
+                if (PF_FWD_WB(tr)) WRN_SW(Wn, d, z, exp_tbl);
             } else {
                 __builtin_amdgcn_sched_barrier(0);
                 WR_W(W, dd, z, LPB);
@@ -934,6 +955,10 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
     *complete = sc ^ 1u;
     *ops += cost;
     return root;
+#undef PF_FWD_A
+#undef PF_FWD_B
+#undef PF_FWD_KEEP
+#undef PF_FWD_WB
 #undef BGET
 }
 

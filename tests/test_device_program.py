@@ -16,7 +16,8 @@ import pytest
 import pyoracle as O
 from mythril_amd import _lib, ir, synth
 
-I_ASSERT, I_KA, I_KB = 1 << 24, 1 << 25, 1 << 26
+I_ASSERT, I_KA, I_KB, I_FA, I_FB = 1 << 24, 1 << 25, 1 << 26, 1 << 27, 1 << 28
+TR_WW = 4 << 18
 
 
 def device_program(batch):
@@ -36,12 +37,17 @@ def device_program(batch):
 
 
 def eval_device(sv, code_rows, values):
-    """SetView.evaluate with the device flags: a KA / KB operand is const[a] / const[b] (held
-    here in two spare register slots), a PF_I_ASSERT op also asserts its B result."""
+    """SetView.evaluate with the device flags: a KA / KB operand is const[a] / const[b], an
+    FA / FB operand the previous instruction's W result (held here in spare register slots);
+    a W result whose PF_TR_WW is cleared is not written back (its register keeps its old
+    value, or none: a later read of it fails here); a PF_I_ASSERT op also asserts its B
+    result."""
     W, B, S = {}, {}, {}
     root = True
+    last = None
     for (w0, w1, aux0, aux1) in code_rows:
-        if w0 & 0xFF == O.OP["END"]:
+        op = w0 & 0xFF
+        if op == O.OP["END"]:
             break
         if w0 & I_KA:
             W[0xFE] = sv.consts[(w1 >> 8) & 0xFF]
@@ -49,7 +55,24 @@ def eval_device(sv, code_rows, values):
         if w0 & I_KB:
             W[0xFD] = sv.consts[(w1 >> 16) & 0xFF]
             w1 = (w1 & ~0xFF0000) | (0xFD << 16)
-        root = _step((w0 & ~(I_ASSERT | I_KA | I_KB), w1, aux0, aux1), sv.consts, W, B, S, values, root)
+        if w0 & I_FA:
+            W[0xFC] = last
+            w1 = (w1 & ~0xFF00) | (0xFC << 8)
+        if w0 & I_FB:
+            W[0xFB] = last
+            w1 = (w1 & ~0xFF0000) | (0xFB << 16)
+        w_result = op < O.OP["B_CONST"] and op != O.OP["W_SPILL"]
+        d = w1 & 0xFF
+        old = W.get(d)
+        root = _step((w0 & ~(I_ASSERT | I_KA | I_KB | I_FA | I_FB), w1, aux0, aux1), sv.consts, W, B, S, values,
+                     root)
+        if w_result:
+            last = W[d]
+            if not (w0 & TR_WW):          # forwarded only: no write-back
+                if old is None:
+                    del W[d]
+                else:
+                    W[d] = old
         if w0 & I_ASSERT:
             root = root and B[w1 & 0xFF]
     return root
@@ -164,6 +187,10 @@ def test_device_program_matches_the_lowered_program(monkeypatch):
     spills = np.isin(ops, [ir.W_SPILL, ir.B_SPILL])
     n_lds = int((spills & ((code[:, 2] & SPILL_LDS) != 0)).sum())
     assert 0 < n_lds < int(spills.sum())     # some spills moved to LDS, not those across an EXP
+    n_fwd = int(((code[:, 0] & (I_FA | I_FB)) != 0).sum())
+    w_res = (ops < ir.B_CONST) & (ops != ir.END) & (ops != ir.W_SPILL)
+    n_nowb = int((w_res & ((code[:, 0] & TR_WW) == 0)).sum())
+    assert n_fwd > 0 and 0 < n_nowb <= n_fwd  # forwarded operands; results only they read
     rng = random.Random(3)
     for s in range(len(batch.descs)):
         sv = O.SetView.from_batch(batch, s)

@@ -5,9 +5,9 @@ export TMPDIR=/tmp
 O=gpurun_out/spillpol
 mkdir -p $O
 P="--no-cpu-baseline --corpus-scenarios 0 --keccak-log2 0 --full-pass-dags 0 --quick-sat-queries 0"
-for rep in 1 2; do
+for rep in $(seq 1 ${REPS:-2}); do
 for SP in ${POLS:-1 2 3}; do
-  PF_VAR_SPILL_USES=$SP timeout -k 10 200 python -u bench.py --steps 5 --warmup 2 $P > $O/b_${SP}_$rep.log 2>&1 || { echo "bench $SP failed"; exit 1; }
+  PF_VAR_SPILL_USES=$SP timeout -k 10 200 python -u bench.py --steps ${STEPS:-5} --warmup 2 $P > $O/b_${SP}_$rep.log 2>&1 || { echo "bench $SP failed"; exit 1; }
   python -c "import json; d=json.loads(open('$O/b_${SP}_$rep.log').read().strip().splitlines()[-1]); print('pol $SP', round(d['value']/1e9,4), round(d['roofline']['kernel_ms_avg'],3))"
 done
 done
