@@ -88,6 +88,11 @@ class Lowerer {
         // eviction (lower.py _var_spill_uses: the same environment variable)
         const char* e = getenv("PF_VAR_SPILL_USES");
         spill_min_uses = e ? std::max(1, atoi(e)) : 1;
+        // ... and at least this many when a W_EXP runs before its last use (the device
+        // program's LDS spill slots are EXP's table entries, so that spill lands in scratch;
+        // lower.py _var_spill_uses_exp: the same environment variable and default)
+        const char* x = getenv("PF_VAR_SPILL_USES_EXP");
+        spill_exp_uses = x ? std::max(0, atoi(x)) : 99;
     }
 
     std::vector<uint32_t> code;    // 4 words per instruction
@@ -106,6 +111,9 @@ class Lowerer {
             }
         }
         for (size_t i = 0; i < nn; ++i) use_off[i + 1] += use_off[i];
+        exp_at.clear();
+        for (size_t t = 0; t < events.size(); ++t)
+            if (!events[t].first && N[events[t].second].kind == PF_W_EXP) exp_at.push_back((int)t);
         use_at.assign(use_off[nn], 0);
         {
             std::vector<int> fill(use_off.begin(), use_off.end() - 1);
@@ -143,8 +151,17 @@ class Lowerer {
     std::vector<int> use_off, use_at;  // uses of node i: use_at[use_off[i] .. use_off[i + 1])
     std::vector<int> where, slot_of, remat, cost, free_slots;
     int filling = NONE;  // the spilled node materialize() is restoring (not a steal candidate)
-    int spill_min_uses = 1;
+    int spill_min_uses = 1, spill_exp_uses = 99;
+    std::vector<int> exp_at;  // event times of the W_EXP nodes, ascending
     RegFile W, B;
+
+    // uses a variable evicted at t must still have to be spilled rather than regenerated
+    int var_min_uses(int nd, int t) const {
+        if (spill_exp_uses <= spill_min_uses || use_off[nd + 1] == use_off[nd]) return spill_min_uses;
+        const int last = use_at[use_off[nd + 1] - 1];
+        const auto it = std::upper_bound(exp_at.begin(), exp_at.end(), t);
+        return (it != exp_at.end() && *it < last) ? spill_exp_uses : spill_min_uses;
+    }
 
     void order(const uint32_t* roots, size_t n_roots) {
         std::vector<int> size(nn, 0);
@@ -309,7 +326,7 @@ class Lowerer {
                 // _VAR_SPILL_COST): one spill now, fills later, no generator re-run
                 const int sz = slot_of[nd] != NONE ? 1
                              : (N[nd].kind == PFL_K_VAR && !free_slots.empty() &&
-                                uses_after(nd, t) >= spill_min_uses) ? 2
+                                uses_after(nd, t) >= var_min_uses(nd, t)) ? 2
                                                                                 : remat_cost(nd);
                 const long long nu = -(long long)next_use(nd, t);
                 if (!have || sz < best_sz || (sz == best_sz && (nu < best_nu || (nu == best_nu && rg < best_r)))) {
@@ -323,7 +340,7 @@ class Lowerer {
                 r = best_r;
                 const int old = rf.holder[r];
                 if (N[old].kind == PFL_K_VAR && slot_of[old] == NONE && !free_slots.empty() &&
-                    uses_after(old, t) >= spill_min_uses)
+                    uses_after(old, t) >= var_min_uses(old, t))
                     spill(r, old, t, false);
             } else {  // spill the value used farthest in the future
                 int vr = -1, vfar = -1;

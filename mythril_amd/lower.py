@@ -325,6 +325,14 @@ def _var_spill_uses() -> int:
     return max(1, int(os.environ.get("PF_VAR_SPILL_USES", "1")))
 
 
+# ... and at least this many when a W_EXP runs before the variable's last use: the device
+# program's LDS spill slots (pathfeas.hip pass 4) are EXP's window-table entries, so such a
+# spill lands in scratch — config 3 regenerates instead (WRITE_SIZE 34 -> 13 MB per launch
+# at -0.3 %, profiles/r05z_spillexp_ab.md).  0 or <= PF_VAR_SPILL_USES: the one rule everywhere
+def _var_spill_uses_exp() -> int:
+    return max(0, int(os.environ.get("PF_VAR_SPILL_USES_EXP", "99")))
+
+
 # ---- native lowering (libpflower.so, include/pf_lower.h) ----------------------------------
 _KIND_CODE = {K_VAR: 200, K_CONST: 201, K_BCONST: 202, K_BVAR: 203}
 _NATIVE = None
@@ -546,10 +554,20 @@ def lower_py(dag: Dag, seed: int = 0, name: str = "", nw: int = ir.NW) -> Progra
     filling: List[Optional[int]] = [None]   # the spilled node materialize() is restoring
 
     min_uses = _var_spill_uses()
+    exp_uses = _var_spill_uses_exp()
+    exp_at = [t for t, (kind, i) in enumerate(events) if kind == "node" and dag.nodes[i].kind == ir.W_EXP]
 
     def uses_after(nd: int, now: int) -> int:
         lst = uses.get(nd, [])
         return len(lst) - bisect.bisect_right(lst, now)
+
+    def var_min_uses(nd: int, now: int) -> int:
+        """Uses a variable evicted at ``now`` must still have to be spilled, not regenerated."""
+        lst = uses.get(nd, [])
+        if exp_uses <= min_uses or not lst:
+            return min_uses
+        k = bisect.bisect_right(exp_at, now)
+        return exp_uses if k < len(exp_at) and exp_at[k] < lst[-1] else min_uses
 
     def rank(t):
         def f(nd):
@@ -557,7 +575,7 @@ def lower_py(dag: Dag, seed: int = 0, name: str = "", nw: int = ir.NW) -> Progra
                 cost = 1
             elif remat_size(nd) is None:
                 return None
-            elif dag.nodes[nd].kind == K_VAR and free_slots and uses_after(nd, t) >= min_uses:
+            elif dag.nodes[nd].kind == K_VAR and free_slots and uses_after(nd, t) >= var_min_uses(nd, t):
                 cost = _VAR_SPILL_COST
             else:
                 cost = remat_cost(nd)
@@ -592,7 +610,7 @@ def lower_py(dag: Dag, seed: int = 0, name: str = "", nw: int = ir.NW) -> Progra
     def alloc(rf, nd, t, pinned):
         def on_evict(rg, old):
             if dag.nodes[old].kind == K_VAR and old not in slot_of and free_slots \
-                    and uses_after(old, t) >= min_uses:
+                    and uses_after(old, t) >= var_min_uses(old, t):
                 spill(rg, old, t, False)
         return rf.alloc(nd, rank(t), pinned, lambda rg, x: spill(rg, x, t), lambda x: next_use(x, t),
                         on_evict)

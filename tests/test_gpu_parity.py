@@ -459,12 +459,17 @@ def test_candidate0_limbs_match_device_materialize(engine):
 def _spill_heavy_programs(n=24, nw=4):
     """Config-3 DAGs lowered over only ``nw`` W registers (those that fit): spills
     everywhere, many of them across an EXP (scratch) and many not (pf_batch_create's LDS
-    slots, PF_SPILL_LDS)."""
+    slots, PF_SPILL_LDS).  Variables are spilled across EXPs too (PF_VAR_SPILL_USES_EXP=0;
+    the default regenerates them there), so both kinds of slot run."""
+    import os
+
     from mythril_amd import lower as L
 
     real = synth.lower
+    env = os.environ.get("PF_VAR_SPILL_USES_EXP")
     out, i = [], 0
     try:
+        os.environ["PF_VAR_SPILL_USES_EXP"] = "0"
         synth.lower = lambda dag, seed=0, name="": L.lower(dag, seed, name, nw)
         while len(out) < n and i < 20 * n:
             try:
@@ -474,6 +479,10 @@ def _spill_heavy_programs(n=24, nw=4):
             i += 1
     finally:
         synth.lower = real
+        if env is None:
+            os.environ.pop("PF_VAR_SPILL_USES_EXP", None)
+        else:
+            os.environ["PF_VAR_SPILL_USES_EXP"] = env
     return out
 
 
