@@ -615,18 +615,18 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
     // the pipelined scalar load
     const pf_code_t* ip = (const pf_code_t*)S.code;
     uint4 In = fetch_ins(ip);
-    // the last W result (PF_I_FA / PF_I_FB operands: pf_batch_create's forwarding peephole
-    // sets them only on the instruction right after a W write)
+    // z, the W result, lives across iterations: at the top of an instruction it still holds
+    // the last W result, which PF_I_FA / PF_I_FB operands read (pf_batch_create's forwarding
+    // peephole sets them only on the instruction right after a W write; nothing writes z in
+    // between — B ops and the narrow W_SPILL leave before the write-back)
+    u256 z;
 #ifndef PF_NO_FORWARD
-    u256 last;
-#define PF_FWD_A() else if (I.x & PF_I_FA) x = last
-#define PF_FWD_B() else if (I.x & PF_I_FB) y = last
-#define PF_FWD_KEEP() last = z
+#define PF_FWD_A() else if (I.x & PF_I_FA) x = z
+#define PF_FWD_B() else if (I.x & PF_I_FB) y = z
 #define PF_FWD_WB(tr) __builtin_expect(((tr) & PF_TR_WW) != 0u, 1)
 #else
 #define PF_FWD_A() else {}
 #define PF_FWD_B() else {}
-#define PF_FWD_KEEP() (void)0
 #define PF_FWD_WB(tr) true
 #endif
     for (;;) {
@@ -661,7 +661,7 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
         __builtin_amdgcn_sched_barrier(0);
         In = fetch_ins(++ip);
 #endif
-        u256 x, y, z;
+        u256 x, y;
         // register indices are trusted: pf_batch_create checks every read and write
         // against the register file of the kernel that runs the set
         if (NREG == 8) {
@@ -932,7 +932,6 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
             // W write-back of every op that reaches here (ops without a W result other than
             // the B ops above — W_SPILL — write the sink register PF_W_SINK)
             maskw(z, w);
-            PF_FWD_KEEP();
             const uint32_t dd = (tr & PF_TR_WW) ? d : (uint32_t)(NREG - 1);
             // keep the 8 indexed moves one s_set_gpr_idx block: the scheduler otherwise
             // interleaves the B update into it and re-enters indexing mode per move
@@ -957,7 +956,6 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
     return root;
 #undef PF_FWD_A
 #undef PF_FWD_B
-#undef PF_FWD_KEEP
 #undef PF_FWD_WB
 #undef BGET
 }
