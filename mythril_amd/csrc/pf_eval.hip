@@ -328,7 +328,23 @@ struct SetCtx {
     const uint32_t* parents;  // parent values base (global) or null
     uint32_t n_ins, n_const, n_vars, seed;
     uint32_t k0, k1;      // Philox key
+    uint32_t nc_rcp;      // urcp32(n_const) (0 without constants): gen_var's x % n_const
 };
+
+// x % d for 32-bit unsigned x, d >= 1, split so the reciprocal of a divisor that stays
+// fixed (a set's constant count) is formed once per set instead of in every generator call:
+// the backend's own expansion of a 32-bit udiv/urem (an f32 reciprocal estimate, one
+// Newton-Raphson step, a quotient estimate low by at most two, two corrections) — exact
+// for every x and d >= 1, the same values as the `%` it replaces
+PF_INL uint32_t urcp32(uint32_t d) {
+    uint32_t z = (uint32_t)(__builtin_amdgcn_rcpf((float)d) * 4294966784.0f);  // 0x4f7ffffe
+    return z + __umulhi(z, (0u - d) * z);
+}
+PF_INL uint32_t umod_rcp(uint32_t x, uint32_t d, uint32_t z) {
+    uint32_t r = x - __umulhi(x, z) * d;
+    r = r >= d ? r - d : r;
+    return r >= d ? r - d : r;
+}
 
 // candidate value of variable v (include/pf_bytecode.h generator contract).
 // Laid out for latency, not branches: the three Philox blocks depend only on (cand, v, key)
@@ -349,7 +365,7 @@ PF_INL u256 gen_var(const SetCtx& S, uint32_t v, uint32_t cand) {
     // (pathfeas.hip), so a set without constants reads that.
     const uint32_t ai = m.y & 3u;
     const uint32_t act = (uint32_t)(kind == PF_VK_ACTOR) & (uint32_t)(ai < hint1);
-    const uint32_t ci = S.n_const ? (m.y % S.n_const) : 0u;
+    const uint32_t ci = S.n_const ? umod_rcp(m.y, S.n_const, S.nc_rcp) : 0u;
     const uint32_t* gp = S.consts + (size_t)(act ? hint0 + ai : ci) * 8u;
     u256 g;
 #ifdef PF_DIAG_NO_GATHER  // timing probe only: the per-lane gather's cost
@@ -420,7 +436,8 @@ PF_INL u256 gen_var(const SetCtx& S, uint32_t v, uint32_t cand) {
         // 2^k+1, 2^160-1}[j] mod 2^w as one formula, (j >= 6 ? 2^p : 0) + delta
         // one power of two serves both the boundary arm (2^p) and the parent-mutation arm
         // (2^k, k = m[2] % w): a lane takes one arm, so the exponent is selected per lane
-        const uint32_t j = m.y % 12u, k = m.z % w;
+        // (w is uniform; a power of two — every 256-bit variable — needs no division)
+        const uint32_t j = m.y % 12u, k = (w & (w - 1u)) == 0u ? (m.z & (w - 1u)) : m.z % w;
         const uint32_t p = j <= 7u ? w - 1u : (j <= 10u ? k : 160u);
         const u256 pw = pow2(sel <= 8u ? p : k);
         u256 bnd;
@@ -976,6 +993,7 @@ PF_INL SetCtx make_ctx(const pf_set_desc* __restrict__ descs, uint32_t set,
     S.seed = D.seed;
     S.k0 = (uint32_t)gseed ^ D.seed;
     S.k1 = (uint32_t)(gseed >> 32);
+    S.nc_rcp = __builtin_amdgcn_readfirstlane(D.n_const ? urcp32(D.n_const) : 0u);  // set is uniform
     return S;
 }
 
@@ -1257,6 +1275,7 @@ pf_materialize_kernel(const pf_set_desc* __restrict__ descs, const uint4* __rest
     S.seed = D.seed;
     S.k0 = (uint32_t)gseed ^ D.seed;
     S.k1 = (uint32_t)(gseed >> 32);
+    S.nc_rcp = D.n_const ? urcp32(D.n_const) : 0u;
     u256 x = gen_var(S, v, cand_ids[req]);
     uint32_t* o = out + ((size_t)req_off[req] + v) * 8u;
 #pragma unroll
