@@ -500,3 +500,83 @@ def test_spill_heavy_programs_match_oracle(engine, flags):
         got = None if res.found[i] == 0xFFFFFFFF else int(res.found[i])
         assert got == want, (i, p.name, got, want)
     assert n_spill == 0 or n_spill > len(progs)
+
+
+def _forwarding_programs():
+    """Hand-built chains for the device program's forwarding pass (pathfeas.hip pass 5):
+    a result read as both operands of the next instruction, a forwarded result also read
+    later (its write-back kept), results feeding compares, ITE and B ops in between, a long
+    mixed chain (DIV, EXP, shifts, CONCAT / EXTRACT), and the same chains at three W
+    registers (spills and fills forwarded)."""
+    progs = []
+    for nw in (ir.NW_NARROW, 3):
+        dag = Dag()
+        x, y, z = dag.var("x", 256), dag.var("y", 256), dag.var("z", 256)
+        r = dag.op(ir.W_MUL, 256, x, y)
+        s = dag.op(ir.W_ADD, 256, r, r)                       # FA + FB
+        t = dag.op(ir.W_XOR, 256, s, x)
+        dag.assert_(dag.op(ir.B_ULT, 256, t, z))
+        progs.append(lower(dag, nw=nw))
+
+        dag = Dag()
+        x, y, z = dag.var("x", 256), dag.var("y", 256), dag.var("z", 256)
+        r = dag.op(ir.W_MUL, 256, x, y)
+        s = dag.op(ir.W_SUB, 256, r, x)                       # r forwarded ...
+        u = dag.op(ir.W_ADD, 256, s, r)                       # ... and read again
+        b = dag.op(ir.B_ULT, 256, u, z)
+        v = dag.op(ir.W_ITE, 256, b, u, s)
+        dag.assert_(dag.op(ir.B_ULE, 256, v, dag.op(ir.W_UDIV, 256, z, dag.op(ir.W_OR, 256, y, dag.const(1, 256)))))
+        progs.append(lower(dag, nw=nw))
+
+        dag = Dag()
+        x, y, z = dag.var("x", 256), dag.var("y", 256), dag.var("z", 256)
+        acc, other = x, y
+        ops = [ir.W_MUL, ir.W_ADD, ir.W_SDIV, ir.W_XOR, ir.W_UREM, ir.W_SUB, ir.W_SMOD, ir.W_AND,
+               ir.W_EXP, ir.W_OR, ir.W_SREM, ir.W_MUL]
+        for k in range(30):
+            op = ops[k % len(ops)]
+            acc = dag.op(op, 256, acc, other if k % 3 else z)
+            if k % 5 == 4:
+                acc = dag.op(ir.W_SHL, 256, acc, dag.const(k, 256))
+            if k % 7 == 6:
+                lo = dag.op(ir.W_EXTRACT, 128, acc, aux=0)
+                acc = dag.op(ir.W_CONCAT, 256, lo, dag.op(ir.W_EXTRACT, 128, other, aux=128), aux=128)
+            other = dag.op(ir.W_ADD, 256, other, acc) if k % 4 == 0 else other
+        dag.assert_(dag.op(ir.B_ULT, 256, acc, other))
+        progs.append(lower(dag, nw=nw))
+    return progs
+
+
+def test_forwarding_chains_match_oracle(engine):
+    """Every explicit candidate's verdict (pf_eval_assignments) and the search's smallest
+    witness on the forwarding chains equal the oracle's — with the device program actually
+    forwarding (PF_I_FA / PF_I_FB set, some write-backs skipped)."""
+    import random
+
+    from test_device_program import I_FA, I_FB, TR_WW, device_program
+
+    progs = _forwarding_programs()
+    code, _ = device_program(ir.Batch(progs))
+    ops = code[:, 0] & 0xFF
+    assert ((code[:, 0] & I_FA) != 0).sum() > 10 and ((code[:, 0] & I_FB) != 0).sum() > 0
+    w_res = (ops < ir.B_CONST) & (ops != ir.END) & (ops != ir.W_SPILL)
+    assert (w_res & ((code[:, 0] & TR_WW) == 0)).sum() > 5
+    rng = random.Random(17)
+    db = engine.upload(progs)
+    for s, p in enumerate(progs):
+        sv = O.SetView.from_batch(ir.Batch([p]), 0)
+        cands = []
+        for _ in range(192):
+            vals = [rng.getrandbits(256) for _ in p.vars]
+            if rng.random() < 0.3:
+                vals = [v >> rng.randrange(0, 256) for v in vals]
+            cands.append(vals)
+        got = engine.eval_assignments(db, s, ir.pack_assignments(p, cands))
+        want = np.array([bool(sv.evaluate(c)) for c in cands])
+        assert (got == want).all(), (s, np.nonzero(got != want)[0][:4])
+    budget, seed = 2048, 0xF0D
+    res = engine.check(db, budget=budget, seed=seed)
+    for i, p in enumerate(progs):
+        want = _oracle_first(p, budget, seed)
+        got = None if res.found[i] == 0xFFFFFFFF else int(res.found[i])
+        assert got == want, (i, got, want)
