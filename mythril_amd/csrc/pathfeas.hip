@@ -931,7 +931,9 @@ int pf_batch_create_on(int device, const uint32_t* code, size_t n_ins, const uin
     // set has constants (pf_eval.hip gen_var), so a set with none reads the entry at its own
     // const_off, which may be the pool's end.
     auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
-    const size_t o_code = 0, o_const = o_code + al(n_ins * 16), o_schema = o_const + al(n_const * 32 + 32),
+    // the code region carries one zero instruction past the last END: the kernel fetches the
+    // slot after an END before its dispatch leaves the program (pf_eval.hip run_program)
+    const size_t o_code = 0, o_const = o_code + al(n_ins * 16 + 16), o_schema = o_const + al(n_const * 32 + 32),
                  o_par = o_schema + al(n_vars * 16), o_desc = o_par + al(n_parents * 32),
                  o_order = o_desc + al(n_sets * sizeof(pf_set_desc)), o_found = o_order + al(n_sets * 4),
                  o_scr = o_found + al(std::max<size_t>(n_sets, 1) * 4),
@@ -1268,7 +1270,7 @@ static int eval_programs(const char* who, int device, const uint32_t* code, size
     auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
     const size_t nv = std::max<size_t>(n_vars, 1), n_dev = code_out.size() / 4, n_out = n_sets * (size_t)n_cand;
     const size_t soa_bytes = nv * 8 * (size_t)n_cand * 4;
-    const size_t o_code = 0, o_const = al(n_dev * 16), o_schema = o_const + al(n_const * 32 + 32),
+    const size_t o_code = 0, o_const = al(n_dev * 16 + 16), o_schema = o_const + al(n_const * 32 + 32),  // + the pad slot
                  o_desc = o_schema + al(nv * 16), o_soa = o_desc + al(n_sets * sizeof(pf_set_desc)),
                  o_out = o_soa + al(soa_bytes), total = o_out + n_out;
     uint8_t* pin = pinned_staging(std::max<size_t>(o_out, n_out));

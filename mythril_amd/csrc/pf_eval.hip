@@ -668,8 +668,13 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
         uint32_t pbucket = op == PF_W_EXP ? 8u : (op == PF_W_CONST ? 9u : unit);
 #endif
         // branch hints: every taken scalar branch refetches the wave's instruction buffer, so
-        // the common path (not END, operands read) is laid out as the fall-through
+        // the common path (operands read) is laid out as the fall-through.  END is a case
+        // of the unit dispatch below, not a test of its own on every instruction: it reads
+        // no operand (traffic bits 0) and its fetch of the slot after it stays inside the
+        // batch (pf_batch_create pads the code region by one instruction)
+#ifdef PF_END_TEST
         if (__builtin_expect(unit == PF_U_END, 0)) break;
+#endif
         // Issue the next fetch only after this instruction's words are decoded: scalar
         // loads return out of order, so a fetch issued before the decode would be waited
         // for together with the one being consumed (lgkmcnt(0)).  And after the operand
@@ -707,6 +712,9 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
             }
         }
 #ifndef PF_FETCH_EARLY
+        // (with END a case of the unit dispatch, every path fetches, and the backend hoists
+        // this invariant load to the top of the iteration: its latency then overlaps the
+        // operand reads — measured with the END case, profiles/r05zd_end_case_ab.md)
         __builtin_amdgcn_sched_barrier(0);
         In = fetch_ins(++ip);
 #endif
@@ -715,6 +723,10 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
         // opcode that needs them: the kernel's code must stay small enough for the
         // instruction cache, since consecutive bytecode instructions jump between units.
         switch (unit) {
+#ifndef PF_END_TEST
+            case PF_U_END:
+                goto program_end;
+#endif
             case PF_U_MUL:
                 // ---- multiplier: MUL = one product; EXP = windowed square-and-multiply over
                 // the low 84 exponent bits + the 2-adic closed form for bits 84..253
@@ -968,6 +980,9 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
         (void)prof;
 #endif
     }
+#ifndef PF_END_TEST
+program_end:
+#endif
     *complete = sc ^ 1u;
     *ops += cost;
     return root;
