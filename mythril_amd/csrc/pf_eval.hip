@@ -712,9 +712,6 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
             }
         }
 #ifndef PF_FETCH_EARLY
-        // (with END a case of the unit dispatch, every path fetches, and the backend hoists
-        // this invariant load to the top of the iteration: its latency then overlaps the
-        // operand reads — measured with the END case, profiles/r05zd_end_case_ab.md)
         __builtin_amdgcn_sched_barrier(0);
         In = fetch_ins(++ip);
 #endif
