@@ -262,3 +262,35 @@ def test_spill_heavy_device_programs_keep_their_values():
         cands = sv.gen_assignments(np.arange(16, dtype=np.uint64), 3)
         for vals in cands + [[rng.getrandbits(sv.var_width(v)) for v in range(len(sv.schema))]]:
             assert eval_device(sv, rows, vals) == sv.evaluate(vals), s
+
+
+def test_forwarding_keeps_the_write_back_of_a_result_read_again():
+    """Pass 5 on a hand-built chain: r = x*y is forwarded into s = r - x and read again by
+    u = s + r, so the MUL keeps its write-back while the SUB (read only by the next
+    instruction) skips it; a result read as both operands of the next instruction is
+    forwarded on both sides."""
+    from mythril_amd.lower import Dag, lower
+
+    dag = Dag()
+    x, y, z = dag.var("x", 256), dag.var("y", 256), dag.var("z", 256)
+    r = dag.op(ir.W_MUL, 256, x, y)
+    s = dag.op(ir.W_SUB, 256, r, x)
+    u = dag.op(ir.W_ADD, 256, s, r)
+    v = dag.op(ir.W_XOR, 256, u, u)
+    dag.assert_(dag.op(ir.B_ULT, 256, v, z))
+    batch = ir.Batch([lower(dag)])
+    code, descs = device_program(batch)
+    rows = code[descs[0][0]:descs[0][0] + descs[0][1]]
+    ops = [int(w0) & 0xFF for w0 in rows[:, 0]]
+    w0 = {op: int(rows[ops.index(op), 0]) for op in (ir.W_MUL, ir.W_SUB, ir.W_ADD, ir.W_XOR)}
+    assert w0[ir.W_MUL] & TR_WW                       # r is read again by the ADD
+    assert w0[ir.W_SUB] & I_FA                        # r forwarded into the SUB ...
+    assert not (w0[ir.W_SUB] & TR_WW)                 # ... whose result only the ADD reads
+    assert w0[ir.W_ADD] & (I_FA | I_FB)
+    assert w0[ir.W_XOR] & I_FA and w0[ir.W_XOR] & I_FB   # u ^ u: both operands forwarded
+    sv = O.SetView.from_batch(batch, 0)
+    rng = random.Random(5)
+    rows_t = [tuple(int(q) for q in row) for row in rows]
+    for _ in range(64):
+        vals = [rng.getrandbits(256) for _ in range(3)]
+        assert eval_device(sv, rows_t, vals) == sv.evaluate(vals)
