@@ -398,18 +398,46 @@ def pmc_traffic(args):
     return d, os.path.relpath(files[-1], os.path.dirname(os.path.abspath(__file__)))
 
 
+# Issue cost of a wave64 VALU instruction by class, SIMD cycles at 4 waves/SIMD (the check
+# kernel's occupancy), 16 independent instructions per wave (tools/movbench.hip,
+# profiles/r04c_movbench.log, normalised at 2.4 GHz like the kernel time below): a simple
+# 32-bit op (v_add_u32 2.95, v_mov 3.09, v_xor 2.89) costs ~3, not the 2 of the nominal
+# issue rate; v_mad_u64_u32 5.13; f64 fma / cvt ~4.97 (v_mul_f64); v_rcp_f64 17.47.
+VALU_COST_4W = {"simple": 2.95, "int64": 5.13, "fma_f64": 4.97, "cvt": 4.97, "trans_f64": 17.47}
+
+
 def valu_view(pmc, kernel_s):
     """Hardware side of the roofline from the PMC summary: wave-level VALU instructions per
     launch (SQ_INSTS_VALU) over the SIMDs' VALU issue slots (a wave64 VALU instruction
     occupies its SIMD for 2 cycles; 1024 SIMDs, MI355X_MICROARCH.md "Wave scheduling"), at
     the effective clock of the PMC run (GRBM_GUI_ACTIVE / 8 XCDs) and, for reference, at
-    2.4 GHz over the live kernel time.  The empty slots are latency the resident waves do not
-    hide (dependent chains, scalar dispatch, waits); no instruction is priced above 2 cycles."""
+    2.4 GHz over the live kernel time.
+
+    ``issue_frac_at_measured_rates`` prices the same instruction mix at the costs the
+    microbenchmark measures for each class at 4 waves/SIMD (VALU_COST_4W: INT64 and the f64
+    classes from their own PMC counters, every other VALU instruction at the simple-op cost —
+    a lower bound, since carry chains, v_cndmask_e64 and 3-source ops cost 4.7-5.0) over
+    1024 SIMDs x 2.4 GHz x the live kernel time.  At ~1 the SIMDs are issue-saturated by
+    this mix: only fewer or cheaper instructions make the kernel faster."""
     if not pmc or "sq" not in pmc:
         return None
     v = pmc["sq"]["SQ_INSTS_VALU"]
     out = {"valu_instr_per_launch": v, "int64_instr_per_launch": pmc["sq"].get("SQ_INSTS_VALU_INT64"),
            "issue_frac_at_2400MHz": 2.0 * v / (1024 * 2.4e9 * kernel_s)}
+    # the PMC workload is the default config (pmc_traffic): 1024 sets x 65,536 candidates =
+    # 2^20 wave-level evaluations of a 64-candidate group
+    out["valu_instr_per_eval_group"] = v / (1024 * 65536 / 64)
+    f64 = pmc.get("f64") or {}
+    i64 = pmc["sq"].get("SQ_INSTS_VALU_INT64")
+    if i64 is not None and f64:
+        fma = f64.get("SQ_INSTS_VALU_FMA_F64", 0.0) + f64.get("SQ_INSTS_VALU_MUL_F64", 0.0) + \
+            f64.get("SQ_INSTS_VALU_ADD_F64", 0.0)
+        cvt, trans = f64.get("SQ_INSTS_VALU_CVT", 0.0), f64.get("SQ_INSTS_VALU_TRANS_F64", 0.0)
+        rest = max(0.0, v - i64 - fma - cvt - trans)
+        cyc = (rest * VALU_COST_4W["simple"] + i64 * VALU_COST_4W["int64"] + fma * VALU_COST_4W["fma_f64"] +
+               cvt * VALU_COST_4W["cvt"] + trans * VALU_COST_4W["trans_f64"])
+        out["issue_frac_at_measured_rates"] = cyc / (1024 * 2.4e9 * kernel_s)
+        out["measured_rates"] = dict(VALU_COST_4W, source="profiles/r04c_movbench.log (4 waves/SIMD)")
     clk = pmc.get("clk")
     if clk and clk.get("GRBM_GUI_ACTIVE"):
         cyc = clk["GRBM_GUI_ACTIVE"] / 8.0

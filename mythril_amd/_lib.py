@@ -82,6 +82,9 @@ SIGNATURES = {
 _lib = None
 _lib_lock = threading.Lock()
 _initialised: set = set()
+# context ids per device tuple handed to pf_init_contexts: an engine built again over the same
+# tuple reuses them instead of adding streams, events and a device pool per build
+_contexts: dict = {}
 
 
 def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
@@ -151,12 +154,16 @@ def init_contexts(devices) -> list:
     device indices wherever the engine names a device."""
     devs = [int(d) for d in devices]
     L = lib()
+    key = tuple(devs)
+    if key in _contexts:
+        return list(_contexts[key])
     n = L.pf_device_count()
     if n <= 0:
         raise PathFeasError("no HIP device visible: the MI355X path-feasibility engine has no CPU fallback")
     arr = (ctypes.c_int32 * len(devs))(*devs)
     out = (ctypes.c_int32 * len(devs))()
     check(L.pf_init_contexts(arr, len(devs), out), f"pf_init_contexts({devs})")
+    _contexts[key] = tuple(out)
     return list(out)
 
 

@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -46,7 +47,12 @@ struct Dev {
     // per buffer were a millisecond of the single-query latency
     std::vector<std::pair<void*, size_t>> pool;
 };
-std::vector<Dev> g_devs;  // ascending device ids
+// ascending keys.  The entries are heap objects that stay put until pf_shutdown, so a Dev*
+// taken by pf_batch_create (which runs without g_mu) survives a concurrent pf_init /
+// pf_init_contexts growing and re-sorting the vector; the vector itself is read and changed
+// under g_devs_mu (and changed only while g_mu is held too, so readers under g_mu need no more).
+std::vector<std::unique_ptr<Dev>> g_devs;
+std::mutex g_devs_mu;
 int g_default = -1;       // index in g_devs of the default device (lowest id)
 // search-kernel waves launched per CU (PF_WAVES_PER_CU overrides both).  Measured on config 3
 // (1024 sets x 65,536 candidates, profiles/r01_wavesweep.md): with the longest-first set order
@@ -128,7 +134,7 @@ struct DevBuf {
 
 Dev* find_dev(int key) {
     for (auto& d : g_devs)
-        if (d.key == key) return &d;
+        if (d->key == key) return d.get();
     return nullptr;
 }
 
@@ -193,7 +199,7 @@ Dev* use_dev(int device) {
         fail("pf_init() has not been called");
         return nullptr;
     }
-    Dev* D = device < 0 ? &g_devs[g_default] : find_dev(device);
+    Dev* D = device < 0 ? g_devs[g_default].get() : find_dev(device);
     if (!D) {
         fail("device %d was not initialised by pf_init", device);
         return nullptr;
@@ -699,13 +705,8 @@ int pf_device_count(void) {
     return n;
 }
 
-int pf_init(uint64_t device_mask) {
-    std::lock_guard<std::mutex> lk(g_mu);
-    int n = 0;
-    HIPCHK(hipGetDeviceCount(&n));
-    if (device_mask == 0) return fail("pf_init: empty device mask");
-    if (n < 64 && (device_mask >> n)) return fail("pf_init: mask %llx names devices beyond the %d visible",
-                                                  (unsigned long long)device_mask, n);
+// launch-geometry knobs from the environment, read by both initialisers
+void read_env_knobs() {
     if (const char* e = getenv("PF_WAVES_PER_CU")) {
         long v = strtol(e, nullptr, 10);
         if (v >= 8 && v <= 4096) g_waves_per_cu_full = g_waves_per_cu_early = (uint32_t)v;
@@ -722,24 +723,44 @@ int pf_init(uint64_t device_mask) {
         long v = strtol(e, nullptr, 10);
         if (v >= 1 && v <= 1024) g_early_chunk_groups = (uint32_t)v;
     }
+}
+
+// one more execution context (device id, API key) with its streams and events; called under
+// g_mu, inserts under g_devs_mu keeping the keys ascending
+int add_dev(int id, int key, const char* who) {
+    HIPCHK(hipSetDevice(id));
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, id));
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail("%s: device %d is %s, this build targets gfx950", who, id, prop.gcnArchName);
+    std::unique_ptr<Dev> D(new Dev());
+    D->id = id;
+    D->key = key;
+    D->num_cus = prop.multiProcessorCount;
+    HIPCHK(hipStreamCreateWithFlags(&D->stream, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&D->up_stream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreate(&D->ev0));
+    HIPCHK(hipEventCreate(&D->ev1));
+    std::lock_guard<std::mutex> dk(g_devs_mu);
+    auto at = std::upper_bound(g_devs.begin(), g_devs.end(), key,
+                               [](int k, const std::unique_ptr<Dev>& e) { return k < e->key; });
+    g_devs.insert(at, std::move(D));
+    g_default = 0;
+    return 0;
+}
+
+int pf_init(uint64_t device_mask) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    int n = 0;
+    HIPCHK(hipGetDeviceCount(&n));
+    if (device_mask == 0) return fail("pf_init: empty device mask");
+    if (n < 64 && (device_mask >> n)) return fail("pf_init: mask %llx names devices beyond the %d visible",
+                                                  (unsigned long long)device_mask, n);
+    read_env_knobs();
     for (int id = 0; id < n && id < 64; ++id) {
         if (!((device_mask >> id) & 1ull) || find_dev(id)) continue;
-        HIPCHK(hipSetDevice(id));
-        hipDeviceProp_t prop;
-        HIPCHK(hipGetDeviceProperties(&prop, id));
-        if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
-            return fail("pf_init: device %d is %s, this build targets gfx950", id, prop.gcnArchName);
-        Dev D;
-        D.id = D.key = id;
-        D.num_cus = prop.multiProcessorCount;
-        HIPCHK(hipStreamCreateWithFlags(&D.stream, hipStreamNonBlocking));
-        HIPCHK(hipStreamCreateWithFlags(&D.up_stream, hipStreamNonBlocking));
-        HIPCHK(hipEventCreate(&D.ev0));
-        HIPCHK(hipEventCreate(&D.ev1));
-        g_devs.push_back(D);
+        if (add_dev(id, id, "pf_init")) return -1;
     }
-    std::sort(g_devs.begin(), g_devs.end(), [](const Dev& a, const Dev& b) { return a.key < b.key; });
-    g_default = 0;
     return 0;
 }
 
@@ -748,46 +769,33 @@ int pf_init_contexts(const int32_t* devices, size_t n, int32_t* ctx_out) {
     int nd = 0;
     HIPCHK(hipGetDeviceCount(&nd));
     if (!devices || !ctx_out || n == 0) return fail("pf_init_contexts: no devices");
+    read_env_knobs();
     int next = PF_CONTEXT_BASE;
-    for (const Dev& D : g_devs) next = std::max(next, D.key + 1);
+    for (const auto& D : g_devs) next = std::max(next, D->key + 1);
     for (size_t i = 0; i < n; ++i) {
         const int id = devices[i];
         if (id < 0 || id >= nd) return fail("pf_init_contexts: device %d of %d visible", id, nd);
-        HIPCHK(hipSetDevice(id));
-        hipDeviceProp_t prop;
-        HIPCHK(hipGetDeviceProperties(&prop, id));
-        if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
-            return fail("pf_init_contexts: device %d is %s, this build targets gfx950", id, prop.gcnArchName);
-        Dev D;
-        D.id = id;
-        D.key = next++;
-        D.num_cus = prop.multiProcessorCount;
-        HIPCHK(hipStreamCreateWithFlags(&D.stream, hipStreamNonBlocking));
-        HIPCHK(hipStreamCreateWithFlags(&D.up_stream, hipStreamNonBlocking));
-        HIPCHK(hipEventCreate(&D.ev0));
-        HIPCHK(hipEventCreate(&D.ev1));
-        g_devs.push_back(D);
-        ctx_out[i] = D.key;
+        if (add_dev(id, next, "pf_init_contexts")) return -1;
+        ctx_out[i] = next++;
     }
-    std::sort(g_devs.begin(), g_devs.end(), [](const Dev& a, const Dev& b) { return a.key < b.key; });
-    g_default = 0;
     return 0;
 }
 
 int pf_shutdown(void) {
     std::lock_guard<std::mutex> lk(g_mu);
+    std::lock_guard<std::mutex> dk(g_devs_mu);
     for (auto& D : g_devs) {
-        hipSetDevice(D.id);
+        hipSetDevice(D->id);
         hipDeviceSynchronize();
         {
             std::lock_guard<std::mutex> pk(g_pool_mu);
-            for (auto& b : D.pool) hipFree(b.first);
-            D.pool.clear();
+            for (auto& b : D->pool) hipFree(b.first);
+            D->pool.clear();
         }
-        hipEventDestroy(D.ev0);
-        hipEventDestroy(D.ev1);
-        hipStreamDestroy(D.stream);
-        if (D.up_stream) hipStreamDestroy(D.up_stream);
+        hipEventDestroy(D->ev0);
+        hipEventDestroy(D->ev1);
+        hipStreamDestroy(D->stream);
+        if (D->up_stream) hipStreamDestroy(D->up_stream);
     }
     g_devs.clear();
     g_default = -1;
@@ -952,8 +960,9 @@ int pf_batch_create_on(int device, const uint32_t* code, size_t n_ins, const uin
         put(o_order, order.data(), n_sets * 4);
     };
 
-    // No g_mu from here on either: the device lookup reads g_devs (fixed after pf_init), the
-    // block comes from the pool under its own lock, errors go through t_err.
+    // No g_mu from here on either: the device lookup holds g_devs_mu (pf_init and
+    // pf_init_contexts insert under it; the Dev objects themselves never move), the block comes
+    // from the pool under its own lock, errors go through t_err.
     Batch* B = nullptr;
     int dev_id = -1;
     hipStream_t ups = nullptr;
@@ -965,7 +974,11 @@ int pf_batch_create_on(int device, const uint32_t* code, size_t n_ins, const uin
     };
     t_defer_err = true;
     {
-        Dev* Dv = use_dev(device);
+        Dev* Dv = nullptr;
+        {
+            std::lock_guard<std::mutex> dk(g_devs_mu);
+            Dv = use_dev(device);
+        }
         if (!Dv) return report(-1);
         if (!handle_out) return report(fail("pf_batch_create: null handle_out"));
         B = new Batch();

@@ -259,25 +259,21 @@ def _lookup_batch(terms: List[T.Term]):
     return None
 
 
-_GPU_OPTIMIZE = None
+_GPU_CLASSES = None
 
 
-def gpu_optimize_class():
-    """The drop-in subclass of ``mythril.laser.smt.Optimize`` (needs Mythril + z3); built
-    once per process.
-
-    Query accounting: ``check`` carries Mythril's own ``@stat_smt_query``
-    (solver_statistics.py:7-25), exactly as ``BaseSolver.check`` does (solver.py:72), so
-    every query — GPU-answered or sent to z3 — bumps ``SolverStatistics().query_count`` and
-    ``solver_time`` once; the z3 fallback runs ``BaseSolver.check``'s body (``_z3_check``)
-    rather than the decorated ``super().check()``, which would count the query twice.
-    ``gpu_sat`` / ``gpu_attempts`` are kept beside them (mythril_amd.smt.solver), so
-    "% discharged" = ``gpu_sat / query_count`` (:func:`discharge_ratio`)."""
-    global _GPU_OPTIMIZE
+def _gpu_solver_classes():
+    """(GpuOptimize, GpuSolver): the drop-in subclasses of ``mythril.laser.smt.Optimize`` and
+    ``mythril.laser.smt.Solver`` (need Mythril + z3), built once per Mythril binding.  Both
+    take the GPU path in the same ``check`` (:class:`_GpuCheck` below); ``GpuOptimize`` adds
+    the objective bookkeeping (a query with objectives always goes to z3)."""
+    global _GPU_CLASSES
     from mythril.laser.smt import Optimize as MythrilOptimize
+    from mythril.laser.smt import Solver as MythrilSolver
 
-    if _GPU_OPTIMIZE is not None and _GPU_OPTIMIZE.__bases__[0] is MythrilOptimize:
-        return _GPU_OPTIMIZE
+    if (_GPU_CLASSES is not None and _GPU_CLASSES[0].__bases__[1] is MythrilOptimize
+            and _GPU_CLASSES[1].__bases__[1] is MythrilSolver):
+        return _GPU_CLASSES
     import z3
     from mythril.laser.ethereum.function_managers import keccak_function_manager
     from mythril.laser.smt.model import Model
@@ -287,7 +283,16 @@ def gpu_optimize_class():
     from .smt.solver import SolverStatistics
     from .z3_terms import converter
 
-    class GpuOptimize(MythrilOptimize):
+    class _GpuCheck:
+        """The shared GPU path.  Query accounting: ``check`` carries Mythril's
+        own ``@stat_smt_query`` (solver_statistics.py:7-25), exactly as ``BaseSolver.check``
+        does (solver.py:72), so every query — GPU-answered or sent to z3 — bumps
+        ``SolverStatistics().query_count`` and ``solver_time`` once; the z3 fallback runs
+        ``BaseSolver.check``'s body (``_z3_check``) rather than the decorated
+        ``super().check()``, which would count the query twice.  ``gpu_sat`` /
+        ``gpu_attempts`` are kept beside them (mythril_amd.smt.solver), so "% discharged" =
+        ``gpu_sat / query_count`` (:func:`discharge_ratio`)."""
+
         def __init__(self):
             super().__init__()
             self._objectives = False
@@ -297,14 +302,6 @@ def gpu_optimize_class():
         def set_timeout(self, timeout: int) -> None:
             self._timeout_ms = timeout
             super().set_timeout(timeout)
-
-        def minimize(self, element):
-            self._objectives = True
-            super().minimize(element)
-
-        def maximize(self, element):
-            self._objectives = True
-            super().maximize(element)
 
         @stat_smt_query
         def check(self, *args):
@@ -355,8 +352,68 @@ def gpu_optimize_class():
                 return self._gpu_model
             return super().model()
 
-    _GPU_OPTIMIZE = GpuOptimize
-    return GpuOptimize
+    class GpuOptimize(_GpuCheck, MythrilOptimize):
+        """The funnel's solver (support/model.py:37): objective-free queries to the GPU."""
+
+        def minimize(self, element):
+            self._objectives = True
+            super().minimize(element)
+
+        def maximize(self, element):
+            self._objectives = True
+            super().maximize(element)
+
+    class GpuSolver(_GpuCheck, MythrilSolver):
+        """``Solver()`` built outside the funnel (calldata.py:78, summary.py:114,
+        summary/core.py:223): the same GPU path; ``reset`` / ``pop`` act on the z3 solver,
+        whose assertions each ``check`` converts afresh."""
+
+    _GPU_CLASSES = (GpuOptimize, GpuSolver)
+    return _GPU_CLASSES
+
+
+def gpu_optimize_class():
+    """The drop-in subclass of ``mythril.laser.smt.Optimize`` (see :func:`_gpu_solver_classes`)."""
+    return _gpu_solver_classes()[0]
+
+
+def gpu_solver_class():
+    """The drop-in subclass of ``mythril.laser.smt.Solver`` (see :func:`_gpu_solver_classes`)."""
+    return _gpu_solver_classes()[1]
+
+
+# Modules that build ``mythril.laser.smt.Solver`` directly, bound by value at their import
+# (``from mythril.laser.smt import Solver``), so each needs its own rebinding: the symbolic
+# calldata slice loop (laser/ethereum/state/calldata.py:16,78 — one query per byte, SAT on
+# every iteration but the last) and the summary plugin's checks (plugins/summary/summary.py:8,
+# 114; summary/core.py:30,223).
+SOLVER_SITES = ("mythril.laser.ethereum.state.calldata",
+                "mythril.laser.plugin.plugins.summary.summary",
+                "mythril.laser.plugin.plugins.summary.core")
+
+
+def _rebind_solver_sites() -> List[str]:
+    """Point every ``SOLVER_SITES`` module's ``Solver`` at ``GpuSolver``; a module not yet
+    loaded is imported first (so a later import finds it rebound), one that cannot be
+    imported is skipped.  Returns the modules rebound."""
+    import importlib
+
+    from mythril.laser.smt import Solver as MythrilSolver
+
+    gpu_solver = gpu_solver_class()
+    done = []
+    for name in SOLVER_SITES:
+        mod = sys.modules.get(name)
+        if mod is None:
+            try:
+                mod = importlib.import_module(name)
+            except Exception as e:  # noqa: BLE001 - an optional Mythril module
+                log.debug("Solver site %s not rebound: %s", name, e)
+                continue
+        if getattr(mod, "Solver", None) in (MythrilSolver, gpu_solver):
+            mod.Solver = gpu_solver
+            done.append(name)
+    return done
 
 
 def _note_z3_model(z3, raw) -> None:
@@ -394,7 +451,8 @@ def discharge_ratio() -> Optional[float]:
 
 
 def install() -> None:
-    """Rebind the funnel's Optimize (support/model.py:13 binds it by value at import), its
+    """Rebind the funnel's Optimize (support/model.py:13 binds it by value at import), the
+    ``Solver`` of the modules that query outside the funnel (:data:`SOLVER_SITES`), its
     ``model_cache`` (support/model.py:20; ``PF_MODEL_CACHE=0`` keeps the reference's) and the
     report's keccak concretisation (``mythril.analysis.solver._replace_with_actual_sha``).  The
     analysis process does not use torch, so the engine is loaded without it (PF_TORCH=0,
@@ -411,6 +469,7 @@ def install() -> None:
         os.environ.setdefault("PF_DEVICES", "all")
 
     funnel.Optimize = gpu_optimize_class()
+    _rebind_solver_sites()
     try:
         # keccak concretisation of reported transaction sequences (analysis/solver.py:129-165,
         # resolved at call time by get_transaction_sequence): batched, GPU for large batches

@@ -870,24 +870,29 @@ class NativeWitness:
 # leaf slots: a dense number per term read through witness_values_many, under which each
 # native witness keeps the value (33 bytes per slot per witness: at most ~0.5 MB each, ~50 MB
 # for a full 100-model cache); renumbered (new epoch) when the table grows past _SLOTS_MAX
+# The table is process-wide while the callers hold only their own store's lock, so it has a
+# lock of its own, and the epoch is returned with the slots from the same snapshot: a caller
+# that renumbers (new epoch) cannot hand another caller its epoch for older slot numbers.
 _SLOTS: Dict[T.Term, int] = {}
 _SLOT_EPOCH = [1]
 _SLOTS_MAX = 1 << 14
+_SLOTS_LOCK = threading.Lock()
 
 
-def _slots_of(terms: List[T.Term]) -> Tuple[np.ndarray, int]:
-    """(slots, how many of them are new)."""
-    if len(_SLOTS) + len(terms) > _SLOTS_MAX:
-        _SLOTS.clear()
-        _SLOT_EPOCH[0] += 1
-    out = np.empty(len(terms), dtype=np.uint32)
-    n0 = len(_SLOTS)
-    for i, t in enumerate(terms):
-        s = _SLOTS.get(t)
-        if s is None:
-            s = _SLOTS[t] = len(_SLOTS)
-        out[i] = s
-    return out, len(_SLOTS) - n0
+def _slots_of(terms: List[T.Term]) -> Tuple[np.ndarray, int, int]:
+    """(slots, how many of them are new, the epoch they belong to)."""
+    with _SLOTS_LOCK:
+        if len(_SLOTS) + len(terms) > _SLOTS_MAX:
+            _SLOTS.clear()
+            _SLOT_EPOCH[0] += 1
+        out = np.empty(len(terms), dtype=np.uint32)
+        n0 = len(_SLOTS)
+        for i, t in enumerate(terms):
+            s = _SLOTS.get(t)
+            if s is None:
+                s = _SLOTS[t] = len(_SLOTS)
+            out[i] = s
+        return out, len(_SLOTS) - n0, _SLOT_EPOCH[0]
 
 
 def witness_values_many(ws: List[NativeWitness], terms: List[T.Term], reg: UFRegistry, threads: int = 1):
@@ -903,11 +908,11 @@ def witness_values_many(ws: List[NativeWitness], terms: List[T.Term], reg: UFReg
     hs = (ctypes.c_void_p * n)(*[w.h for w in ws])
     with st.lock:
         ids = np.array([st.export(t) for t in terms], dtype=np.uint32)
-        slots, fresh = _slots_of(terms)
+        slots, fresh, epoch = _slots_of(terms)
         if not fresh:
             # every term was read before: mostly 32-byte copies, cheaper than waking the pool
             threads = 1
-        st.L.pflt_witness_values(hs, n, ids.ctypes.data_as(_u32p), k, slots.ctypes.data_as(_u32p), _SLOT_EPOCH[0],
+        st.L.pflt_witness_values(hs, n, ids.ctypes.data_as(_u32p), k, slots.ctypes.data_as(_u32p), epoch,
                                  blob.ctypes.data_as(_u32p), len(blob),
                                  serial, max(1, threads), out.ctypes.data_as(_u32p),
                                  ok.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))

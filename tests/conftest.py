@@ -13,6 +13,13 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (run on the GPU box)")
+    config.addinivalue_line("markers", "first: run before every other test of the session "
+                                       "(the RCCL test initialises torch.distributed before any "
+                                       "other GPU work of the process)")
+
+
+def pytest_collection_modifyitems(config, items):
+    items.sort(key=lambda it: 0 if it.get_closest_marker("first") else 1)
 
 
 @pytest.fixture(scope="session")

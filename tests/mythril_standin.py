@@ -1,46 +1,56 @@
-"""Stand-ins for the Mythril modules the engine's seams touch (Mythril is not importable in
-this image: z3, eth_abi and eth_hash are missing — SURVEY.md §8c).
+"""A test harness in the shape of the Mythril modules the engine's seams touch (Mythril itself
+is not importable in this image: z3, eth_abi and eth_hash are missing — SURVEY.md §8c).
 
-Each piece restates the reference module it stands for LINE FOR LINE where the engine's code
-meets it (class bases, ``__init__`` signatures, decorators, the loader's construction
-sequence), so the drop-in ``Optimize``, the witness model and the plugin run inside exactly
-the control flow a real analysis gives them.  A stand-in that simplifies the reference at a
-seam hides the very bugs these tests exist to find (round-2 review: a ``check`` without
-``@stat_smt_query``, a ``MythrilPlugin`` without ``__init__(**kwargs)``).
+What the harness keeps from Mythril is the *interface contract* at each seam, not Mythril's
+code: the module names the drop-in rebinds, the class bases it subclasses, the constructor
+signatures, which names are resolved at call time and which are bound at import, the call
+order of the query funnel, the LRU semantics of the model cache and the plugin construction
+sequence.  Every piece below is written from that contract; the behaviour each one must have
+is pinned by ``tests/test_standin_contract.py`` with the reference line it follows.
 
-* ``mythril.support.support_utils`` — ``Singleton`` (support_utils.py:15-34), ``LRUCache``,
-  ``ModelCache.check_quick_sat`` (:35-71: deep copy + ``eval(..., model_completion=True)``);
-* ``mythril.laser.smt.solver.solver_statistics`` — ``stat_smt_query`` / ``SolverStatistics``
-  (solver_statistics.py:7-42);
-* ``mythril.laser.smt`` — ``BaseSolver``/``Solver``/``Optimize`` over ``z3.Optimize`` with the
-  decorated ``check`` that silences stdout and maps a ``Z3Exception`` to ``unknown``
-  (solver/solver.py:20-143), ``Model`` (model.py:6-59), ``Bool``, ``And``, ``simplify``;
-* ``mythril.support.model`` — ``solver_worker`` / ``get_model`` (support/model.py:23-125),
-  including the ``except Exception`` -> ``unknown`` around the worker's result;
-* ``Constraints.is_possible`` (constraints.py:31-46), ``WorldState.constraints``
-  (world_state.py:39), the keccak manager singleton;
-* the plugin stack: ``LaserPlugin`` (laser/plugin/interface.py), ``PluginBuilder``
-  (laser/plugin/builder.py:6-21), ``MythrilPlugin`` / ``MythrilLaserPlugin``
-  (plugin/interface.py:6-46), ``LaserPluginLoader`` (laser/plugin/loader.py:12-75),
-  ``PluginDiscovery`` (plugin/discovery.py:11-73; the installed entry points are injected,
-  since nothing is pip-installed here) and ``MythrilPluginLoader`` (plugin/loader.py:19-79).
+Seams (reference file:line of the contract):
+
+* ``mythril.support.support_utils`` — a per-class singleton metaclass (support_utils.py:15-25),
+  the size-100 LRU of cached models and ``ModelCache.check_quick_sat`` (:35-71: newest model
+  first, evaluated on a private deep copy with ``model_completion=True``, the hit bumped,
+  memoised by ``functools.lru_cache(2**10)``);
+* ``mythril.laser.smt.solver.solver_statistics`` — ``stat_smt_query`` counts one query and its
+  time while statistics are enabled (solver_statistics.py:7-25);
+* ``mythril.laser.smt`` — ``BaseSolver``/``Solver``/``Optimize`` over the z3 objects, ``check``
+  decorated, stdout silenced, a ``Z3Exception`` reported as ``unknown``
+  (solver/solver.py:20-143); ``Model`` over a list of z3 models (model.py:6-59); the ``Bool``
+  / ``BitVec`` wrappers and ``symbol_factory`` the call sites use;
+* ``mythril.support.model`` — ``get_model`` / ``solver_worker`` (support/model.py:23-125):
+  quick-sat first for objective-free queries, then a ``ThreadPool(1)`` worker that builds
+  ``Optimize()`` through the module global, a timeout or any worker error is ``unknown``;
+* ``Constraints.is_possible`` (constraints.py:31-46) and ``WorldState.constraints``;
+* the ``Solver()`` call sites outside the funnel: the calldata slice loop
+  (laser/ethereum/state/calldata.py:64-93, one query per byte) and the summary plugin's
+  condition checks (plugins/summary/summary.py:114-117, summary/core.py:222-227) — each module
+  binds ``Solver`` at import, which is what ``install()`` rebinds;
+* the plugin stack: ``LaserPlugin``, ``PluginBuilder`` (laser/plugin/builder.py:6-21),
+  ``MythrilPlugin`` / ``MythrilLaserPlugin`` (plugin/interface.py:6-46), ``LaserPluginLoader``
+  (laser/plugin/loader.py:12-75), ``PluginDiscovery`` (plugin/discovery.py:11-73, the installed
+  entry points injected) and ``MythrilPluginLoader`` (plugin/loader.py:19-79);
+* the report's keccak concretisation step (analysis/solver.py:96-99 -> :129-165).
 
 Test infrastructure only.
 """
 
 from __future__ import annotations
 
+import contextlib
+import functools
+import itertools
 import os
 import sys
+import time
 import types
 from abc import ABC, abstractmethod
 from collections import OrderedDict
 from copy import deepcopy
-from functools import lru_cache
-from multiprocessing import TimeoutError
+from multiprocessing import TimeoutError as PoolTimeout
 from multiprocessing.pool import ThreadPool
-from time import time
-from typing import Dict
 
 MODULES = (
     "mythril", "mythril.exceptions", "mythril.laser", "mythril.laser.smt",
@@ -48,10 +58,13 @@ MODULES = (
     "mythril.laser.smt.solver.solver_statistics", "mythril.support", "mythril.support.model",
     "mythril.support.support_utils", "mythril.laser.ethereum",
     "mythril.laser.ethereum.function_managers", "mythril.laser.ethereum.state",
-    "mythril.laser.ethereum.state.constraints", "mythril.laser.plugin",
-    "mythril.laser.plugin.builder", "mythril.laser.plugin.interface",
-    "mythril.laser.plugin.loader", "mythril.plugin", "mythril.plugin.interface",
-    "mythril.plugin.discovery", "mythril.plugin.loader", "mythril.analysis", "mythril.analysis.solver")
+    "mythril.laser.ethereum.state.constraints", "mythril.laser.ethereum.state.calldata",
+    "mythril.laser.plugin", "mythril.laser.plugin.builder", "mythril.laser.plugin.interface",
+    "mythril.laser.plugin.loader", "mythril.laser.plugin.plugins",
+    "mythril.laser.plugin.plugins.summary", "mythril.laser.plugin.plugins.summary.summary",
+    "mythril.laser.plugin.plugins.summary.core", "mythril.plugin", "mythril.plugin.interface",
+    "mythril.plugin.discovery", "mythril.plugin.loader", "mythril.analysis",
+    "mythril.analysis.solver")
 
 
 def host_sha3(value):
@@ -61,67 +74,72 @@ def host_sha3(value):
     return pyoracle.keccak256(bytes(value))
 
 
-def build(z3, installed_plugins=None):
-    """Module objects keyed by their Mythril names, bound to the given z3 module.
-    ``installed_plugins`` = {entry-point name: "module:attr"}, the ``"mythril.plugins"``
-    entry points ``PluginDiscovery`` loads (discovery.py:22-36) — nothing is pip-installed
-    here, so the test passes the value the package metadata declares (pyproject.toml)."""
-    mods = {n: types.ModuleType(n) for n in MODULES}
+@contextlib.contextmanager
+def _stdout_silenced():
+    """The solver's stdout guard: libz3 may print while checking."""
+    saved = sys.stdout
+    with open(os.devnull, "w") as sink:
+        sys.stdout = sink
+        try:
+            yield
+        finally:
+            sys.stdout = saved
 
-    # ---- support_utils.py:15-34 -----------------------------------------------------------
+
+# ---- singletons, statistics ----------------------------------------------------------------
+
+def _singleton_meta():
+    """A fresh per-class singleton metaclass: ``Cls()`` builds the instance once and hands
+    the same object back ever after, whatever arguments later calls pass."""
+    registry = {}
+
     class Singleton(type):
-        _instances: Dict = {}
+        _instances = registry
 
         def __call__(cls, *args, **kwargs):
-            if cls not in cls._instances:
-                cls._instances[cls] = super(Singleton, cls).__call__(*args, **kwargs)
-            return cls._instances[cls]
+            if cls not in registry:
+                registry[cls] = type.__call__(cls, *args, **kwargs)
+            return registry[cls]
 
-    mods["mythril.support.support_utils"].Singleton = Singleton
+    return Singleton
 
-    # ---- exceptions (mythril/exceptions.py:16-28) -------------------------------------
-    class UnsatError(Exception):
-        pass
 
-    class SolverTimeOutException(UnsatError):
-        pass
+def _statistics(Singleton):
+    class SolverStatistics(metaclass=Singleton):
+        """Query count and solver time, recorded only while ``enabled`` (the analyzer turns
+        it on, mythril_analyzer.py:147)."""
 
-    mods["mythril.exceptions"].UnsatError = UnsatError
-    mods["mythril.exceptions"].SolverTimeOutException = SolverTimeOutException
-
-    # ---- solver_statistics.py:7-42 --------------------------------------------------------
-    def stat_smt_query(func):
-        stat_store = SolverStatistics()
-
-        def function_wrapper(*args, **kwargs):
-            if not stat_store.enabled:
-                return func(*args, **kwargs)
-
-            stat_store.query_count += 1
-            begin = time()
-
-            result = func(*args, **kwargs)
-
-            end = time()
-            stat_store.solver_time += end - begin
-
-            return result
-
-        return function_wrapper
-
-    class SolverStatistics(object, metaclass=Singleton):
         def __init__(self):
             self.enabled = False
             self.query_count = 0
             self.solver_time = 0
 
         def __repr__(self):
-            return "Query count: {} \nSolver time: {}".format(self.query_count, self.solver_time)
+            return f"Query count: {self.query_count} \nSolver time: {self.solver_time}"
 
-    stats_mod = mods["mythril.laser.smt.solver.solver_statistics"]
-    stats_mod.stat_smt_query, stats_mod.SolverStatistics = stat_smt_query, SolverStatistics
+    def stat_smt_query(check):
+        @functools.wraps(check)
+        def counted(*args, **kwargs):
+            stats = SolverStatistics()
+            if not stats.enabled:
+                return check(*args, **kwargs)
+            stats.query_count += 1
+            started = time.time()
+            answer = check(*args, **kwargs)
+            stats.solver_time += time.time() - started
+            return answer
 
-    # ---- facade ------------------------------------------------------------------------
+        return counted
+
+    return SolverStatistics, stat_smt_query
+
+
+# ---- the smt facade --------------------------------------------------------------------------
+
+def _facade(z3, stat_smt_query):
+    def unwrap(x):
+        return x.raw if hasattr(x, "raw") else x
+
     class Bool:
         def __init__(self, raw):
             self.raw = raw
@@ -132,46 +150,85 @@ def build(z3, installed_plugins=None):
         def __hash__(self):
             return hash(self.raw)
 
+    class BitVec:
+        def __init__(self, raw):
+            self.raw = raw
+
+        def simplify(self):
+            self.raw = z3.simplify(self.raw)
+
+        @property
+        def symbolic(self):
+            return not z3.is_bv_value(self.raw)
+
+        @property
+        def value(self):
+            return self.raw.as_long() if z3.is_bv_value(self.raw) else None
+
+        def size(self):
+            return self.raw.size()
+
+        def __add__(self, other):
+            if isinstance(other, int):
+                other = z3.BitVecVal(other, self.raw.size())
+            return BitVec(self.raw + unwrap(other))
+
+        def __eq__(self, other):  # noqa: D105 - a constraint, like z3's
+            return Bool(self.raw == unwrap(other))
+
+        def __ne__(self, other):
+            return Bool(self.raw != unwrap(other))
+
+        def __hash__(self):
+            return hash(self.raw)
+
+    class SymbolFactory:
+        @staticmethod
+        def BitVecVal(value, size, annotations=None):
+            return BitVec(z3.BitVecVal(value, size))
+
+        @staticmethod
+        def BitVecSym(name, size, annotations=None):
+            return BitVec(z3.BitVec(name, size))
+
     def And(*args):
-        return Bool(z3.And([a.raw for a in args]))
+        return Bool(z3.And([unwrap(a) for a in args]))
 
     def simplify(expression):
         expression.simplify()
         return expression
 
-    # ---- model.py:6-59 -----------------------------------------------------------------------
     class Model:
+        """Several z3 models seen as one (``raw`` is the list)."""
+
         def __init__(self, models=None):
             self.raw = models or []
 
         def decls(self):
-            result = []
-            for internal_model in self.raw:
-                result.extend(internal_model.decls())
-            return result
+            return [d for internal in self.raw for d in internal.decls()]
 
         def __getitem__(self, item):
-            for internal_model in self.raw:
-                is_last_model = self.raw.index(internal_model) == len(self.raw) - 1
+            last = len(self.raw) - 1
+            for pos, internal in enumerate(self.raw):
                 try:
-                    result = internal_model[item]
-                    if result is not None:
-                        return result
+                    found = internal[item]
                 except IndexError:
-                    if is_last_model:
+                    if pos == last:
                         raise
                     continue
+                if found is not None:
+                    return found
             return None
 
         def eval(self, expression, model_completion=False):
-            for internal_model in self.raw:
-                is_last_model = self.raw.index(internal_model) == len(self.raw) - 1
-                is_relevant_model = expression.decl() in list(internal_model.decls())
-                if is_relevant_model or is_last_model:
-                    return internal_model.eval(expression, model_completion)
+            # the first model that declares the expression's head, else the last one
+            head = expression.decl()
+            last = len(self.raw) - 1
+            for pos, internal in enumerate(self.raw):
+                if pos == last or head in list(internal.decls()):
+                    return internal.eval(expression, model_completion)
             return None
 
-    # ---- solver/solver.py:20-143 ------------------------------------------------------------
     class BaseSolver:
         def __init__(self, raw):
             self.raw = raw
@@ -183,39 +240,35 @@ def build(z3, installed_plugins=None):
             self.raw.set(unsat_core=True)
 
         def add(self, *constraints):
-            z3_constraints = [c.raw for c in constraints]
-            self.raw.add(z3_constraints)
-
-        def assert_and_track(self, constraints, name):
-            self.raw.assert_and_track(constraints.raw, name)
+            self.raw.add([unwrap(c) for c in constraints])
 
         def append(self, *constraints):
-            self.add(*constraints)
+            return self.add(*constraints)   # through add, so an override sees appends too
+
+        def assert_and_track(self, constraints, name):
+            self.raw.assert_and_track(unwrap(constraints), name)
 
         @stat_smt_query
         def check(self, *args):
-            old_stdout = sys.stdout
-            with open(os.devnull, "w") as dev_null_fd:
-                sys.stdout = dev_null_fd
+            with _stdout_silenced():
                 try:
-                    evaluate = self.raw.check(args)
+                    return self.raw.check(args)
                 except z3.z3types.Z3Exception:
-                    evaluate = z3.unknown
-            sys.stdout = old_stdout
-            return evaluate
+                    return z3.unknown
 
         def model(self):
             try:
-                return Model([self.raw.model()])
+                inner = self.raw.model()
             except z3.z3types.Z3Exception:
                 return Model()
+            return Model([inner])
 
         def sexpr(self):
             return self.raw.sexpr()
 
     class Solver(BaseSolver):
         def __init__(self):
-            super().__init__(z3.Solver())
+            BaseSolver.__init__(self, z3.Solver())
 
         def reset(self):
             self.raw.reset()
@@ -225,58 +278,53 @@ def build(z3, installed_plugins=None):
 
     class Optimize(BaseSolver):
         def __init__(self):
-            super().__init__(z3.Optimize())
+            BaseSolver.__init__(self, z3.Optimize())
 
         def minimize(self, element):
-            self.raw.minimize(element.raw)
+            self.raw.minimize(unwrap(element))
 
         def maximize(self, element):
-            self.raw.maximize(element.raw)
+            self.raw.maximize(unwrap(element))
 
-    smt = mods["mythril.laser.smt"]
-    smt.Bool, smt.And, smt.simplify, smt.Optimize, smt.Solver = Bool, And, simplify, Optimize, Solver
-    smt.BaseSolver, smt.Model, smt.SolverStatistics = BaseSolver, Model, SolverStatistics
-    mods["mythril.laser.smt.model"].Model = Model
-    for name in ("mythril.laser.smt.solver", "mythril.laser.smt.solver.solver"):
-        mods[name].BaseSolver, mods[name].Solver, mods[name].Optimize = BaseSolver, Solver, Optimize
-    mods["mythril.laser.smt.solver"].SolverStatistics = SolverStatistics
+    return types.SimpleNamespace(Bool=Bool, BitVec=BitVec, symbol_factory=SymbolFactory(), And=And,
+                                 simplify=simplify, Model=Model, BaseSolver=BaseSolver, Solver=Solver,
+                                 Optimize=Optimize)
 
-    # ---- keccak manager singleton -----------------------------------------------------
-    kfm = types.SimpleNamespace(interval_hook_for_size={}, concrete_hashes={},
-                                create_conditions=lambda: Bool(z3.BoolVal(True)))
-    mods["mythril.laser.ethereum.function_managers"].keccak_function_manager = kfm
 
-    # ---- ModelCache (support_utils.py:35-71) -------------------------------------------
+# ---- model cache ------------------------------------------------------------------------------
+
+def _model_cache(z3):
     class LRUCache:
+        """``get`` -> value (the key becomes the newest) or -1; ``put`` -> the key becomes the
+        newest, the oldest key leaves when a new key would exceed ``size``."""
+
         def __init__(self, size):
             self.size = size
             self.lru_cache = OrderedDict()
 
         def get(self, key):
-            try:
-                value = self.lru_cache.pop(key)
-                self.lru_cache[key] = value
-                return value
-            except KeyError:
+            if key not in self.lru_cache:
                 return -1
+            self.lru_cache.move_to_end(key)
+            return self.lru_cache[key]
 
         def put(self, key, value):
-            try:
-                self.lru_cache.pop(key)
-            except KeyError:
-                if len(self.lru_cache) >= self.size:
-                    self.lru_cache.popitem(last=False)
+            if key in self.lru_cache:
+                self.lru_cache.move_to_end(key)
+            elif len(self.lru_cache) >= self.size:
+                self.lru_cache.popitem(last=False)
             self.lru_cache[key] = value
 
     class ModelCache:
         def __init__(self):
             self.model_cache = LRUCache(size=100)
 
-        @lru_cache(maxsize=2 ** 10)
+        @functools.lru_cache(maxsize=2 ** 10)
         def check_quick_sat(self, constraints):
-            for model in reversed(self.model_cache.lru_cache.keys()):
-                model_copy = deepcopy(model)
-                if z3.is_true(model_copy.eval(constraints, model_completion=True)):
+            newest_first = list(self.model_cache.lru_cache)[::-1]
+            for model in newest_first:
+                # completion adds interpretations to the model it runs on: a private copy
+                if z3.is_true(deepcopy(model).eval(constraints, model_completion=True)):
                     self.model_cache.put(model, self.model_cache.get(model) + 1)
                     return model
             return False
@@ -284,93 +332,159 @@ def build(z3, installed_plugins=None):
         def put(self, key, value):
             self.model_cache.put(key, value)
 
-    mods["mythril.support.support_utils"].LRUCache = LRUCache
-    mods["mythril.support.support_utils"].ModelCache = ModelCache
+    return LRUCache, ModelCache
 
-    # ---- the funnel (support/model.py:23-125) ------------------------------------------
-    funnel = mods["mythril.support.model"]
-    funnel.Optimize = Optimize
-    funnel.model_cache = ModelCache()
-    funnel.solver_timeout_default = 10000
 
+# ---- the query funnel ---------------------------------------------------------------------------
+
+def _funnel(z3, funnel, smt, UnsatError, SolverTimeOutException):
     def solver_worker(constraints, minimize=(), maximize=(), solver_timeout=None):
-        s = funnel.Optimize()  # resolved at call time: the name install() rebinds
-        s.set_timeout(solver_timeout)
-        for constraint in constraints:
-            s.add(constraint)
-        for e in minimize:
-            s.minimize(e)
-        for e in maximize:
-            s.maximize(e)
-        result = s.check()
-        return result, s
+        solver = funnel.Optimize()   # the module global, read per call: what install() rebinds
+        solver.set_timeout(solver_timeout)
+        solver.add(*constraints)
+        for kind, objectives in (("minimize", minimize), ("maximize", maximize)):
+            for objective in objectives:
+                getattr(solver, kind)(objective)
+        return solver.check(), solver
 
-    @lru_cache(maxsize=2 ** 23)
-    def get_model(constraints, minimize=(), maximize=(), solver_timeout=None):
-        solver_timeout = solver_timeout or funnel.solver_timeout_default
-        if solver_timeout <= 0:
-            raise SolverTimeOutException
-        for constraint in constraints:
-            if isinstance(constraint, bool) and not constraint:
-                raise UnsatError
-        if isinstance(constraints, tuple) is False:
-            constraints = constraints.get_all_constraints()
-        constraints = [c for c in constraints if isinstance(c, bool) is False]
-        if len(maximize) + len(minimize) == 0:
-            ret_model = funnel.model_cache.check_quick_sat(simplify(And(*constraints)).raw)
-            if ret_model:
-                return ret_model
+    def run_worker(constraints, minimize, maximize, timeout):
         pool = ThreadPool(1)
         try:
-            thread_result = pool.apply_async(
-                solver_worker, args=(constraints, minimize, maximize, solver_timeout))
+            pending = pool.apply_async(solver_worker, args=(constraints, minimize, maximize, timeout))
             try:
-                result, s = thread_result.get(solver_timeout)
-            except TimeoutError:
-                result = z3.unknown
-            except Exception:
-                result = z3.unknown
+                return pending.get(timeout)
+            except PoolTimeout:
+                return z3.unknown, None
+            except Exception:  # noqa: BLE001 - any worker failure reads as unknown
+                return z3.unknown, None
         finally:
             pool.terminate()
-        if result == z3.sat:
-            funnel.model_cache.model_cache.put(s.model(), 1)
-            return s.model()
-        elif result == z3.unknown:
+
+    @functools.lru_cache(maxsize=2 ** 23)
+    def get_model(constraints, minimize=(), maximize=(), solver_timeout=None):
+        timeout = solver_timeout or funnel.solver_timeout_default
+        if timeout <= 0:
             raise SolverTimeOutException
-        raise UnsatError
+        if any(isinstance(c, bool) and not c for c in constraints):
+            raise UnsatError
+        if not isinstance(constraints, tuple):
+            constraints = constraints.get_all_constraints()
+        smt_constraints = [c for c in constraints if not isinstance(c, bool)]
+        if not minimize and not maximize:
+            hit = funnel.model_cache.check_quick_sat(smt.simplify(smt.And(*smt_constraints)).raw)
+            if hit:
+                return hit
+        verdict, solver = run_worker(smt_constraints, minimize, maximize, timeout)
+        if verdict == z3.unknown:
+            raise SolverTimeOutException
+        if verdict != z3.sat:
+            raise UnsatError
+        # the cache receives one model() result and the caller another (two calls)
+        funnel.model_cache.model_cache.put(solver.model(), 1)
+        return solver.model()
 
-    funnel.solver_worker, funnel.get_model = solver_worker, get_model
+    return solver_worker, get_model
 
-    # ---- Constraints / WorldState --------------------------------------------------------
+
+def _state(funnel, kfm, UnsatError, SolverTimeOutException):
     class Constraints(list):
         def is_possible(self, solver_timeout=None):
             try:
                 funnel.get_model(self, solver_timeout=solver_timeout)
-            except SolverTimeOutException:
-                return solver_timeout is not None
-            except UnsatError:
-                return False
+            except UnsatError as e:
+                # a timeout (an UnsatError subclass) under a short custom timeout is "maybe"
+                return isinstance(e, SolverTimeOutException) and solver_timeout is not None
             return True
 
         def get_all_constraints(self):
-            return self[:] + [kfm.create_conditions()]
+            return list(self) + [kfm.create_conditions()]
 
         def __hash__(self):
-            return tuple(self[:]).__hash__()
+            return hash(tuple(self))
 
     class WorldState:
         def __init__(self, constraints=None):
             self.constraints = Constraints(constraints or [])
 
-    mods["mythril.laser.ethereum.state.constraints"].Constraints = Constraints
-    mods["mythril.laser.ethereum.state"].WorldState = WorldState
+    return Constraints, WorldState
 
-    # ---- laser/plugin/interface.py ---------------------------------------------------------
+
+# ---- Solver() call sites outside the funnel ---------------------------------------------------
+
+def _calldata_module(mod, smt, z3):
+    """The calldata slice loop: from ``start``, one ``Solver()`` query per index (timeout 1 s)
+    asking whether the index can still differ from ``stop``; an ``unsat`` or ``unknown``
+    verdict ends the slice.  ``Solver`` is this module's global (bound at import)."""
+    mod.Solver = smt.Solver
+
+    class Calldata:
+        def __init__(self, tx_id, values):
+            self.tx_id = tx_id
+            self.values = list(values)   # concrete bytes; symbolic beyond them
+
+        @property
+        def size(self):
+            return len(self.values)
+
+        def _load(self, index):
+            i = index.value if isinstance(index, smt.BitVec) else index
+            if i is not None and i < len(self.values):
+                return self.values[i]
+            array = z3.Array(f"{self.tx_id}_calldata", z3.BitVecSort(256), z3.BitVecSort(8))
+            return smt.BitVec(z3.Select(array, index.raw))
+
+        def __getitem__(self, item):
+            if not isinstance(item, slice):
+                return self._load(item)
+            first = 0 if item.start is None else item.start
+            stride = 1 if item.step is None else item.step
+            stop = self.size if item.stop is None else item.stop
+            cursor = first if isinstance(first, smt.BitVec) else smt.symbol_factory.BitVecVal(first, 256)
+            parts = []
+            for _ in itertools.count():
+                query = mod.Solver()
+                query.set_timeout(1000)
+                query.add(cursor != stop)
+                if query.check() in (z3.unsat, z3.unknown):
+                    return parts
+                byte = self._load(cursor)
+                parts.append(byte if isinstance(byte, smt.BitVec) else smt.symbol_factory.BitVecVal(byte, 8))
+                cursor = smt.simplify(cursor + stride)
+
+    mod.Calldata = Calldata
+
+
+def _summary_modules(summary_mod, core_mod, smt, z3, kfm):
+    """The summary plugin's two condition checks, each over its module's ``Solver``."""
+    summary_mod.Solver = smt.Solver
+    core_mod.Solver = smt.Solver
+
+    def summary_applies(constraints, solver_timeout):
+        # summary.py:114-117: the state's constraints after the summary's conditions
+        query = summary_mod.Solver()
+        query.set_timeout(solver_timeout)
+        query.add(*constraints)
+        return query.check() == z3.sat
+
+    def keys_may_alias(state_key, key):
+        # core.py:222-227: one storage key against another, with the keccak conditions
+        query = core_mod.Solver()
+        query.set_timeout(3000)
+        query.add(state_key == key)
+        query.add(kfm.create_conditions())
+        return query.check() == z3.sat
+
+    summary_mod.summary_applies = summary_applies
+    core_mod.keys_may_alias = keys_may_alias
+
+
+# ---- plugins ---------------------------------------------------------------------------------------
+
+def _plugins(Singleton, installed_plugins):
     class LaserPlugin:
         def initialize(self, symbolic_vm):
             raise NotImplementedError
 
-    # ---- laser/plugin/builder.py:6-21 -------------------------------------------------------
     class PluginBuilder(ABC):
         name = "Default Plugin Name"
 
@@ -379,9 +493,8 @@ def build(z3, installed_plugins=None):
 
         @abstractmethod
         def __call__(self, *args, **kwargs):
-            pass
+            ...
 
-    # ---- plugin/interface.py:6-46 -----------------------------------------------------------
     class MythrilPlugin:
         author = "Default Author"
         name = "Plugin Name"
@@ -390,12 +503,11 @@ def build(z3, installed_plugins=None):
         plugin_version = "0.0.1 "
         plugin_description = "This is an example plugin description"
 
-        def __init__(self, **kwargs):
+        def __init__(self, **kwargs):   # takes the plugin args, sets nothing (no `enabled`)
             pass
 
         def __repr__(self):
-            plugin_name = type(self).__name__
-            return f"{plugin_name} - {self.plugin_version} - {self.author}"
+            return f"{type(self).__name__} - {self.plugin_version} - {self.author}"
 
     class MythrilCLIPlugin(MythrilPlugin):
         pass
@@ -403,8 +515,7 @@ def build(z3, installed_plugins=None):
     class MythrilLaserPlugin(MythrilPlugin, PluginBuilder, ABC):
         pass
 
-    # ---- laser/plugin/loader.py:12-75 -------------------------------------------------------
-    class LaserPluginLoader(object, metaclass=Singleton):
+    class LaserPluginLoader(metaclass=Singleton):
         def __init__(self):
             self.laser_plugin_builders = {}
             self.plugin_args = {}
@@ -414,43 +525,35 @@ def build(z3, installed_plugins=None):
             self.plugin_args[plugin_name] = kwargs
 
         def load(self, plugin_builder):
-            if plugin_builder.name in self.laser_plugin_builders:
-                return
-            self.laser_plugin_builders[plugin_builder.name] = plugin_builder
+            self.laser_plugin_builders.setdefault(plugin_builder.name, plugin_builder)
 
         def is_enabled(self, plugin_name):
-            if plugin_name not in self.laser_plugin_builders:
-                return False
-            else:
-                return self.laser_plugin_builders[plugin_name].enabled
+            builder = self.laser_plugin_builders.get(plugin_name)
+            return builder is not None and builder.enabled
 
         def enable(self, plugin_name):
-            if plugin_name not in self.laser_plugin_builders:
+            builder = self.laser_plugin_builders.get(plugin_name)
+            if builder is None:
                 return ValueError(f"Plugin with name: {plugin_name} was not loaded")
-            self.laser_plugin_builders[plugin_name].enabled = True
+            builder.enabled = True
 
         def instrument_virtual_machine(self, symbolic_vm, with_plugins):
-            for plugin_name, plugin_builder in self.laser_plugin_builders.items():
-                enabled = (plugin_builder.enabled if not with_plugins
-                           else plugin_name in with_plugins)
+            for name, builder in self.laser_plugin_builders.items():
+                wanted = name in with_plugins if with_plugins else builder.enabled
+                if wanted:
+                    plugin = builder(**self.plugin_args.get(name, {}))
+                    plugin.initialize(symbolic_vm)
+                    self.plugin_list[name] = plugin
 
-                if not enabled:
-                    continue
-
-                plugin = plugin_builder(**self.plugin_args.get(plugin_name, {}))
-                plugin.initialize(symbolic_vm)
-                self.plugin_list[plugin_name] = plugin
-
-    # ---- plugin/discovery.py:11-73 (entry points injected) ---------------------------------
-    class PluginDiscovery(object, metaclass=Singleton):
+    class PluginDiscovery(metaclass=Singleton):
         _installed_plugins = None
 
         def init_installed_plugins(self):
             from importlib.metadata import EntryPoint
 
-            self._installed_plugins = {
-                name: EntryPoint(name, value, "mythril.plugins").load()
-                for name, value in (installed_plugins or {}).items()}
+            self._installed_plugins = {}
+            for name, target in (installed_plugins or {}).items():
+                self._installed_plugins[name] = EntryPoint(name, target, "mythril.plugins").load()
 
         @property
         def installed_plugins(self):
@@ -459,34 +562,29 @@ def build(z3, installed_plugins=None):
             return self._installed_plugins
 
         def is_installed(self, plugin_name):
-            return plugin_name in self.installed_plugins.keys()
+            return plugin_name in self.installed_plugins
 
         def build_plugin(self, plugin_name, plugin_args):
             if not self.is_installed(plugin_name):
                 raise ValueError(f"Plugin with name: `{plugin_name}` is not installed")
-
-            plugin = self.installed_plugins.get(plugin_name)
-            if plugin is None or not issubclass(plugin, MythrilPlugin):
+            cls = self.installed_plugins.get(plugin_name)
+            if cls is None or not issubclass(cls, MythrilPlugin):
                 raise ValueError(f"No valid plugin was found for {plugin_name}")
-
-            return plugin(**plugin_args)
+            return cls(**plugin_args)
 
         def get_plugins(self, default_enabled=None):
+            plugins = self.installed_plugins
             if default_enabled is None:
-                return list(self.installed_plugins.keys())
+                return list(plugins)
+            return [n for n, cls in plugins.items() if cls.plugin_default_enabled == default_enabled]
 
-            return [plugin_name
-                    for plugin_name, plugin_class in self.installed_plugins.items()
-                    if plugin_class.plugin_default_enabled == default_enabled]
-
-    # ---- plugin/loader.py:19-79 -------------------------------------------------------------
     class UnsupportedPluginType(Exception):
         pass
 
-    class MythrilPluginLoader(object, metaclass=Singleton):
+    class MythrilPluginLoader(metaclass=Singleton):
         def __init__(self):
             self.loaded_plugins = []
-            self.plugin_args = dict()
+            self.plugin_args = {}
             self._load_default_enabled()
 
         def set_args(self, plugin_name, **kwargs):
@@ -495,82 +593,153 @@ def build(z3, installed_plugins=None):
         def load(self, plugin):
             if not isinstance(plugin, MythrilPlugin):
                 raise ValueError("Passed plugin is not of type MythrilPlugin")
-            if isinstance(plugin, MythrilLaserPlugin):
-                self._load_laser_plugin(plugin)
-            else:
+            if not isinstance(plugin, MythrilLaserPlugin):
                 raise UnsupportedPluginType("Passed plugin type is not yet supported")
-
+            LaserPluginLoader().load(plugin)
             self.loaded_plugins.append(plugin)
 
-        @staticmethod
-        def _load_laser_plugin(plugin):
-            LaserPluginLoader().load(plugin)
-
         def _load_default_enabled(self):
-            for plugin_name in PluginDiscovery().get_plugins(default_enabled=True):
-                plugin = PluginDiscovery().build_plugin(
-                    plugin_name, self.plugin_args.get(plugin_name, {}))
-                self.load(plugin)
+            discovery = PluginDiscovery()
+            for name in discovery.get_plugins(default_enabled=True):
+                self.load(discovery.build_plugin(name, self.plugin_args.get(name, {})))
 
-    # ---- analysis/solver.py:129-165 (_replace_with_actual_sha), resolving the keccak
-    # manager and symbol_factory through their modules at call time like the reference's
-    # module globals; get_transaction_sequence calls it by its module-global name ----------
+    return types.SimpleNamespace(
+        LaserPlugin=LaserPlugin, PluginBuilder=PluginBuilder, MythrilPlugin=MythrilPlugin,
+        MythrilCLIPlugin=MythrilCLIPlugin, MythrilLaserPlugin=MythrilLaserPlugin,
+        LaserPluginLoader=LaserPluginLoader, PluginDiscovery=PluginDiscovery,
+        UnsupportedPluginType=UnsupportedPluginType, MythrilPluginLoader=MythrilPluginLoader)
+
+
+# ---- the report's keccak concretisation ---------------------------------------------------------
+
+def _report_module(mod, mods):
+    """Each 64-hex-digit window of a transaction's calldata (after the selector, or after the
+    creation code when the input carries it) that contains the keccak manager's hash marker
+    and is a concrete hash the model knows is replaced by the keccak of its preimage, the
+    preimage read from the model through the width's inverse function."""
+
+    def preimage_of(kfm, sf, known, model, digest):
+        found = None
+        for width, digests in known.items():   # the last width that knows it wins
+            if digest in digests:
+                _, inverse = kfm.store_function[width]
+                raw = model.eval(inverse(sf.BitVecVal(digest, 256)).raw)
+                found = sf.BitVecVal(raw.as_long(), width)
+        return found
+
     def _replace_with_actual_sha(concrete_transactions, model, code=None):
-        keccak_function_manager = mods["mythril.laser.ethereum.function_managers"].keccak_function_manager
-        symbol_factory = mods["mythril.laser.smt"].symbol_factory
-        concrete_hashes = keccak_function_manager.get_concrete_hash_data(model)
+        # the manager and factory are read through their modules at call time
+        kfm = mods["mythril.laser.ethereum.function_managers"].keccak_function_manager
+        sf = mods["mythril.laser.smt"].symbol_factory
+        known = kfm.get_concrete_hash_data(model)
         for tx in concrete_transactions:
-            if keccak_function_manager.hash_matcher not in tx["input"]:
+            original = tx["input"]
+            if kfm.hash_matcher not in original:
                 continue
-            if code is not None and code.bytecode in tx["input"]:
-                s_index = len(code.bytecode) + 2
-            else:
-                s_index = 10
-            for i in range(s_index, len(tx["input"])):
-                data_slice = tx["input"][i: i + 64]
-                if keccak_function_manager.hash_matcher not in data_slice or len(data_slice) != 64:
+            with_code = code is not None and code.bytecode in original
+            head = len(code.bytecode) + 2 if with_code else 10
+            for pos in range(head, len(original)):
+                window = tx["input"][pos:pos + 64]
+                if len(window) != 64 or kfm.hash_matcher not in window:
                     continue
-                find_input = symbol_factory.BitVecVal(int(data_slice, 16), 256)
-                input_ = None
-                for size in concrete_hashes:
-                    _, inverse = keccak_function_manager.store_function[size]
-                    if find_input.value not in concrete_hashes[size]:
-                        continue
-                    input_ = symbol_factory.BitVecVal(model.eval(inverse(find_input).raw).as_long(), size)
-                if input_ is None:
+                pre = preimage_of(kfm, sf, known, model, int(window, 16))
+                if pre is None:
                     continue
-                keccak = keccak_function_manager.find_concrete_keccak(input_)
-                hex_keccak = hex(keccak.value)[2:]
-                if len(hex_keccak) != 64:
-                    hex_keccak = "0" * (64 - len(hex_keccak)) + hex_keccak
-                tx["input"] = tx["input"][:s_index] + tx["input"][s_index:].replace(
-                    tx["input"][i: 64 + i], hex_keccak)
+                digest = "%064x" % kfm.find_concrete_keccak(pre).value
+                current = tx["input"]
+                tx["input"] = current[:head] + current[head:].replace(window, digest)
 
     def get_transaction_sequence_tail(concrete_transactions, model, code=None):
-        """The concretisation step of get_transaction_sequence (analysis/solver.py:96-99)."""
-        mods["mythril.analysis.solver"]._replace_with_actual_sha(concrete_transactions, model, code)
+        """The concretisation step of get_transaction_sequence (analysis/solver.py:96-99),
+        calling the step by its module-global name."""
+        mod._replace_with_actual_sha(concrete_transactions, model, code)
         return concrete_transactions
 
-    mods["mythril.analysis.solver"]._replace_with_actual_sha = _replace_with_actual_sha
-    mods["mythril.analysis.solver"].get_transaction_sequence_tail = get_transaction_sequence_tail
-    mods["mythril.support.support_utils"].sha3 = host_sha3
+    mod._replace_with_actual_sha = _replace_with_actual_sha
+    mod.get_transaction_sequence_tail = get_transaction_sequence_tail
 
-    mods["mythril.laser.plugin.builder"].PluginBuilder = PluginBuilder
-    mods["mythril.laser.plugin.interface"].LaserPlugin = LaserPlugin
-    mods["mythril.laser.plugin.loader"].LaserPluginLoader = LaserPluginLoader
+
+# ---- assembly -------------------------------------------------------------------------------------
+
+def build(z3, installed_plugins=None):
+    """Module objects keyed by their Mythril names, bound to the given z3 module.
+    ``installed_plugins`` = {entry-point name: "module:attr"}, the ``"mythril.plugins"``
+    entry points discovery loads — nothing is pip-installed here, so the test passes the value
+    the package metadata declares (pyproject.toml)."""
+    mods = {n: types.ModuleType(n) for n in MODULES}
+    Singleton = _singleton_meta()
+
+    class UnsatError(Exception):
+        pass
+
+    class SolverTimeOutException(UnsatError):
+        pass
+
+    SolverStatistics, stat_smt_query = _statistics(Singleton)
+    smt = _facade(z3, stat_smt_query)
+    LRUCache, ModelCache = _model_cache(z3)
+
+    exc = mods["mythril.exceptions"]
+    exc.UnsatError, exc.SolverTimeOutException = UnsatError, SolverTimeOutException
+    stats_mod = mods["mythril.laser.smt.solver.solver_statistics"]
+    stats_mod.stat_smt_query, stats_mod.SolverStatistics = stat_smt_query, SolverStatistics
+    smt_mod = mods["mythril.laser.smt"]
+    for name in ("Bool", "BitVec", "symbol_factory", "And", "simplify", "Optimize", "Solver",
+                 "BaseSolver", "Model"):
+        setattr(smt_mod, name, getattr(smt, name))
+    smt_mod.SolverStatistics = SolverStatistics
+    mods["mythril.laser.smt.model"].Model = smt.Model
+    for name in ("mythril.laser.smt.solver", "mythril.laser.smt.solver.solver"):
+        m = mods[name]
+        m.BaseSolver, m.Solver, m.Optimize = smt.BaseSolver, smt.Solver, smt.Optimize
+    mods["mythril.laser.smt.solver"].SolverStatistics = SolverStatistics
+
+    kfm = types.SimpleNamespace(interval_hook_for_size={}, concrete_hashes={},
+                                create_conditions=lambda: smt.Bool(z3.BoolVal(True)))
+    mods["mythril.laser.ethereum.function_managers"].keccak_function_manager = kfm
+
+    utils = mods["mythril.support.support_utils"]
+    utils.Singleton, utils.LRUCache, utils.ModelCache, utils.sha3 = Singleton, LRUCache, ModelCache, host_sha3
+
+    funnel = mods["mythril.support.model"]
+    funnel.Optimize = smt.Optimize        # bound at import (support/model.py:13)
+    funnel.model_cache = ModelCache()
+    funnel.solver_timeout_default = 10000
+    funnel.solver_worker, funnel.get_model = _funnel(z3, funnel, smt, UnsatError, SolverTimeOutException)
+
+    Constraints, WorldState = _state(funnel, kfm, UnsatError, SolverTimeOutException)
+    mods["mythril.laser.ethereum.state.constraints"].Constraints = Constraints
+    mods["mythril.laser.ethereum.state"].WorldState = WorldState
+
+    _calldata_module(mods["mythril.laser.ethereum.state.calldata"], smt, z3)
+    _summary_modules(mods["mythril.laser.plugin.plugins.summary.summary"],
+                     mods["mythril.laser.plugin.plugins.summary.core"], smt, z3, kfm)
+
+    pl = _plugins(Singleton, installed_plugins)
+    mods["mythril.laser.plugin.builder"].PluginBuilder = pl.PluginBuilder
+    mods["mythril.laser.plugin.interface"].LaserPlugin = pl.LaserPlugin
+    mods["mythril.laser.plugin.loader"].LaserPluginLoader = pl.LaserPluginLoader
     pi = mods["mythril.plugin.interface"]
-    pi.MythrilPlugin, pi.MythrilCLIPlugin, pi.MythrilLaserPlugin = MythrilPlugin, MythrilCLIPlugin, MythrilLaserPlugin
-    mods["mythril.plugin.discovery"].PluginDiscovery = PluginDiscovery
-    mods["mythril.plugin.loader"].MythrilPluginLoader = MythrilPluginLoader
-    mods["mythril.plugin.loader"].UnsupportedPluginType = UnsupportedPluginType
+    pi.MythrilPlugin, pi.MythrilCLIPlugin, pi.MythrilLaserPlugin = (pl.MythrilPlugin, pl.MythrilCLIPlugin,
+                                                                    pl.MythrilLaserPlugin)
+    mods["mythril.plugin.discovery"].PluginDiscovery = pl.PluginDiscovery
+    mods["mythril.plugin.loader"].MythrilPluginLoader = pl.MythrilPluginLoader
+    mods["mythril.plugin.loader"].UnsupportedPluginType = pl.UnsupportedPluginType
+
+    _report_module(mods["mythril.analysis.solver"], mods)
+
     return mods, types.SimpleNamespace(
-        Bool=Bool, Model=Model, Optimize=Optimize, Solver=Solver, Constraints=Constraints,
-        WorldState=WorldState, ModelCache=ModelCache, UnsatError=UnsatError,
+        Bool=smt.Bool, BitVec=smt.BitVec, symbol_factory=smt.symbol_factory, Model=smt.Model,
+        Optimize=smt.Optimize, Solver=smt.Solver, Constraints=Constraints, WorldState=WorldState,
+        LRUCache=LRUCache, ModelCache=ModelCache, UnsatError=UnsatError,
         SolverTimeOutException=SolverTimeOutException, SolverStatistics=SolverStatistics,
-        LaserPlugin=LaserPlugin, PluginBuilder=PluginBuilder, MythrilPlugin=MythrilPlugin,
-        MythrilLaserPlugin=MythrilLaserPlugin, LaserPluginLoader=LaserPluginLoader,
-        PluginDiscovery=PluginDiscovery, MythrilPluginLoader=MythrilPluginLoader,
-        Singleton=Singleton, funnel=funnel, kfm=kfm)
+        stat_smt_query=stat_smt_query, LaserPlugin=pl.LaserPlugin, PluginBuilder=pl.PluginBuilder,
+        MythrilPlugin=pl.MythrilPlugin, MythrilLaserPlugin=pl.MythrilLaserPlugin,
+        LaserPluginLoader=pl.LaserPluginLoader, PluginDiscovery=pl.PluginDiscovery,
+        MythrilPluginLoader=pl.MythrilPluginLoader, Singleton=Singleton, funnel=funnel, kfm=kfm,
+        calldata=mods["mythril.laser.ethereum.state.calldata"],
+        summary=mods["mythril.laser.plugin.plugins.summary.summary"],
+        summary_core=mods["mythril.laser.plugin.plugins.summary.core"])
 
 
 def install(monkeypatch, z3, installed_plugins=None):
