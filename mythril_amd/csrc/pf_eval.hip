@@ -270,6 +270,19 @@ PF_INL u256 pow2m1(uint32_t k) {  // 2^k - 1
     return r;
 }
 
+#if defined(PF_PROBE_2X_GEN) || defined(PF_PROBE_2X_DIV) || defined(PF_PROBE_2X_EXP) || \
+    defined(PF_PROBE_2X_MUL) || defined(PF_PROBE_2X_PHILOX)
+// Doubling probes (timing only, tools/gpu_probe2x.sh): a unit runs twice on operands that
+// differ by a per-lane zero the compiler cannot see through, and the second result is folded
+// in under that zero — same values, same branches, twice the unit's issue.  The time added is
+// the unit's marginal cost in the running kernel, without the value shift of a removal probe.
+PF_INL uint32_t hidden_zero() {
+    uint32_t z;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+    return z;
+}
+#endif
+
 // boundary-arm deltas (gen_var): entry j in bits 3j..3j+2, biased by 2
 #define PF_BND_DELTA 0x2ca281b1aull
 
@@ -355,7 +368,19 @@ PF_INL uint32_t umod_rcp(uint32_t x, uint32_t d, uint32_t z) {
 PF_INL u256 gen_var(const SetCtx& S, uint32_t v, uint32_t cand) {
     const uint4 sc = S.schema[v];  // uniform -> scalar load
     const uint64_t p0 = mul_wide(cand, PF_PHILOX_M0);  // round 1 of all three blocks
+#ifdef PF_PROBE_2X_PHILOX
+    uint4 m = philox_gen(p0, v, 2u, S.k0, S.k1);
+    const uint32_t hzp = hidden_zero();
+    {
+        const uint64_t p0b = mul_wide(cand ^ hzp, PF_PHILOX_M0);
+        const uint4 mb = philox_gen(p0b, v, 2u, S.k0, S.k1);
+        const uint4 r0b = philox_gen(p0b, v, 0u, S.k0, S.k1);
+        const uint4 r1b = philox_gen(p0b, v, 1u, S.k0, S.k1);
+        m.w ^= (mb.w ^ r0b.x ^ r1b.y) & hzp;
+    }
+#else
     const uint4 m = philox_gen(p0, v, 2u, S.k0, S.k1);
+#endif
     const uint32_t kind = sc.x & 0xffu, w = (sc.x >> 8) & 0x3ffu;
     const uint32_t hint0 = sc.y, hint1 = sc.z, pslot = sc.w;
     // The one per-lane gather (a constant of the set for the +-1 arm, or the actor table
@@ -522,6 +547,8 @@ PF_INL u256 gen_var(const SetCtx& S, uint32_t v, uint32_t cand) {
 }
 
 enum Mode { MODE_GEN = 0, MODE_SOA = 1 };
+
+
 
 // Per-unit cycle accounting (profiling builds only, tools/unitprof.py): s_memtime deltas of
 // every bytecode instruction, bucketed by datapath unit (EXP separately), kept in SGPRs.
@@ -730,6 +757,15 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
                 // (pf::exp256_split)
                 if (op == PF_W_MUL) {
                     z = pf::mul256(x, y);
+#ifdef PF_PROBE_2X_MUL
+                    {
+                        const uint32_t hz = hidden_zero();
+                        u256 x2 = x;
+                        x2.l[0] ^= hz;
+                        const u256 z2 = pf::mul256(x2, y);
+                        z.l[7] ^= z2.l[7] & hz;
+                    }
+#endif
                 } else {
 #ifdef PF_DIAG_NO_EXP
                     z = pf::add256(x, y);
@@ -737,7 +773,18 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
 #ifdef PF_PROFILE_UNITS
                     z = pf::exp256_split(x, y, exp_tbl, 64u, &prof->c[15]);
 #else
+#ifdef PF_PROBE_2X_EXP
+                    {
+                        const uint32_t hz = hidden_zero();
+                        u256 x2 = x;
+                        x2.l[1] ^= hz;
+                        const u256 z2 = pf::exp256_split(x2, y, exp_tbl, 64u);
+                        z = pf::exp256_split(x, y, exp_tbl, 64u);
+                        z.l[7] ^= z2.l[7] & hz;
+                    }
+#else
                     z = pf::exp256_split(x, y, exp_tbl, 64u);
+#endif
 #endif
 #endif
                     PF_WAIT_ALL();
@@ -778,6 +825,16 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
                 q = ua; rr = ub;
 #else
                 pf::udivrem256(ua, ub, &q, &rr);
+#ifdef PF_PROBE_2X_DIV
+                {
+                    const uint32_t hz = hidden_zero();
+                    u256 ua2 = ua, q2, r2;
+                    ua2.l[0] ^= hz;
+                    pf::udivrem256(ua2, ub, &q2, &r2);
+                    q.l[0] ^= q2.l[0] & hz;
+                    rr.l[0] ^= r2.l[7] & hz;
+                }
+#endif
 #endif
                 // x and y are not read past the division (their registers are free in it):
                 // UMUL_NOOVF's a comes back from LDS, SMOD's signed divisor is rebuilt from |b|
@@ -825,6 +882,14 @@ PF_INL uint32_t run_program(const SetCtx& S, uint32_t cand, bool active, uint32_
                     z = pf::zero256(); z.l[0] = cand ^ aux;
 #else
                     z = gen_var(S, aux, cand);
+#ifdef PF_PROBE_2X_GEN
+                    {
+                        const uint32_t hz = hidden_zero();
+                        const u256 z2 = gen_var(S, aux, cand ^ hz);
+                        z.l[0] ^= z2.l[0] & (hz - 1u) & hz;
+                        z.l[1] ^= z2.l[7] & hz;
+                    }
+#endif
 #endif
                 } else {
 #pragma unroll

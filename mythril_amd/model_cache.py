@@ -64,6 +64,9 @@ class QuickSatStats:
     reference_loops: int = 0  # queries the converter / lowering could not take (reference loop)
     leaf_evals: int = 0       # (model, leaf) values computed (the rest were memoised)
     leaf_evals_native: int = 0   # of which by the native witness evaluator (pflt_witness_values)
+    verdicts_memo: int = 0       # (model, conjunct) verdicts read from a model's memo
+    verdicts_native: int = 0     # ... computed by the native witness evaluator (small batches)
+    verdicts_engine: int = 0     # ... computed on the engine (pf_eval_programs)
     phase_s: Dict[str, float] = field(default_factory=dict)
 
 
@@ -144,11 +147,30 @@ class ExplicitGroups:
     the position in the query's leaf list of each program variable (the SoA rows the
     programs read, in pf_eval_programs' order); ``pack`` the packed arrays, made once."""
 
-    __slots__ = ("programs", "gather", "offsets", "_pack")
+    __slots__ = ("programs", "gather", "offsets", "conjs", "_pack")
 
-    def __init__(self, programs, gather: np.ndarray, offsets: List[int]):
+    def __init__(self, programs, gather: np.ndarray, offsets: List[int], conjs: Optional[List[T.Term]] = None):
         self.programs, self.gather, self.offsets = programs, gather, offsets
+        self.conjs = conjs      # with CONJ_PROGRAMS: the conjunct term of each program
         self._pack = None
+
+    def spans(self) -> List[Tuple[int, int]]:
+        ends = self.offsets[1:] + [len(self.gather)]
+        return list(zip(self.offsets, ends))
+
+    def subset(self, ks: Sequence[int]) -> Tuple[List[int], "ExplicitGroups"]:
+        """(leaf positions, group) of programs ``ks`` alone: the group's gather renumbered
+        onto the returned positions (indices into the query's leaf list)."""
+        spans = self.spans()
+        pos: Dict[int, int] = {}
+        gather, offsets = [], []
+        for k in ks:
+            lo, hi = spans[k]
+            offsets.append(len(gather))
+            for g in self.gather[lo:hi]:
+                gather.append(pos.setdefault(int(g), len(pos)))
+        return list(pos), ExplicitGroups([self.programs[k] for k in ks], np.array(gather, dtype=np.int64), offsets,
+                                         [self.conjs[k] for k in ks] if self.conjs is not None else None)
 
     def pack(self):
         if self._pack is None:
@@ -272,7 +294,7 @@ def explicit_groups(query: T.Term):
                     for t in vt:
                         gather.append(pos.setdefault(t, len(pos)))
                 hit = (list(pos), ExplicitGroups([p for _, p in lowered], np.array(gather, dtype=np.int64),
-                                                 offsets))
+                                                 offsets, [gr[0] for gr in groups] if CONJ_PROGRAMS else None))
         except (LoweringError, ValueError, OverflowError, RecursionError) as e:
             hit = f"{type(e).__name__}: {e}"
         with _PROG_LOCK:
@@ -298,35 +320,55 @@ _EMPTY_REG = _EmptyRegistry()
 
 class LeafValues:
     """One cached model's values of leaf terms, each computed once and kept as the 32 bytes
-    (little-endian) of its row in pf_eval_assignments' input."""
+    (little-endian) of its row in pf_eval_assignments' input.
 
-    __slots__ = ("evaluate", "vals")
+    ``evaluate_many`` (optional) values several leaves in ONE evaluation of the model — a z3
+    model evaluates the concatenation of the leaves with one ``eval``, sharing every common
+    subterm (store chains, keccak applications) the way the reference's single eval of the
+    whole conjunction does, where one ``eval`` per leaf re-walked them per leaf."""
 
-    def __init__(self, evaluate: Callable[[T.Term], int]):
+    __slots__ = ("evaluate", "evaluate_many", "vals", "verdicts")
+
+    def __init__(self, evaluate: Callable[[T.Term], int],
+                 evaluate_many: Optional[Callable[[Sequence[T.Term]], List[int]]] = None):
         self.evaluate = evaluate
+        self.evaluate_many = evaluate_many
         self.vals: Dict[T.Term, bytes] = {}
+        # conjunct -> its truth under this model (CONJ_PROGRAMS): a model is immutable, so a
+        # conjunct is evaluated under it once, whichever query it comes with
+        self.verdicts: Dict[T.Term, bool] = {}
+
+    def _put(self, t: T.Term, x: int) -> bytes:
+        v = self.vals[t] = (int(x) & T.M(max(t.width, 1))).to_bytes(32, "little")
+        return v
 
     def row(self, leaves: Sequence[T.Term]) -> Optional[bytes]:
         """The values of ``leaves`` as one byte row; None if the model's evaluator rejects
         one of them."""
         vals = self.vals
-        out = []
+        missing = [t for t in dict.fromkeys(leaves) if t not in vals]
+        if len(missing) > 1 and self.evaluate_many is not None:
+            try:
+                for t, x in zip(missing, self.evaluate_many(missing)):
+                    self._put(t, x)
+            except Exception as e:  # noqa: BLE001 - per leaf below finds the one it rejects
+                log.debug("batched leaf evaluation declined: %s", e)
         new = 0
-        for t in leaves:
-            v = vals.get(t)
-            if v is None:
-                try:
-                    x = int(self.evaluate(t))
-                except Exception as e:  # noqa: BLE001 - the reference statement decides then
-                    log.debug("leaf %s not evaluated: %s", t.op, e)
-                    return None
-                v = vals[t] = (x & T.M(max(t.width, 1))).to_bytes(32, "little")
+        for t in missing:
+            if t in vals:
                 new += 1
-            out.append(v)
+                continue
+            try:
+                x = int(self.evaluate(t))
+            except Exception as e:  # noqa: BLE001 - the reference statement decides then
+                log.debug("leaf %s not evaluated: %s", t.op, e)
+                return None
+            self._put(t, x)
+            new += 1
         if new:
             with _STATS_LOCK:
                 STATS.leaf_evals += new
-        return b"".join(out)
+        return b"".join([vals[t] for t in leaves])
 
     def value(self, t: T.Term) -> Optional[int]:
         v = self.vals.get(t)
@@ -514,6 +556,18 @@ def choose(query: T.Term, leaf_values: Sequence[Optional[LeafValues]],
         phases[name] = phases.get(name, 0.0) + now - t
         return now
 
+    if VERDICT_MEMO and CONJ_PROGRAMS and query is not T.TRUE:
+        # conjunct by conjunct from the models' verdict memos: nothing is lowered unless some
+        # (model, conjunct) pair goes to the engine
+        if engine is None:
+            from .engine import get_engine
+
+            engine = get_engine()
+        conjs = query_conjuncts(query)
+        t = lap("lower", t0)
+        choice, host, launches, on_engine_n = _choose_memo(conjs, leaf_values, reference, engine, k1, lap, t)
+        _account(choice, host, launches, on_engine_n, phases)
+        return choice
     if query is T.TRUE:
         leaves, program = [], None
     else:
@@ -529,6 +583,215 @@ def choose(query: T.Term, leaf_values: Sequence[Optional[LeafValues]],
                                                      engine, lap, t)
     _account(choice, host, launches, on_engine_n, phases)
     return choice
+
+
+# Per-(model, conjunct) verdicts (CONJ_PROGRAMS): a cached model is immutable, so the truth
+# of a conjunct under it is computed once and kept in the model's LeafValues; a query is then
+# decided model by model, newest first, from the memo — a model with a false conjunct is out,
+# one whose every conjunct is true is the answer — and only the unknown (model, conjunct) pairs
+# of the models the walk reaches are evaluated.  LASER's queries along a path share all but
+# their newest conjuncts, so after the first query of a path most of the work is one new
+# conjunct under the few models the old conjuncts leave standing.  The unknown pairs of a
+# batch of models go in one engine launch (only the programs of the unknown conjuncts, over
+# only those models' rows); a batch of natively held GPU witnesses with at most
+# HOST_VERDICT_PAIRS unknown pairs is evaluated by the native witness evaluator instead
+# (csrc/pf_recheck.cpp: the interpretation Z3WitnessView.eval applies, natively) — for a few
+# pairs the launch's fixed cost dominates.  PF_QS_MEMO=0 restores the all-models launches;
+# PF_QS_HOST_PAIRS=0 sends every batch to the engine.
+VERDICT_MEMO = os.environ.get("PF_QS_MEMO", "1") != "0"
+HOST_VERDICT_PAIRS = int(os.environ.get("PF_QS_HOST_PAIRS", "256"))
+
+
+def _memo_status(lv: Optional[LeafValues], conjs: Sequence[T.Term]) -> Optional[bool]:
+    """False if a conjunct is known false under the model, True if every one is known true,
+    else None (some unknown)."""
+    if lv is None:
+        return None
+    vd = lv.verdicts
+    unknown = False
+    for c in conjs:
+        v = vd.get(c)
+        if v is None:
+            unknown = True
+        elif not v:
+            return False
+    return None if unknown else True
+
+
+def eval_rows_each(group: ExplicitGroups, rows, n_leaves: int, engine) -> np.ndarray:
+    """SAT flags [program][model] of a group's programs over explicit model rows (one
+    pf_eval_programs launch)."""
+    soa = soa_of(rows, n_leaves)[group.gather] if n_leaves else soa_of(rows, 0)
+    if hasattr(engine, "eval_programs"):
+        return engine.eval_programs(group.pack(), soa)
+    n = soa.shape[-1]
+    out = np.ones((len(group.programs), n), dtype=bool)
+    for k, (prog, (lo, hi)) in enumerate(zip(group.programs, group.spans())):
+        out[k] = _eval_one(prog, np.ascontiguousarray(soa[lo:hi]) if hi > lo else soa_of(rows, 0)[:, :, :n], engine)
+    return out
+
+
+_QCONJ: "OrderedDict[T.Term, List[T.Term]]" = OrderedDict()
+_SUBGROUPS: "OrderedDict[Tuple[T.Term, ...], object]" = OrderedDict()
+
+
+def query_conjuncts(query: T.Term) -> List[T.Term]:
+    """The query's flattened, de-duplicated conjuncts (explicit_groups' split), cached."""
+    with _PROG_LOCK:
+        hit = _QCONJ.get(query)
+        if hit is not None:
+            _QCONJ.move_to_end(query)
+            return hit
+    if query.op == "and":
+        conj = [c for c in dict.fromkeys(flat_conjuncts(list(query.args))) if c is not T.TRUE]
+    else:
+        conj = [query]
+    with _PROG_LOCK:
+        _QCONJ[query] = conj
+        while len(_QCONJ) > _PROGRAMS_MAX:
+            _QCONJ.popitem(last=False)
+    return conj
+
+
+def conjunct_group(conjs: Sequence[T.Term]) -> Tuple[List[T.Term], ExplicitGroups]:
+    """(leaf terms, group) of one program per conjunct, run side by side (cached by the
+    conjunct tuple); raises LoweringError if a conjunct cannot be lowered."""
+    key = tuple(conjs)
+    with _PROG_LOCK:
+        hit = _SUBGROUPS.get(key)
+        if hit is not None:
+            _SUBGROUPS.move_to_end(key)
+            return hit
+    lowered = [_conj_program(c) for c in conjs]
+    pos: Dict[T.Term, int] = {}
+    gather, offsets = [], []
+    for vt, prog in lowered:
+        if len(vt) != n_vars(prog):
+            raise LoweringError("explicit group: variables and leaves differ")
+        offsets.append(len(gather))
+        for t in vt:
+            gather.append(pos.setdefault(t, len(pos)))
+    hit = (list(pos), ExplicitGroups([p for _, p in lowered], np.array(gather, dtype=np.int64), offsets, list(conjs)))
+    with _PROG_LOCK:
+        _SUBGROUPS[key] = hit
+        while len(_SUBGROUPS) > _PROGRAMS_MAX:
+            _SUBGROUPS.popitem(last=False)
+    return hit
+
+
+def _resolve(batch: List[int], conjs: Sequence[T.Term], leaf_values, engine, noval: set) -> Tuple[int, int]:
+    """Compute the unknown conjunct verdicts of the models ``batch`` into their memos;
+    (launches, models on the engine).  A model whose leaves cannot be valued goes to
+    ``noval`` (the reference statement decides it)."""
+    todo: Dict[int, List[int]] = {}
+    for j in batch:
+        vd = leaf_values[j].verdicts
+        ks = [k for k, c in enumerate(conjs) if c not in vd]
+        if ks:
+            todo[j] = ks
+    if not todo:
+        return 0, 0
+    natives = [j for j in todo if isinstance(leaf_values[j], NativeLeafValues)]
+    if natives and HOST_VERDICT_PAIRS > 0:
+        ks = sorted({k for j in natives for k in todo[j]})
+        if len(natives) * len(ks) <= HOST_VERDICT_PAIRS:
+            from .smt import native_terms
+
+            groups: Dict[Tuple[int, int], List[int]] = {}
+            for j in natives:
+                lv = leaf_values[j]
+                groups.setdefault((id(lv.native.st), id(lv.reg)), []).append(j)
+            terms = [conjs[k] for k in ks]
+            n_done = 0
+            for js in groups.values():
+                lvs = [leaf_values[j] for j in js]
+                vals, ok = native_terms.witness_values_many([lv.native for lv in lvs], terms, lvs[0].reg,
+                                                            min(LEAF_THREADS, len(lvs)))
+                for m, j in enumerate(js):
+                    vd = leaf_values[j].verdicts
+                    for q, k in enumerate(ks):
+                        if ok[m, q]:
+                            vd[conjs[k]] = bool(vals[m, q, 0] & 1)
+                            n_done += 1
+                    todo[j] = [k for k in todo[j] if conjs[k] not in vd]
+                    if not todo[j]:
+                        del todo[j]
+            with _STATS_LOCK:
+                STATS.verdicts_native += n_done
+    if not todo:
+        return 0, 0
+    js = list(todo)
+    ks = sorted({k for j in js for k in todo[j]})
+    sub_leaves, sub = conjunct_group([conjs[k] for k in ks])
+    nat = native_rows([leaf_values[j] for j in js], sub_leaves)
+    block = getattr(nat, "block", None)
+    if block is not None:
+        rows, on = block, js
+    else:
+        rows, on = [], []
+        for m, j in enumerate(js):
+            r = nat[m] if m in nat else leaf_values[j].row(sub_leaves)
+            if r is None:
+                noval.add(j)
+                continue
+            rows.append(r)
+            on.append(j)
+    if not on:
+        return 0, 0
+    flags = eval_rows_each(sub, rows, len(sub_leaves), engine)
+    for m, j in enumerate(on):
+        vd = leaf_values[j].verdicts
+        for q, k in enumerate(ks):
+            vd[conjs[k]] = bool(flags[q, m])
+    with _STATS_LOCK:
+        STATS.verdicts_engine += len(on) * len(ks)
+    return 1, len(on)
+
+
+def _choose_memo(conjs: Sequence[T.Term], leaf_values, reference, engine, k1, lap, t):
+    """choose() over the per-(model, conjunct) memo: (choice, host, launches, models on the
+    engine).  Models are walked newest first; an undecided model and the next ones (up to
+    the (k1 + 1)-th with dear leaves the first time, all the rest after) are resolved as one
+    batch, so the answer is the reference loop's: the first model in the order that holds."""
+    n = len(leaf_values)
+    host = launches = on_engine_n = 0
+    noval: set = set()
+    memo_hits = 0
+    first = True
+    i = 0
+    choice = None
+    while i < n:
+        lv = leaf_values[i]
+        st = _memo_status(lv, conjs) if i not in noval else None
+        if st is False:
+            memo_hits += 1
+            i += 1
+            continue
+        if st is True:
+            memo_hits += 1
+            choice = i
+            break
+        if lv is None or i in noval:   # unvaluable: the reference statement, in its place
+            host += 1
+            if reference(i):
+                choice = i
+                break
+            i += 1
+            continue
+        rest = leaf_values[i:]
+        end = i + (first_stage_end(rest, k1) if first else len(rest))
+        first = False
+        batch = [j for j in range(i, max(end, i + 1))
+                 if leaf_values[j] is not None and j not in noval and _memo_status(leaf_values[j], conjs) is None]
+        t = lap("leaves", t)
+        nl, ne = _resolve(batch, conjs, leaf_values, engine, noval)
+        launches += nl
+        on_engine_n += ne
+        t = lap("eval", t)
+    lap("host", t)
+    with _STATS_LOCK:
+        STATS.verdicts_memo += memo_hits
+    return choice, host, launches, on_engine_n
 
 
 def _account(choice, host, launches, on_engine_n, phases) -> None:
@@ -620,24 +883,58 @@ def leaf_evaluator(z3, internal):
     w = getattr(getattr(internal, "internal", None), "w", None)
     if w is not None and hasattr(w, "leaf_value"):
         return w.leaf_value
+    return _z3_leaf_evaluators(z3, internal)[0]
+
+
+def _z3_leaf_evaluators(z3, internal):
+    """(one leaf, several leaves) evaluators of a z3 model on one private deep copy.  The
+    batched form evaluates ``Concat`` of the leaves (a Bool leaf as a 1-bit ``If``) with one
+    ``eval(..., model_completion=True)`` and splits the value: one evaluation per model and
+    query, as the reference's ``eval`` of the whole conjunction (support_utils.py:63), so
+    shared subterms are evaluated once and completion happens inside one call."""
     from .z3_terms import converter
 
     conv = converter(z3)
     holder: list = []
 
-    def ev(t: T.Term) -> int:
+    def copy_():
         if not holder:
             holder.append(deepcopy(internal))
-        return z3_literal(z3, holder[0].eval(conv.ast_of(t), model_completion=True))
+        return holder[0]
 
-    return ev
+    def ev(t: T.Term) -> int:
+        return z3_literal(z3, copy_().eval(conv.ast_of(t), model_completion=True))
+
+    def ev_many(ts: Sequence[T.Term]) -> List[int]:
+        parts, widths = [], []
+        for t in ts:
+            a = conv.ast_of(t)
+            if z3.is_bool(a):
+                a = z3.If(a, z3.BitVecVal(1, 1), z3.BitVecVal(0, 1))
+            parts.append(a)
+            widths.append(a.size())
+        v = copy_().eval(parts[0] if len(parts) == 1 else z3.Concat(*parts), model_completion=True)
+        if not z3.is_bv_value(v):
+            raise ValueError("batched leaf evaluation: not a numeral")
+        x = v.as_long()
+        out = [0] * len(ts)
+        for i in range(len(ts) - 1, -1, -1):
+            out[i] = x & ((1 << widths[i]) - 1)
+            x >>= widths[i]
+        return out
+
+    return ev, ev_many
 
 
 def leaf_values_of(z3, internal) -> LeafValues:
     """The LeafValues of one internal model: natively held for a GPU witness whose buckets
     were lowered natively (NativeLeafValues), else over ``leaf_evaluator``."""
-    ev = leaf_evaluator(z3, internal)
     wm = getattr(internal, "internal", None)
+    w = getattr(wm, "w", None)
+    if w is None or not hasattr(w, "leaf_value"):
+        ev, ev_many = _z3_leaf_evaluators(z3, internal)
+        return LeafValues(ev, ev_many)
+    ev = w.leaf_value
     parts, reg = getattr(wm, "parts", None), getattr(wm, "reg", None)
     if parts and reg is not None and NATIVE_LEAVES:
         from .smt import native_terms

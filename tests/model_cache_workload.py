@@ -210,12 +210,16 @@ def quick_sat_profile(n_models: int = 100, n_scenarios: int = 16, n_queries: int
             gpu.put(b, 1)
         MC.STATS.__init__()
         t_ref, t_gpu, agree, hits = [], [], 0, 0
-        for q in queries:
+        slowest = (0.0, -1, {})
+        for qi, q in enumerate(queries):
             t0 = time.perf_counter()
             a = ref.check_quick_sat(q)
             t1 = time.perf_counter()
+            ph0 = dict(MC.STATS.phase_s)
             b = gpu.check_quick_sat(q)
             t2 = time.perf_counter()
+            if t2 - t1 > slowest[0]:
+                slowest = (t2 - t1, qi, {k: round(1e3 * (v - ph0.get(k, 0.0)), 3) for k, v in MC.STATS.phase_s.items()})
             t_ref.append(1e3 * (t1 - t0))
             t_gpu.append(1e3 * (t2 - t1))
             agree += (a is False and b is False) or (
@@ -233,6 +237,11 @@ def quick_sat_profile(n_models: int = 100, n_scenarios: int = 16, n_queries: int
                 "engine_calls": st.engine_calls, "models_on_engine": st.models_engine,
                 "models_by_reference_statement": st.models_host, "leaf_evals": st.leaf_evals,
                 "leaf_evals_native": st.leaf_evals_native,
+                "slowest_query": {"index": slowest[1], "ms": round(1e3 * slowest[0], 3), "phase_ms": slowest[2]},
+                "verdicts": {"memo": st.verdicts_memo, "native": st.verdicts_native, "engine": st.verdicts_engine},
+                "baseline": "reference_loop_ms is the stand-in's loop (tests/mythril_standin.py "
+                            "ModelCache.check_quick_sat: deepcopy + eval per model) over the stand-in z3 "
+                            "(tests/fake_z3.py ModelRef) and Z3WitnessView models, not libz3",
                 "phase_ms_per_query": {k: round(1e3 * v / max(st.queries, 1), 4) for k, v in st.phase_s.items()}}
     finally:
         mp.undo()

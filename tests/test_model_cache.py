@@ -63,11 +63,13 @@ def _check_stream(ns, models, queries):
     return picks
 
 
-@pytest.mark.parametrize("first_stage", [0, 4])
-def test_quick_sat_choice_matches_reference_loop(standin, monkeypatch, first_stage):
-    """first_stage 0: every model in one launch; 4: the production two-launch setting."""
+@pytest.mark.parametrize("first_stage,memo", [(0, True), (4, True), (0, False), (4, False)])
+def test_quick_sat_choice_matches_reference_loop(standin, monkeypatch, first_stage, memo):
+    """first_stage 0: every model in one launch; 4: the production two-launch setting; with
+    and without the per-(model, conjunct) verdict memo."""
     oracle_engine.install(monkeypatch)
     monkeypatch.setattr(MC, "FIRST_STAGE", first_stage)
+    monkeypatch.setattr(MC, "VERDICT_MEMO", memo)
     models, queries, _, _ = W.build(z3, standin, n_models=100, n_scenarios=6, n_queries=30)
     assert len(models) == 100
     picks = _check_stream(standin, models, queries)
@@ -75,10 +77,14 @@ def test_quick_sat_choice_matches_reference_loop(standin, monkeypatch, first_sta
     assert len({p for p in picks if p is not None}) >= 1
 
 
-def test_quick_sat_witness_only_cache(standin, monkeypatch):
+@pytest.mark.parametrize("host_pairs", [0, 256])
+def test_quick_sat_witness_only_cache(standin, monkeypatch, host_pairs):
     """A cache of GPU witnesses only — the live case: every model's leaves native, one
-    launch from the (models, leaves, 8) block — same choices as the reference loop."""
+    launch from the (models, leaves, 8) block (host_pairs 0), or small batches of unknown
+    (model, conjunct) verdicts by the native witness evaluator (256) — same choices as the
+    reference loop."""
     oracle_engine.install(monkeypatch)
+    monkeypatch.setattr(MC, "HOST_VERDICT_PAIRS", host_pairs)
     models, queries, _, _ = W.build(z3, standin, n_models=40, n_scenarios=4, n_queries=20, gpu_frac=1.0,
                                     empty_frac=0.0)
     models = [m for m in models if m.raw and isinstance(m.raw[0], integration.Z3WitnessView)]
@@ -86,7 +92,11 @@ def test_quick_sat_witness_only_cache(standin, monkeypatch):
     MC.STATS.__init__()
     picks = _run_both(standin, models, queries)
     assert picks[-1] is None and any(p is not None for p in picks)
-    assert MC.STATS.models_host == 0 and MC.STATS.leaf_evals == 0 and MC.STATS.leaf_evals_native > 0
+    assert MC.STATS.models_host == 0 and MC.STATS.leaf_evals == 0
+    if host_pairs:
+        assert MC.STATS.verdicts_native > 0 and MC.STATS.verdicts_memo > 0
+    else:
+        assert MC.STATS.leaf_evals_native > 0 and MC.STATS.verdicts_engine > 0 and MC.STATS.verdicts_native == 0
 
 
 def test_quick_sat_small_caches_and_empty(standin, monkeypatch):
@@ -139,7 +149,9 @@ def test_a_model_the_leaves_cannot_value_goes_to_the_reference_statement(standin
             return Picky(self._interp)
 
         def eval(self, e, model_completion=False):
-            if e.decl().kind() == z3.Z3_OP_SELECT:
+            # rejects the leaf forms (a select, or the leaves' concatenation of the batched
+            # evaluation), accepts the whole query
+            if e.decl().kind() in (z3.Z3_OP_SELECT, z3.Z3_OP_CONCAT):
                 raise z3.Z3Exception("no")
             return super().eval(e, model_completion)
 
@@ -491,3 +503,42 @@ def test_gpu_witness_leaves_native_equal_python(standin, engine):
         w = wms[j].w
         for t, limbs in zip(leaves, r):
             assert native_terms.ints_of(limbs[None])[0] == w.leaf_value(t) & T.M(max(t.width, 1)), t
+
+
+@pytest.mark.parametrize("batched", [True, False])
+def test_completion_shared_between_leaves_matches_whole_conjunction(standin, monkeypatch, batched):
+    """z3's model completion ADDS interpretations to the model it evaluates on (fake_z3
+    ModelRef does the same), so evaluating a query's leaves one by one on one private copy —
+    or all of them in one eval of their concatenation — could in principle differ from the
+    reference's single eval of the whole conjunction (support_utils.py:62-63) when leaves
+    share symbols the model does not interpret.  Models here interpret only some of the
+    symbols the queries read (a scalar, an array, a function), the queries read the
+    uninterpreted ones through several leaves, and the choice must equal the reference
+    loop's on every query, per leaf and batched."""
+    oracle_engine.install(monkeypatch)
+    monkeypatch.setattr(MC, "FIRST_STAGE", 0)
+    if not batched:
+        orig = MC._z3_leaf_evaluators
+        monkeypatch.setattr(MC, "_z3_leaf_evaluators", lambda z, im: (orig(z, im)[0], None))
+    x, y = z3.BitVec("x", 256), z3.BitVec("y", 256)
+    A = z3.Array("A", z3.BitVecSort(256), z3.BitVecSort(256))
+    f = z3.Function("f", z3.BitVecSort(256), z3.BitVecSort(256))
+    V = lambda v: z3.BitVecVal(v, 256)  # noqa: E731
+    models = [standin.Model([z3.ModelRef(interp)]) for interp in (
+        {},                                          # nothing interpreted
+        {x.decl(): 3},                               # x only
+        {y.decl(): 4, A.decl(): ({4: 9}, 2)},        # y and A
+        {A.decl(): ({0: 1}, 0), f: ({(5,): 6}, 7)},
+        {x.decl(): 0, y.decl(): 0},
+    )]
+    queries = [
+        z3.And(z3.Select(A, y) == V(0), y == V(0)),                    # completes y, A
+        z3.And(z3.Select(A, y + V(1)) == z3.Select(A, y), x == V(0)),
+        z3.And(f(y) == f(V(0)), z3.Select(A, x) == V(0)),
+        z3.And(f(x) == V(0), z3.ULT(y, V(5)), z3.Select(A, y) == V(9)),
+        z3.And(z3.Select(A, x) == V(1), f(V(5)) == V(6)),
+        z3.And(f(x + y) == f(y + x), z3.Select(A, V(4)) == V(2)),
+        z3.And(y == V(1), y == V(2)),                                   # no model
+    ]
+    picks = _run_both(standin, models, [z3.simplify(q) for q in queries])
+    assert picks[-1] is None and sum(p is not None for p in picks) >= 3
