@@ -271,29 +271,84 @@ struct NodeKeyHash {
     }
 };
 
+// Hash-consing table of a DAG: open addressing over node ids (the key is the node itself),
+// linear probing, grown at half load.  A std::unordered_map<NodeKey, id> allocated one
+// 80-byte node per DAG node and, reserved for 4,096 entries per job, zeroed a 32 KB bucket
+// array for buckets of a few dozen nodes — allocation churn that was a large share of a
+// single query's lowering.
+struct NodeTable {
+    std::vector<int32_t> slot;   // -1 = empty
+    size_t used = 0;
+    void clear() { std::vector<int32_t>().swap(slot); used = 0; }
+};
+
+inline uint64_t node_hash(uint32_t kind, uint32_t width, uint32_t nargs, const int32_t* args, uint32_t aux,
+                          bool is_bool, const C8* cv) {
+    uint64_t h = 0x9E3779B97F4A7C15ull;
+    auto mix = [&](uint32_t w) { h = (h ^ w) * 0x100000001B3ull; };
+    mix(kind);
+    mix(width);
+    mix(nargs);
+    mix(aux);
+    for (uint32_t i = 0; i < nargs; i++) mix((uint32_t)args[i]);
+    mix(is_bool ? 1u : 0u);
+    if (kind == K_CONST)  // a constant without a value given is the zero constant
+        for (int i = 0; i < 8; i++) mix(cv ? cv->l[i] : 0u);
+    return h ^ (h >> 29);
+}
+
 struct Dag {
     std::vector<DNode> nodes;
     std::vector<int32_t> roots;
     std::vector<DVar> vars;
     std::vector<C8> forced;
-    std::unordered_map<NodeKey, int32_t, NodeKeyHash> memo;
+    NodeTable memo;
     std::unordered_map<std::string, int32_t> var_index;
 
-    explicit Dag(size_t reserve = 4096) { memo.reserve(reserve); }
+    explicit Dag(size_t reserve = 64) {
+        size_t cap = 16;
+        while (cap < 2 * reserve) cap <<= 1;
+        memo.slot.assign(cap, -1);
+        nodes.reserve(reserve);
+    }
+
+    bool same(const DNode& n, uint32_t kind, uint32_t width, const int32_t* args, uint32_t nargs, uint32_t aux,
+              bool is_bool, const C8* cv) const {
+        if (n.kind != kind || n.width != width || n.nargs != nargs || n.aux != aux || n.is_bool != is_bool) return false;
+        for (uint32_t i = 0; i < nargs; i++)
+            if (n.args[i] != args[i]) return false;
+        if (kind == K_CONST) {
+            static const C8 zero{};
+            return memcmp(n.cv.l, (cv ? cv : &zero)->l, sizeof(n.cv.l)) == 0;
+        }
+        return true;
+    }
+
+    void grow() {
+        std::vector<int32_t> old;
+        old.swap(memo.slot);
+        memo.slot.assign(old.size() * 2, -1);
+        const size_t mask = memo.slot.size() - 1;
+        for (int32_t id : old) {
+            if (id < 0) continue;
+            const DNode& n = nodes[(size_t)id];
+            size_t h = (size_t)node_hash(n.kind, n.width, n.nargs, n.args, n.aux, n.is_bool, &n.cv) & mask;
+            while (memo.slot[h] >= 0) h = (h + 1) & mask;
+            memo.slot[h] = id;
+        }
+    }
 
     int32_t add_n(uint32_t kind, uint32_t width, const int32_t* args, uint32_t nargs, uint32_t aux,
                   bool is_bool, const C8* cv = nullptr) {
-        NodeKey k;
-        memset(&k, 0, sizeof(k));
-        k.kind = kind;
-        k.width = width;
-        k.nargs = nargs;
-        for (uint32_t i = 0; i < nargs; i++) k.args[i] = args[i];
-        k.aux = aux;
-        k.is_bool = is_bool ? 1u : 0u;
-        if (cv && kind == K_CONST) k.cv = *cv;
-        auto it = memo.find(k);
-        if (it != memo.end()) return it->second;
+        if (memo.slot.empty()) memo.slot.assign(16, -1);
+        const size_t mask = memo.slot.size() - 1;
+        size_t h = (size_t)node_hash(kind, width, nargs, args, aux, is_bool, cv) & mask;
+        for (;;) {
+            const int32_t id = memo.slot[h];
+            if (id < 0) break;
+            if (same(nodes[(size_t)id], kind, width, args, nargs, aux, is_bool, cv)) return id;
+            h = (h + 1) & mask;
+        }
         DNode n;
         memset(&n, 0, sizeof(n));
         n.kind = kind;
@@ -305,7 +360,8 @@ struct Dag {
         n.is_bool = is_bool;
         const int32_t id = (int32_t)nodes.size();
         nodes.push_back(n);
-        memo.emplace(k, id);
+        memo.slot[h] = id;
+        if (2 * ++memo.used > memo.slot.size()) grow();
         return id;
     }
 
@@ -1590,8 +1646,32 @@ void emit_program(Dag& d, Result* R) {
 
 // One bucket: terms -> DAG -> hints -> program (pflt_lower).  Reads the store only, so
 // buckets lower concurrently (pflt_lower_many).  Never throws: a failure is R->rc / R->err.
+#ifdef PFLT_PROFILE
+// phase timers of lower_job (profiling builds only, tools/lower_profile.py): ns per phase,
+// summed over every job, printed at exit
+#include <atomic>
+#include <chrono>
+static std::atomic<uint64_t> g_prof_ns[6];
+static const char* g_prof_names[6] = {"setup", "term->dag", "hints", "emit", "result", "jobs"};
+struct ProfPrint {
+    ~ProfPrint() {
+        for (int i = 0; i < 6; i++) fprintf(stderr, "pflt_prof %s %llu\n", g_prof_names[i], (unsigned long long)g_prof_ns[i].load());
+    }
+} g_prof_print;
+static inline uint64_t prof_now() {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+        std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+#define PROF_LAP(k) do { const uint64_t t_ = prof_now(); g_prof_ns[k] += t_ - t_lap; t_lap = t_; } while (0)
+#else
+#define PROF_LAP(k) ((void)0)
+#endif
 Result* lower_job(const Store& S, const std::vector<uint32_t>& rs, const Parents& P, const uint32_t* registry,
                   size_t n_registry, uint32_t flags) {
+#ifdef PFLT_PROFILE
+    uint64_t t_lap = prof_now();
+    g_prof_ns[5] += 1;
+#endif
     Result* R = new Result();
     R->in_roots = rs;
     R->parented = !P.empty();
@@ -1635,7 +1715,9 @@ Result* lower_job(const Store& S, const std::vector<uint32_t>& rs, const Parents
             if (S.t[r].depth > PF_MAX_TERM_DEPTH)
                 lerr("term nested %u deep (more than %u): left to z3", S.t[r].depth, (unsigned)PF_MAX_TERM_DEPTH);
         }
+        PROF_LAP(0);
         L.lower(rs);
+        PROF_LAP(1);
         R->var_terms = L.var_terms;
         R->uf_apps = L.uf_apps;
         for (const std::string& name : L.array_order) {
@@ -1673,17 +1755,20 @@ Result* lower_job(const Store& S, const std::vector<uint32_t>& rs, const Parents
                 d.vars[i].has_parent = true;
             }
         }
+        PROF_LAP(2);
         if (flags & PFLT_PROGRAM) {
             emit_program(d, R);
         } else {
             pack(d, &R->packed_nodes, &R->pool);
         }
+        PROF_LAP(3);
         for (const DVar& v : d.vars) {
             R->names += v.name;
             R->names.push_back('\0');
         }
         R->dag = std::move(L.d);
-        decltype(R->dag.memo)().swap(R->dag.memo);  // the hash-consing table is done with
+        R->dag.memo.clear();  // the hash-consing table is done with
+        PROF_LAP(4);
         return R;
     } catch (const TermError& e) {
         R->rc = e.rc;
@@ -2087,7 +2172,7 @@ void synth_dag(uint32_t dag_id, bool plant, const double* cdf, Result* R, std::v
     }
     R->parented = plant;
     R->dag = std::move(d);
-    decltype(R->dag.memo)().swap(R->dag.memo);
+    R->dag.memo.clear();
 }
 
 }  // namespace

@@ -691,6 +691,15 @@ def _resolve(batch: List[int], conjs: Sequence[T.Term], leaf_values, engine, nov
             todo[j] = ks
     if not todo:
         return 0, 0
+    t_r = time.perf_counter()
+
+    def sub_phase(name):
+        nonlocal t_r
+        now = time.perf_counter()
+        with _STATS_LOCK:
+            STATS.phase_s[name] = STATS.phase_s.get(name, 0.0) + now - t_r
+        t_r = now
+
     natives = [j for j in todo if isinstance(leaf_values[j], NativeLeafValues)]
     if natives and HOST_VERDICT_PAIRS > 0:
         ks = sorted({k for j in natives for k in todo[j]})
@@ -718,6 +727,7 @@ def _resolve(batch: List[int], conjs: Sequence[T.Term], leaf_values, engine, nov
                         del todo[j]
             with _STATS_LOCK:
                 STATS.verdicts_native += n_done
+            sub_phase("eval.native_verdicts")
     if not todo:
         return 0, 0
     js = list(todo)
@@ -736,9 +746,11 @@ def _resolve(batch: List[int], conjs: Sequence[T.Term], leaf_values, engine, nov
                 continue
             rows.append(r)
             on.append(j)
+    sub_phase("eval.rows")
     if not on:
         return 0, 0
     flags = eval_rows_each(sub, rows, len(sub_leaves), engine)
+    sub_phase("eval.engine")
     for m, j in enumerate(on):
         vd = leaf_values[j].verdicts
         for q, k in enumerate(ks):
@@ -750,14 +762,16 @@ def _resolve(batch: List[int], conjs: Sequence[T.Term], leaf_values, engine, nov
 
 def _choose_memo(conjs: Sequence[T.Term], leaf_values, reference, engine, k1, lap, t):
     """choose() over the per-(model, conjunct) memo: (choice, host, launches, models on the
-    engine).  Models are walked newest first; an undecided model and the next ones (up to
-    the (k1 + 1)-th with dear leaves the first time, all the rest after) are resolved as one
-    batch, so the answer is the reference loop's: the first model in the order that holds."""
+    engine).  Models are walked newest first; an undecided model and the next ones up to the
+    (k + 1)-th with dear leaves are resolved as one batch — k = k1 the first time, four times
+    as many each time after (natively held witnesses ride along), so a deep answer costs a
+    few launches and at most ~4x the dear models the reference loop would evaluate — and the
+    answer is the reference loop's: the first model in the order that holds."""
     n = len(leaf_values)
     host = launches = on_engine_n = 0
     noval: set = set()
     memo_hits = 0
-    first = True
+    kk = k1
     i = 0
     choice = None
     while i < n:
@@ -779,8 +793,8 @@ def _choose_memo(conjs: Sequence[T.Term], leaf_values, reference, engine, k1, la
             i += 1
             continue
         rest = leaf_values[i:]
-        end = i + (first_stage_end(rest, k1) if first else len(rest))
-        first = False
+        end = i + first_stage_end(rest, kk)
+        kk *= 4
         batch = [j for j in range(i, max(end, i + 1))
                  if leaf_values[j] is not None and j not in noval and _memo_status(leaf_values[j], conjs) is None]
         t = lap("leaves", t)
