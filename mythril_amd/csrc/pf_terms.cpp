@@ -23,6 +23,7 @@
 #include <cstring>
 #include <atomic>
 #include <list>
+#include <deque>
 #include <map>
 #include <string>
 #include <thread>
@@ -584,10 +585,52 @@ struct VarTerm {
     uint32_t c;     // extract hi
 };
 
+// term id -> Val memo of a lowering: open addressing over the term ids, values in a deque (a
+// reference handed out stays valid while the table grows, as with the node-based map this
+// replaces, without its per-entry allocation)
+struct ValMemo {
+    std::vector<uint32_t> key;   // term id + 1, 0 = empty
+    std::vector<uint32_t> idx;
+    std::deque<Val> vals;
+    ValMemo() : key(64, 0u), idx(64, 0u) {}
+    static size_t hsh(uint32_t t) { return (size_t)((t * 0x9E3779B1u) ^ (t >> 15)); }
+    Val* find(uint32_t t) {
+        const size_t mask = key.size() - 1;
+        for (size_t h = hsh(t) & mask;; h = (h + 1) & mask) {
+            if (key[h] == 0u) return nullptr;
+            if (key[h] == t + 1u) return &vals[idx[h]];
+        }
+    }
+    Val& put(uint32_t t, Val&& v) {
+        if (2 * (vals.size() + 1) > key.size()) {
+            std::vector<uint32_t> ok, oi;
+            ok.swap(key);
+            oi.swap(idx);
+            key.assign(ok.size() * 2, 0u);
+            idx.assign(ok.size() * 2, 0u);
+            const size_t m2 = key.size() - 1;
+            for (size_t i = 0; i < ok.size(); i++) {
+                if (!ok[i]) continue;
+                size_t h = hsh(ok[i] - 1u) & m2;
+                while (key[h]) h = (h + 1) & m2;
+                key[h] = ok[i];
+                idx[h] = oi[i];
+            }
+        }
+        const size_t mask = key.size() - 1;
+        size_t h = hsh(t) & mask;
+        while (key[h]) h = (h + 1) & mask;
+        key[h] = t + 1u;
+        idx[h] = (uint32_t)vals.size();
+        vals.push_back(std::move(v));
+        return vals.back();
+    }
+};
+
 struct Lowering {
     const Store& S;
     Dag d;
-    std::unordered_map<uint32_t, Val> memo;
+    ValMemo memo;
     std::vector<VarTerm> var_terms;
     // base array name -> [(idx id, arr id, idx node, value node)]; names in insertion order
     std::vector<std::string> array_order;
@@ -696,10 +739,11 @@ struct Lowering {
 
     // ---- generic lowering -----------------------------------------------------------
     const Val& w(uint32_t t) {
-        auto it = memo.find(t);
-        if (it != memo.end()) return it->second;
+        if (const Val* hit = memo.find(t)) return *hit;
         Val v = lower_bv(t);
-        return memo.emplace(t, std::move(v)).first->second;
+        // lower_bv may have put t itself (a recursive path to the same term): keep the first
+        if (const Val* hit = memo.find(t)) return *hit;
+        return memo.put(t, std::move(v));
     }
 
     int32_t node(uint32_t t) {
@@ -709,10 +753,10 @@ struct Lowering {
     }
 
     int32_t b(uint32_t t) {
-        auto it = memo.find(t);
-        if (it != memo.end()) return it->second.node;
+        if (const Val* hit = memo.find(t)) return hit->node;
         const int32_t n = lower_bool(t);
-        memo.emplace(t, Val{false, n, {}});
+        if (const Val* hit = memo.find(t)) return hit->node;
+        memo.put(t, Val{false, n, {}});
         return n;
     }
 
