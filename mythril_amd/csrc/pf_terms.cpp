@@ -295,7 +295,12 @@ inline uint64_t node_hash(uint32_t kind, uint32_t width, uint32_t nargs, const i
     mix(is_bool ? 1u : 0u);
     if (kind == K_CONST)  // a constant without a value given is the zero constant
         for (int i = 0; i < 8; i++) mix(cv ? cv->l[i] : 0u);
-    return h ^ (h >> 29);
+    // fmix64: the table indexes with the low bits, which the FNV products alone spread poorly
+    h ^= h >> 33;
+    h *= 0xff51afd7ed558ccdull;
+    h ^= h >> 33;
+    h *= 0xc4ceb9fe1a85ec53ull;
+    return h ^ (h >> 33);
 }
 
 struct Dag {
