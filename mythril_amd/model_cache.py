@@ -593,7 +593,7 @@ def choose(query: T.Term, leaf_values: Sequence[Optional[LeafValues]],
 # their newest conjuncts, so after the first query of a path most of the work is one new
 # conjunct under the few models the old conjuncts leave standing.  The unknown pairs of a
 # batch of models go in one engine launch (only the programs of the unknown conjuncts, over
-# only those models' rows); a batch of natively held GPU witnesses with at most
+# only those models' rows); a batch of natively held GPU witnesses alone with at most
 # HOST_VERDICT_PAIRS unknown pairs is evaluated by the native witness evaluator instead
 # (csrc/pf_recheck.cpp: the interpretation Z3WitnessView.eval applies, natively) — for a few
 # pairs the launch's fixed cost dominates.  PF_QS_MEMO=0 restores the all-models launches;
@@ -701,7 +701,10 @@ def _resolve(batch: List[int], conjs: Sequence[T.Term], leaf_values, engine, nov
         t_r = now
 
     natives = [j for j in todo if isinstance(leaf_values[j], NativeLeafValues)]
-    if natives and HOST_VERDICT_PAIRS > 0:
+    # only a batch of natives alone: with dear models in it the launch is made anyway, and
+    # the witnesses ride in it (measured, profiles/r06_quick_sat.md: the mixed cache's
+    # slowest query 23 ms that way against 77-88 ms with the witnesses taken natively first)
+    if natives and len(natives) == len(todo) and HOST_VERDICT_PAIRS > 0:
         ks = sorted({k for j in natives for k in todo[j]})
         if len(natives) * len(ks) <= HOST_VERDICT_PAIRS:
             from .smt import native_terms

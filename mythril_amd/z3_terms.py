@@ -106,7 +106,9 @@ class Z3Converter:
     def ast_of(self, t: T.Term):
         """A z3 AST for a term: the AST it was converted from, else (for the leaf terms the
         explicit lowering synthesises — a base-array read below a store chain, a 256-bit
-        chunk of a wide UF application — and for bare symbols) one built from its parts."""
+        chunk of a wide UF application — and for bare symbols) one built from its parts and
+        kept, so the same term always gets the same AST (a model's ``eval`` then shares its
+        subterms across leaves instead of re-walking a fresh copy per call)."""
         with self._lock:
             a = self._rev.get(t)
         if a is not None:
@@ -114,19 +116,23 @@ class Z3Converter:
         z3 = self.z3
         op = t.op
         if op == "select":
-            return z3.Select(self.ast_of(t.args[0]), self.ast_of(t.args[1]))
-        if op == "extract":
+            a = z3.Select(self.ast_of(t.args[0]), self.ast_of(t.args[1]))
+        elif op == "extract":
             hi, lo = t.val
-            return z3.Extract(hi, lo, self.ast_of(t.args[0]))
-        if op == "var":
-            return z3.BitVec(t.val, t.width)
-        if op == "bvar":
-            return z3.Bool(t.val)
-        if op == "array":
-            return z3.Array(t.val, z3.BitVecSort(t.sort[1]), z3.BitVecSort(t.sort[2]))
-        if op == "bv":
-            return z3.BitVecVal(t.val, t.width)
-        raise LoweringError(f"no z3 AST for a {op} term")
+            a = z3.Extract(hi, lo, self.ast_of(t.args[0]))
+        elif op == "var":
+            a = z3.BitVec(t.val, t.width)
+        elif op == "bvar":
+            a = z3.Bool(t.val)
+        elif op == "array":
+            a = z3.Array(t.val, z3.BitVecSort(t.sort[1]), z3.BitVecSort(t.sort[2]))
+        elif op == "bv":
+            a = z3.BitVecVal(t.val, t.width)
+        else:
+            raise LoweringError(f"no z3 AST for a {op} term")
+        with self._lock:
+            self._store(a, t)
+        return a
 
     def terms(self, es) -> List[T.Term]:
         with self._lock:
