@@ -378,10 +378,6 @@ PF_INL u256 gen_var(const SetCtx& S, uint32_t v, uint32_t cand) {
         const uint4 r1b = philox_gen(p0b, v, 1u, S.k0, S.k1);
         m.w ^= (mb.w ^ r0b.x ^ r1b.y) & hzp;
     }
-#elif defined(PF_PROBE_GEN_NOM)  // timing probe only (other witnesses): no strategy block
-    const uint4 rq = philox_gen(p0, v, 0u, S.k0, S.k1);
-    const uint4 m = make_uint4(__builtin_amdgcn_alignbit(rq.y, rq.z, 13u) ^ rq.w, __builtin_amdgcn_alignbit(rq.w, rq.x, 7u) ^ rq.z,
-                               __builtin_amdgcn_alignbit(rq.x, rq.y, 19u) ^ rq.w, __builtin_amdgcn_alignbit(rq.z, rq.w, 11u) ^ rq.x);
 #else
     const uint4 m = philox_gen(p0, v, 2u, S.k0, S.k1);
 #endif
@@ -451,32 +447,6 @@ PF_INL u256 gen_var(const SetCtx& S, uint32_t v, uint32_t cand) {
         out.l[0] = r0.x & 1u;
     } else {
         const uint32_t sel = m.x & 15u;
-        // boundary arm (sel 5..8): {0, 1, 2, 3, 2^w-1, 2^w-2, 2^(w-1), 2^(w-1)-1, 2^k, 2^k-1,
-        // 2^k+1, 2^160-1}[j] mod 2^w as one formula, (j >= 6 ? 2^p : 0) + delta
-        // one power of two serves both the boundary arm (2^p) and the parent-mutation arm
-        // (2^k, k = m[2] % w): a lane takes one arm, so the exponent is selected per lane
-        // (w is uniform; a power of two — every 256-bit variable — needs no division)
-        const uint32_t j = m.y % 12u, k = (w & (w - 1u)) == 0u ? (m.z & (w - 1u)) : m.z % w;
-        const uint32_t p = j <= 7u ? w - 1u : (j <= 10u ? k : 160u);
-        const u256 pw = pow2(sel <= 8u ? p : k);
-#ifndef PF_GEN_ARMS_OLD
-        // The boundary arm (2^p or 0, plus a small delta) and the constant arm (const +0/+1/-1)
-        // are each "a base plus a signed 32-bit delta", and a lane takes one arm: their bases go
-        // through the per-lane select with the other arms' (whose delta is 0) and ONE 256-bit
-        // add of the selected delta, sign-extended, follows — values bit for bit as the two
-        // adds of the contract's wording (tests/test_generator.py, GPU parity)
-        // delta by j, 3 bits per entry biased by 2 (a ternary chain here became a divergent
-        // if-chain): j 0..11 -> 0 1 2 3 -1 -2 0 -1 0 -1 1 -1
-        const int32_t d_bnd = (int32_t)((PF_BND_DELTA >> (3u * j)) & 7ull) - 2;
-        const uint32_t usepow = j >= 6u ? 0xffffffffu : 0u;
-        int32_t d_cst = 0;
-        if (S.n_const > 0u) {  // uniform; without constants the arm is the uniform value
-            const uint32_t dsel = m.z % 3u;  // +0, +1, -1
-            d_cst = dsel == 0u ? 0 : (dsel == 1u ? 1 : -1);
-        }
-        const bool cst_const = S.n_const > 0u;
-        const int32_t delta = sel <= 4u ? 0 : (sel <= 8u ? d_bnd : (sel <= 11u ? d_cst : 0));
-#else
         // constant +-1 arm (sel 9..11)
         u256 cst = rv;
         if (S.n_const > 0u) {
@@ -487,8 +457,18 @@ PF_INL u256 gen_var(const SetCtx& S, uint32_t v, uint32_t cand) {
             for (int i = 1; i < 8; i++) dl.l[i] = dsel == 2u ? 0xffffffffu : 0u;
             cst = pf::add256(g, dl);
         }
+        // boundary arm (sel 5..8): {0, 1, 2, 3, 2^w-1, 2^w-2, 2^(w-1), 2^(w-1)-1, 2^k, 2^k-1,
+        // 2^k+1, 2^160-1}[j] mod 2^w as one formula, (j >= 6 ? 2^p : 0) + delta
+        // one power of two serves both the boundary arm (2^p) and the parent-mutation arm
+        // (2^k, k = m[2] % w): a lane takes one arm, so the exponent is selected per lane
+        // (w is uniform; a power of two — every 256-bit variable — needs no division)
+        const uint32_t j = m.y % 12u, k = (w & (w - 1u)) == 0u ? (m.z & (w - 1u)) : m.z % w;
+        const uint32_t p = j <= 7u ? w - 1u : (j <= 10u ? k : 160u);
+        const u256 pw = pow2(sel <= 8u ? p : k);
         u256 bnd;
         {
+            // delta by j, 3 bits per entry biased by 2 (a ternary chain here became a
+            // divergent if-chain): j 0..11 -> 0 1 2 3 -1 -2 0 -1 0 -1 1 -1
             const int32_t delta = (int32_t)((PF_BND_DELTA >> (3u * j)) & 7ull) - 2;
             u256 base = pw;
             const uint32_t usepow = j >= 6u ? 0xffffffffu : 0u;
@@ -500,7 +480,6 @@ PF_INL u256 gen_var(const SetCtx& S, uint32_t v, uint32_t cand) {
             for (int i = 0; i < 8; i++) base.l[i] &= usepow;
             bnd = pf::add256(base, dl);
         }
-#endif
         // parent-mutation arm (sel 12..13): one bit of the parent flipped in a quarter of
         // the lanes; without a parent, a random byte
         u256 mut = pf::zero256();
@@ -514,27 +493,6 @@ PF_INL u256 gen_var(const SetCtx& S, uint32_t v, uint32_t cand) {
         // small arm (sel 14..15): 1..16 random low bits
         const uint32_t nb = 1u + (m.y & 15u);
         const uint32_t small = r0.x & ((nb >= 32u) ? 0xffffffffu : ((1u << nb) - 1u));
-#ifndef PF_GEN_ARMS_OLD
-        {
-            u256 base;
-#pragma unroll
-            for (int i = 0; i < 8; i++) {
-                const uint32_t sm = i == 0 ? small : 0u;
-                base.l[i] = sel <= 4u ? rv.l[i]
-                          : (sel <= 8u ? (pw.l[i] & usepow)
-                                       : (sel <= 11u ? (cst_const ? g.l[i] : rv.l[i]) : (sel <= 13u ? mut.l[i] : sm)));
-            }
-            u256 dl;
-            dl.l[0] = (uint32_t)delta;
-            const uint32_t fill = delta < 0 ? 0xffffffffu : 0u;
-#pragma unroll
-            for (int i = 1; i < 8; i++) dl.l[i] = fill;
-            out = pf::add256(base, dl);
-            // the actor set (transaction/symbolic.py:215) in most lanes
-#pragma unroll
-            for (int i = 0; i < 8; i++) out.l[i] = act ? g.l[i] : out.l[i];
-        }
-#else
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             const uint32_t sm = i == 0 ? small : 0u;
@@ -543,7 +501,6 @@ PF_INL u256 gen_var(const SetCtx& S, uint32_t v, uint32_t cand) {
             // the actor set (transaction/symbolic.py:215) in most lanes
             out.l[i] = act ? g.l[i] : out.l[i];
         }
-#endif
 #ifndef PF_DIAG_NO_LASER_ARMS  // timing probe only: the LASER-aware arms compiled out
         if (kind == PF_VK_VALUE) {  // uniform: call values are 0 in half the lanes
 #pragma unroll
