@@ -260,6 +260,19 @@ struct Node {
 };
 bool is_leaf(uint32_t k) { return k >= PFL_K_VAR && k <= PFL_K_BVAR; }
 
+// Adjacency lists in compressed-row form: row r is idx[off[r] .. off[r + 1]) — two allocations
+// for the whole DAG where a vector per node cost one each (the hint solver runs per bucket,
+// and a single query's lowering spent ~16 % of its samples in the allocator)
+struct Csr {
+    std::vector<int> off, idx;
+    struct Row {
+        const int *b, *e;
+        const int* begin() const { return b; }
+        const int* end() const { return e; }
+    };
+    Row operator[](size_t r) const { return Row{idx.data() + off[r], idx.data() + off[r + 1]}; }
+};
+
 class Seeder {
    public:
     static constexpr int MAX_CHOICES = 4096;
@@ -269,16 +282,33 @@ class Seeder {
            const U* soft)
         : N(nodes), nn(nn), pool(pool), vw(widths, widths + nv), soft(soft, soft + nv), nv(nv),
           has_bits(nv, 0), bits_v(nv), bits_m(nv), has_rng(nv, 0), rng_lo(nv), rng_hi(nv),
-          memo(nn), have(nn, 0), users(nn), leaf(nv), hv(nn, -1) {
-        for (size_t i = 0; i < nn; i++) {
-            const Node& n = N[i];
-            for (uint32_t k = 0; k < n.nargs; k++) {
-                bool dup = false;
-                for (uint32_t j = 0; j < k; j++) dup |= n.args[j] == n.args[k];
-                if (!dup) users[n.args[k]].push_back((int)i);
+          memo(nn), have(nn, 0), hv(nn, -1) {
+        // two passes per list: counts, then each row filled in node order (the order the
+        // per-node vectors had)
+        users.off.assign(nn + 1, 0);
+        leaf.off.assign(nv + 1, 0);
+        auto each_user = [&](auto&& f) {
+            for (size_t i = 0; i < nn; i++) {
+                const Node& n = N[i];
+                for (uint32_t k = 0; k < n.nargs; k++) {
+                    bool dup = false;
+                    for (uint32_t j = 0; j < k; j++) dup |= n.args[j] == n.args[k];
+                    if (!dup) f(n.args[k], (int)i);
+                }
             }
-            if (n.kind == PFL_K_VAR || n.kind == PFL_K_BVAR) leaf[n.aux].push_back((int)i);
-        }
+        };
+        each_user([&](uint32_t a, int) { users.off[a + 1]++; });
+        for (size_t i = 0; i < nn; i++)
+            if (N[i].kind == PFL_K_VAR || N[i].kind == PFL_K_BVAR) leaf.off[N[i].aux + 1]++;
+        for (size_t r = 0; r < nn; r++) users.off[r + 1] += users.off[r];
+        for (size_t r = 0; r < nv; r++) leaf.off[r + 1] += leaf.off[r];
+        users.idx.resize(users.off[nn]);
+        leaf.idx.resize(leaf.off[nv]);
+        std::vector<int> fill(users.off.begin(), users.off.end() - 1);
+        each_user([&](uint32_t a, int i) { users.idx[fill[a]++] = i; });
+        fill.assign(leaf.off.begin(), leaf.off.end() - 1);
+        for (size_t i = 0; i < nn; i++)
+            if (N[i].kind == PFL_K_VAR || N[i].kind == PFL_K_BVAR) leaf.idx[fill[N[i].aux]++] = (int)i;
     }
 
     std::vector<U> run(const uint32_t* roots, size_t n_roots, int* n_sat) {
@@ -336,7 +366,7 @@ class Seeder {
     bool force = false;
     std::vector<U> memo;
     std::vector<char> have;
-    std::vector<std::vector<int>> users, leaf;
+    Csr users, leaf;
     std::vector<signed char> hv;                      // has_var memo: -1 unknown
     std::vector<int> ev_stack, ch_stack, hv_stack;    // scratch (none of these recurse)
     std::vector<int> rs_leaves, rs_stack;
