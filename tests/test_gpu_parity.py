@@ -580,3 +580,47 @@ def test_forwarding_chains_match_oracle(engine):
         want = _oracle_first(p, budget, seed)
         got = None if res.found[i] == 0xFFFFFFFF else int(res.found[i])
         assert got == want, (i, got, want)
+
+
+_WIDTHS = (1, 8, 32, 64, 160, 256)
+
+
+@pytest.mark.parametrize("w", _WIDTHS)
+def test_every_op_at_laser_widths(engine, w):
+    """Every arithmetic op and compare at the widths LASER's terms take — a Bool-sized bit
+    vector, calldata bytes, 32/64-bit words, 160-bit addresses, full words — 384 seeded
+    operand pairs each (boundary values, short random values, powers of two ± 1, uniform),
+    GPU against the oracle; each pair also with a corrupted expectation, which must fail."""
+    fns = {"add": O.bvadd, "sub": O.bvsub, "mul": O.bvmul, "udiv": O.bvudiv, "urem": O.bvurem,
+           "sdiv": O.bvsdiv, "srem": O.bvsrem, "smod": O.bvsmod, "shl": O.bvshl,
+           "lshr": O.bvlshr, "ashr": O.bvashr, "exp": O.bvexp}
+    M = ir.mask(w)
+
+    def cmp(name, a, b):
+        sa = a - (1 << w) if a >> (w - 1) else a
+        sb = b - (1 << w) if b >> (w - 1) else b
+        return int({"ult": a < b, "ule": a <= b, "slt": sa < sb, "sle": sa <= sb,
+                    "uadd_noovf": a + b <= M, "umul_noovf": a * b <= M}[name])
+
+    names = sorted(fns) + sorted(_CMPS)
+    progs = [_op_program(n, w) for n in names]
+    db = engine.upload(progs)
+    rng = np.random.default_rng(0xB175 + w)
+    for s, name in enumerate(names):
+        cands = []
+        for _ in range(384):
+            a, b = _rand_operand(rng, w), _rand_operand(rng, w)
+            if name in ("shl", "lshr", "ashr") and rng.random() < 0.6:
+                b = int(rng.integers(0, w + 2)) & M
+            if name in fns:
+                r = fns[name](a, b, w)
+                cands.append([a, b, r])
+                cands.append([a, b, r ^ (1 << int(rng.integers(0, w)))])
+            else:
+                r = cmp(name, a, b)
+                cands.append([a, b, r])
+                cands.append([a, b, r ^ 1])
+        got = engine.eval_assignments(db, s, ir.pack_assignments(progs[s], cands))
+        want = np.array([i % 2 == 0 for i in range(len(cands))])
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, (name, w, [[hex(v) for v in cands[i]] for i in bad[:3]])
