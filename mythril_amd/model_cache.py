@@ -318,6 +318,9 @@ _EMPTY_REG = _EmptyRegistry()
 
 # ---- per-model leaf values --------------------------------------------------------------
 
+LEAF_VALS_MAX = 1 << 15
+
+
 class LeafValues:
     """One cached model's values of leaf terms, each computed once and kept as the 32 bytes
     (little-endian) of its row in pf_eval_assignments' input.
@@ -346,6 +349,8 @@ class LeafValues:
         """The values of ``leaves`` as one byte row; None if the model's evaluator rejects
         one of them."""
         vals = self.vals
+        if len(vals) > LEAF_VALS_MAX:   # bounded like the verdict memo: values are recomputable
+            vals.clear()
         missing = [t for t in dict.fromkeys(leaves) if t not in vals]
         if len(missing) > 1 and self.evaluate_many is not None:
             try:
@@ -602,6 +607,11 @@ VERDICT_MEMO = os.environ.get("PF_QS_MEMO", "1") != "0"
 HOST_VERDICT_PAIRS = int(os.environ.get("PF_QS_HOST_PAIRS", "256"))
 
 
+# a model's verdict memo is cleared past this many conjuncts (a long analysis poses tens of
+# thousands; the verdicts are recomputable, the memory of 100 models x all of them is not)
+VERDICTS_MAX = 1 << 14
+
+
 def _memo_status(lv: Optional[LeafValues], conjs: Sequence[T.Term]) -> Optional[bool]:
     """False if a conjunct is known false under the model, True if every one is known true,
     else None (some unknown)."""
@@ -691,6 +701,10 @@ def _resolve(batch: List[int], conjs: Sequence[T.Term], leaf_values, engine, nov
             todo[j] = ks
     if not todo:
         return 0, 0
+    for j in todo:
+        if len(leaf_values[j].verdicts) > VERDICTS_MAX:
+            leaf_values[j].verdicts.clear()
+            todo[j] = list(range(len(conjs)))
     t_r = time.perf_counter()
 
     def sub_phase(name):

@@ -542,3 +542,18 @@ def test_completion_shared_between_leaves_matches_whole_conjunction(standin, mon
     ]
     picks = _run_both(standin, models, [z3.simplify(q) for q in queries])
     assert picks[-1] is None and sum(p is not None for p in picks) >= 3
+
+
+def test_verdict_memo_is_bounded(standin, monkeypatch):
+    """A model's per-conjunct verdict memo is cleared once it passes VERDICTS_MAX entries,
+    and the choices stay the reference loop's."""
+    oracle_engine.install(monkeypatch)
+    monkeypatch.setattr(MC, "VERDICTS_MAX", 3)
+    models, queries, _, _ = W.build(z3, standin, n_models=12, n_scenarios=3, n_queries=12)
+    _run_both(standin, models, queries)
+    gpu = MC.gpu_model_cache_class()()
+    for m in models:
+        gpu.put(m, 1)
+    for q in queries:
+        gpu.check_quick_sat(q)
+    assert all(len(lv.verdicts) <= 3 + 16 for _, lv in gpu._leaves.values())
