@@ -46,6 +46,9 @@ struct Dev {
     // created and freed per call, and hipMalloc + hipFree (which synchronises the device)
     // per buffer were a millisecond of the single-query latency
     std::vector<std::pair<void*, size_t>> pool;
+    // timing events of freed batches, reused (hipEventCreate / Destroy per batch were two
+    // runtime calls each on the single-query path); under g_pool_mu
+    std::vector<hipEvent_t> ev_free;
 };
 // ascending keys.  The entries are heap objects that stay put until pf_shutdown, so a Dev*
 // taken by pf_batch_create (which runs without g_mu) survives a concurrent pf_init /
@@ -181,7 +184,29 @@ void release_batch(Dev* D, Batch* B) {
         pool_release(D, B->d_mem, B->mem_cap);
         B->d_mem = nullptr;
     }
+    if (D) {
+        std::lock_guard<std::mutex> pk(g_pool_mu);
+        for (hipEvent_t* e : {&B->ev0, &B->ev1}) {
+            if (*e && D->ev_free.size() < 64) {
+                D->ev_free.push_back(*e);
+                *e = nullptr;
+            }
+        }
+    }
     delete B;
+}
+
+// an event from the device's free list, else a new one
+hipError_t event_acquire(Dev* D, hipEvent_t* e) {
+    {
+        std::lock_guard<std::mutex> pk(g_pool_mu);
+        if (!D->ev_free.empty()) {
+            *e = D->ev_free.back();
+            D->ev_free.pop_back();
+            return hipSuccess;
+        }
+    }
+    return hipEventCreate(e);
 }
 
 // A launch on a caller's stream (the *_dev entry points) returns without waiting; before the
@@ -791,6 +816,8 @@ int pf_shutdown(void) {
             std::lock_guard<std::mutex> pk(g_pool_mu);
             for (auto& b : D->pool) hipFree(b.first);
             D->pool.clear();
+            for (hipEvent_t e : D->ev_free) hipEventDestroy(e);
+            D->ev_free.clear();
         }
         hipEventDestroy(D->ev0);
         hipEventDestroy(D->ev1);
@@ -1006,7 +1033,7 @@ int pf_batch_create_on(int device, const uint32_t* code, size_t n_ins, const uin
         B->d_order = reinterpret_cast<uint32_t*>(base + o_order);
         B->d_found = reinterpret_cast<uint32_t*>(base + o_found);
         B->d_scratch = reinterpret_cast<uint32_t*>(base + o_scr);
-        if (hipEventCreate(&B->ev0) != hipSuccess || hipEventCreate(&B->ev1) != hipSuccess) {
+        if (event_acquire(Dv, &B->ev0) != hipSuccess || event_acquire(Dv, &B->ev1) != hipSuccess) {
             const int rc = fail("pf_batch_create: hipEventCreate failed");
             release_batch(Dv, B);
             return report(rc);
@@ -1059,8 +1086,16 @@ int pf_batch_free(uint64_t handle) {
     Batch* B = as_batch(handle);
     if (!B) return 0;
     Dev* D = use_dev(B->device);
-    // a *_dev launch may still be reading the batch on a caller's stream: drain the device
+#ifdef PF_FREE_DEVICE_SYNC
     hipDeviceSynchronize();
+#else
+    // a *_dev launch may still be reading the batch on a caller's stream: drain the stream of
+    // the device's last launch (switch_stream has drained every earlier one; the library's
+    // own launches are complete when their call returns, and the upload's copy when
+    // pf_batch_create returned).  A whole-device synchronisation here cost every
+    // single-query call a device-wide round trip.
+    if (D && D->last_stream) hipStreamSynchronize(D->last_stream);
+#endif
     if (D) D->last_stream = nullptr;
     release_batch(D, B);
     return 0;
