@@ -236,3 +236,43 @@ def test_gpu_two_contexts_on_one_device(engine, monkeypatch):
     assert answers["one"] == answers["two"]
     assert any(a is not None for a in answers["one"])
     gpu_check.reset_cache()
+
+
+@pytest.mark.gpu
+def test_gpu_batch_uploads_while_contexts_are_added(engine):
+    """pf_batch_create runs its device lookup and upload without the library lock, so it can
+    race a pf_init_contexts that grows the device table.  The table's entries are
+    heap objects that never move and the lookup holds the table's own lock: uploads on one
+    thread while another adds contexts must neither crash nor mix up devices, and every
+    batch still searches to the single-thread answer."""
+    import threading
+
+    from mythril_amd import _lib
+
+    progs = _progs(24, first=1700, plant=True)
+    flags = ir.FLAG_EARLY_EXIT | ir.FLAG_SHORTCIRCUIT
+    ref = engine.check(engine.upload(progs), budget=1024, seed=0, flags=flags).found
+    errors = []
+    stop = threading.Event()
+
+    def add_contexts():
+        try:
+            for k in range(1, 9):   # distinct device tuples: each call adds contexts
+                _lib.init_contexts([0] * k)
+                if stop.is_set():
+                    break
+        except Exception as e:  # noqa: BLE001 - reported below
+            errors.append(e)
+
+    t = threading.Thread(target=add_contexts)
+    t.start()
+    try:
+        for _ in range(12):
+            db = engine.upload(progs)
+            got = engine.check(db, budget=1024, seed=0, flags=flags).found
+            db.free()
+            assert np.array_equal(got, ref)
+    finally:
+        stop.set()
+        t.join()
+    assert not errors, errors
