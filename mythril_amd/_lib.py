@@ -167,16 +167,30 @@ def init_contexts(devices) -> list:
     return list(out)
 
 
+# A one-element ctypes array over the numpy buffer (from_buffer: C-contiguous and writable, or
+# it raises) passes the buffer's address as T* for about a third of ndarray.ctypes.data_as's
+# cost (numpy builds its _ctypes helper per call); read-only and empty arrays take data_as.
+_U32_1, _U8_1, _U64_1 = ctypes.c_uint32 * 1, ctypes.c_uint8 * 1, ctypes.c_uint64 * 1
+
+
+def _ptr(a: np.ndarray, one, ptype):
+    try:
+        return one.from_buffer(a)
+    except (TypeError, ValueError):
+        assert a.flags.c_contiguous
+        return a.ctypes.data_as(ptype)
+
+
 def ptr_u32(a: np.ndarray):
-    assert a.dtype == np.uint32 and a.flags.c_contiguous
-    return a.ctypes.data_as(_u32p)
+    assert a.dtype == np.uint32
+    return _ptr(a, _U32_1, _u32p)
 
 
 def ptr_u8(a: np.ndarray):
-    assert a.dtype == np.uint8 and a.flags.c_contiguous
-    return a.ctypes.data_as(_u8p)
+    assert a.dtype == np.uint8
+    return _ptr(a, _U8_1, _u8p)
 
 
 def ptr_u64(a: np.ndarray):
-    assert a.dtype == np.uint64 and a.flags.c_contiguous
-    return a.ctypes.data_as(_u64p)
+    assert a.dtype == np.uint64
+    return _ptr(a, _U64_1, _u64p)

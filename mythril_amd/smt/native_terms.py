@@ -40,6 +40,32 @@ GET_VARS, GET_VAR_TERMS, GET_UF_APPS, GET_READS, GET_CODE, GET_CONSTS, GET_NODES
 VT_TERM, VT_SELECT, VT_EXTRACT = 0, 1, 2
 
 _u32p = ctypes.POINTER(ctypes.c_uint32)
+_U32_1, _U8_1, _I8_1 = ctypes.c_uint32 * 1, ctypes.c_uint8 * 1, ctypes.c_int8 * 1
+
+
+# Pointer arguments: a one-element ctypes array over the numpy buffer (from_buffer) passes its
+# address as T* for about a third of ndarray.ctypes.data_as's cost, which builds numpy's
+# _ctypes helper on every call (a single query makes ~30 of these calls).  Read-only, empty
+# and non-contiguous arrays take data_as.
+def _p32(a: np.ndarray):
+    try:
+        return _U32_1.from_buffer(a)
+    except (TypeError, ValueError):
+        return a.ctypes.data_as(_u32p)
+
+
+def _p8(a: np.ndarray):
+    try:
+        return _U8_1.from_buffer(a)
+    except (TypeError, ValueError):
+        return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+
+
+def _pi8(a: np.ndarray):
+    try:
+        return _I8_1.from_buffer(a)
+    except (TypeError, ValueError):
+        return a.ctypes.data_as(ctypes.POINTER(ctypes.c_int8))
 
 
 def _limbs_of(v: int) -> List[int]:
@@ -230,7 +256,7 @@ def synth_programs(first_id: int, n: int, plant: bool, cdf) -> Optional[Tuple[li
     nv = np.zeros(max(n, 1), dtype=np.uint32)
     c = np.ascontiguousarray(cdf, dtype=np.float64)
     rc = L.pflt_synth(first_id, n, 1 if plant else 0, c.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), hs,
-                      wit.ctypes.data_as(_u32p), nv.ctypes.data_as(_u32p))
+                      _p32(wit), _p32(nv))
     results = [_Result(st, hs[i]) for i in range(n) if hs[i]]
     if rc != 0:
         raise ValueError(L.pflt_last_error().decode(errors="replace"))
@@ -335,14 +361,14 @@ class _Result:
 
     def get(self, which: int, n: int, cols: int) -> np.ndarray:
         out = np.zeros(max(n * cols, 1), dtype=np.uint32)
-        self.st.L.pflt_result_get(self.h, which, out.ctypes.data_as(_u32p), None)
+        self.st.L.pflt_result_get(self.h, which, _p32(out), None)
         return out[:n * cols].reshape(n, cols) if cols > 1 else out[:n]
 
     def variables(self) -> List[ir.Var]:
         nv, nb = self.info[0], self.info[1]
         out = np.zeros(max(nv * 13, 1), dtype=np.uint32)
         names = ctypes.create_string_buffer(max(nb, 1))
-        self.st.L.pflt_result_get(self.h, GET_VARS, out.ctypes.data_as(_u32p), names)
+        self.st.L.pflt_result_get(self.h, GET_VARS, _p32(out), names)
         labels = names.raw[:nb].split(b"\0")[:nv]
         rows = out[:13 * nv].reshape(nv, 13)
         pbytes = np.ascontiguousarray(rows[:, 5:13]).astype("<u4").tobytes()
@@ -441,9 +467,9 @@ def lower_native(bucket: List[T.Term], reg: UFRegistry, parent: Optional[dict], 
         regb = _registry_blob(reg)
         pn, pnv, npn, pr, prv, npr = _parent_args(st, parent)
         rc = ctypes.c_int(0)
-        h = st.L.pflt_lower(st.h, roots.ctypes.data_as(_u32p), len(bucket), regb.ctypes.data_as(_u32p),
-                            len(regb), pn, pnv.ctypes.data_as(_u32p), npn, pr.ctypes.data_as(_u32p),
-                            prv.ctypes.data_as(_u32p), npr, flags, seed & 0xFFFFFFFF, ctypes.byref(rc))
+        h = st.L.pflt_lower(st.h, _p32(roots), len(bucket), _p32(regb),
+                            len(regb), pn, _p32(pnv), npn, _p32(pr),
+                            _p32(prv), npr, flags, seed & 0xFFFFFFFF, ctypes.byref(rc))
         if not h:
             msg = st.L.pflt_last_error().decode(errors="replace")
             if rc.value == -2:
@@ -495,10 +521,10 @@ def recheck(bucket: List[T.Term], lo: Lowered, values: List[int], reg: UFRegistr
         d_, u_, r_, ro_ = a(desc), a(ufs), a(reads), a(roots)
         regb = _registry_blob(reg)
         out = np.zeros(max(len(roots), 1), dtype=np.uint8)
-        rc = L.pflt_recheck(st.h, d_.ctypes.data_as(_u32p), len(lo.var_terms), vals.ctypes.data_as(_u32p),
-                            u_.ctypes.data_as(_u32p), len(ufs), r_.ctypes.data_as(_u32p), len(reads) // 2,
-                            regb.ctypes.data_as(_u32p), len(regb), ro_.ctypes.data_as(_u32p), len(roots),
-                            out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))
+        rc = L.pflt_recheck(st.h, _p32(d_), len(lo.var_terms), _p32(vals),
+                            _p32(u_), len(ufs), _p32(r_), len(reads) // 2,
+                            _p32(regb), len(regb), _p32(ro_), len(roots),
+                            _p8(out))
     if rc != 0:
         return None
     return bool(out[:len(roots)].all())
@@ -522,8 +548,8 @@ def buckets(constraints: List[T.Term]) -> Optional[List[List[T.Term]]]:
         while True:
             ids = np.zeros(cap, dtype=np.uint32)
             sizes = np.zeros(cap, dtype=np.uint32)
-            nb = L.pflt_buckets(st.h, roots.ctypes.data_as(_u32p), len(constraints), ids.ctypes.data_as(_u32p),
-                                cap, sizes.ctypes.data_as(_u32p), cap)
+            nb = L.pflt_buckets(st.h, _p32(roots), len(constraints), _p32(ids),
+                                cap, _p32(sizes), cap)
             if nb != -1:
                 break
             cap *= 4
@@ -578,7 +604,7 @@ def candidate0_limbs(prog) -> Optional[np.ndarray]:
         return None
     nv = int(r.info[0])
     out = np.empty((max(nv, 1), 8), dtype=np.uint32)
-    if not r.st.L.pflt_result_candidate0(r.h, out.ctypes.data_as(_u32p)):
+    if not r.st.L.pflt_result_candidate0(r.h, _p32(out)):
         return None
     return out[:nv]
 
@@ -626,8 +652,8 @@ class NativeProgram(ir.PackedProgram):
 
 def _parent_handle(st: TermStore, parent: dict):
     pn, pnv, npn, pr, prv, npr = _parent_args(st, parent)
-    return st.L.pflt_parent_new(pn, pnv.ctypes.data_as(_u32p), npn, pr.ctypes.data_as(_u32p),
-                                prv.ctypes.data_as(_u32p), npr)
+    return st.L.pflt_parent_new(pn, _p32(pnv), npn, _p32(pr),
+                                _p32(prv), npr)
 
 
 def recent_parent_handle(bucket: List[T.Term], st: Optional[TermStore] = None):
@@ -640,7 +666,7 @@ def recent_parent_handle(bucket: List[T.Term], st: Optional[TermStore] = None):
     st = st or batch_api()
     with st.lock:
         roots = np.array([st.export(c) for c in bucket] or [0], dtype=np.uint32)
-        return st.L.pflt_recent_parent(st.h, roots.ctypes.data_as(_u32p), len(bucket)) or None
+        return st.L.pflt_recent_parent(st.h, _p32(roots), len(bucket)) or None
 
 
 def parent_dict(h, st: Optional[TermStore] = None) -> dict:
@@ -654,7 +680,7 @@ def parent_dict(h, st: Optional[TermStore] = None) -> dict:
     nv = np.zeros(max(nw, 1), dtype=np.uint32)
     rd = np.zeros(max(2 * nr, 1), dtype=np.uint32)
     rv = np.zeros(max(8 * nr, 1), dtype=np.uint32)
-    st.L.pflt_parent_get(h, names, nv.ctypes.data_as(_u32p), rd.ctypes.data_as(_u32p), rv.ctypes.data_as(_u32p))
+    st.L.pflt_parent_get(h, names, _p32(nv), _p32(rd), _p32(rv))
     out: dict = {}
     labels = names.raw[:nb].split(b"\0")[:nn]
     o = 0
@@ -686,7 +712,7 @@ def note_vars(vals: Dict[str, int], recent_size: int) -> None:
     if names:
         w = np.array(words, dtype=np.uint32)
         with st.lock:
-            st.L.pflt_note_vars(st.h, b"\0".join(names) + b"\0", w.ctypes.data_as(_u32p), len(names),
+            st.L.pflt_note_vars(st.h, b"\0".join(names) + b"\0", _p32(w), len(names),
                                 recent_size)
 
 
@@ -698,7 +724,7 @@ def note_result(lo: NativeLowered, limbs: np.ndarray, recent_size: int) -> None:
     if v.size == 0:
         v = np.zeros(8, dtype=np.uint32)
     with st.lock:
-        st.L.pflt_note_result(st.h, lo.res.h, v.ctypes.data_as(_u32p), recent_size)
+        st.L.pflt_note_result(st.h, lo.res.h, _p32(v), recent_size)
 
 
 def recent_clear() -> None:
@@ -740,7 +766,7 @@ def lower_many(jobs: List[Tuple[List[T.Term], object]], reg: UFRegistry, hints: 
         arr["seed"] = np.array(seeds, dtype=np.uint64) & 0xFFFFFFFF
         regb = _registry_blob(reg)
         res = (ctypes.c_void_p * n)()
-        st.L.pflt_lower_many(st.h, arr.ctypes.data, n, regb.ctypes.data_as(_u32p), len(regb),
+        st.L.pflt_lower_many(st.h, arr.ctypes.data, n, _p32(regb), len(regb),
                              max(1, threads), res)
     out = []
     for j in range(n):
@@ -771,9 +797,9 @@ def pack_batch(programs: List[NativeProgram]):
     descs = np.zeros((max(n, 1), 8), dtype=np.uint32)
     seeds = np.array([p.seed & 0xFFFFFFFF for p in programs] or [0], dtype=np.uint32)
     lut = ir.reach_lut()
-    st.L.pflt_pack_batch(hs, n, seeds.ctypes.data_as(_u32p), lut.ctypes.data_as(_u32p), lut.shape[1],
-                         code.ctypes.data_as(_u32p), consts.ctypes.data_as(_u32p), schema.ctypes.data_as(_u32p),
-                         parents.ctypes.data_as(_u32p), descs.ctypes.data_as(_u32p))
+    st.L.pflt_pack_batch(hs, n, _p32(seeds), _p32(lut), lut.shape[1],
+                         _p32(code), _p32(consts), _p32(schema),
+                         _p32(parents), _p32(descs))
     return code[:ni], consts[:nc], schema[:nv], parents[:np_], descs[:n]
 
 
@@ -802,8 +828,8 @@ def recheck_many(los: List[NativeLowered], limbs: np.ndarray, reg: UFRegistry, t
     regb = _registry_blob(reg)
     status = np.zeros(n, dtype=np.int8)
     with st.lock:
-        st.L.pflt_recheck_many(st.h, hs, n, v.ctypes.data_as(_u32p), regb.ctypes.data_as(_u32p), len(regb),
-                               max(1, threads), status.ctypes.data_as(ctypes.POINTER(ctypes.c_int8)))
+        st.L.pflt_recheck_many(st.h, hs, n, _p32(v), _p32(regb), len(regb),
+                               max(1, threads), _pi8(status))
     return status
 
 
@@ -854,8 +880,8 @@ class NativeWitness:
         blob, serial = _registry_blob_serial(reg)
         hs = (ctypes.c_void_p * len(parts))(*[lo.res.h for lo, _ in parts])
         with st.lock:
-            h = st.L.pflt_witness_new(st.h, hs, len(parts), vals.ctypes.data_as(_u32p),
-                                      blob.ctypes.data_as(_u32p), len(blob), serial)
+            h = st.L.pflt_witness_new(st.h, hs, len(parts), _p32(vals),
+                                      _p32(blob), len(blob), serial)
         if not h:
             return None
         return cls(st, h, [lo for lo, _ in parts])
@@ -912,8 +938,8 @@ def witness_values_many(ws: List[NativeWitness], terms: List[T.Term], reg: UFReg
         if not fresh:
             # every term was read before: mostly 32-byte copies, cheaper than waking the pool
             threads = 1
-        st.L.pflt_witness_values(hs, n, ids.ctypes.data_as(_u32p), k, slots.ctypes.data_as(_u32p), epoch,
-                                 blob.ctypes.data_as(_u32p), len(blob),
-                                 serial, max(1, threads), out.ctypes.data_as(_u32p),
-                                 ok.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))
+        st.L.pflt_witness_values(hs, n, _p32(ids), k, _p32(slots), epoch,
+                                 _p32(blob), len(blob),
+                                 serial, max(1, threads), _p32(out),
+                                 _p8(ok))
     return out, ok.astype(bool)
