@@ -2,7 +2,7 @@
 queries, one check_sets call each with the answer caches cleared) on the GPU box: where the
 host part of a single query's latency goes.  Tool.
 
-usage: python tools/sq_cprofile.py [top] [reps]"""
+usage: [SQ_ONLY=i,j,..] python tools/sq_cprofile.py [top] [reps]"""
 import cProfile
 import os
 import pstats
@@ -21,6 +21,8 @@ gpu_check.warm_pool()
 c = corpus.build(48, 2, seed=2024)
 gpu_check.check_sets([q.constraints for q in c.queries], registry=c.kfm.registry)
 sample = [q for q in c.queries if q.label == "sat"][:96]
+if os.environ.get("SQ_ONLY"):   # comma-separated sample indices (tools/sq_tail.py numbering)
+    sample = [sample[int(i)] for i in os.environ["SQ_ONLY"].split(",")]
 
 
 def one_pass():
