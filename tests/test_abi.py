@@ -5,6 +5,7 @@ import os
 import re
 import subprocess
 
+import numpy as np
 import pytest
 
 from mythril_amd import _lib, ir
@@ -97,3 +98,36 @@ def test_engine_runs_without_torch_on_gpu():
                          text=True, timeout=120)
     assert out.returncode == 0, out.stderr[-2000:]
     assert out.stdout.strip().splitlines()[-1] == "False"
+
+
+def test_pointer_helpers_pass_the_buffer_address():
+    """_lib.ptr_* and native_terms._p32/_p8/_pi8 hand ctypes the numpy buffer's own address
+    (from_buffer, or data_as for read-only and empty arrays) and refuse non-contiguous
+    arrays, as ndarray.ctypes.data_as with the contiguity assert did."""
+    from mythril_amd.smt import native_terms as NT
+
+    def addr(p):
+        return ctypes.cast(p, ctypes.c_void_p).value
+
+    a = np.arange(16, dtype=np.uint32)
+    ro = np.frombuffer(np.arange(4, dtype=np.uint32).tobytes(), dtype=np.uint32)
+    assert not ro.flags.writeable
+    empty = np.zeros(0, dtype=np.uint32)
+    for x in (a, ro, empty, a.reshape(4, 4)):
+        assert addr(_lib.ptr_u32(x)) == x.ctypes.data or x.size == 0
+        assert addr(NT._p32(x)) == x.ctypes.data or x.size == 0
+    b = np.arange(8, dtype=np.uint8)
+    assert addr(_lib.ptr_u8(b)) == b.ctypes.data and addr(NT._p8(b)) == b.ctypes.data
+    c = np.arange(4, dtype=np.uint64)
+    assert addr(_lib.ptr_u64(c)) == c.ctypes.data
+    i8 = np.zeros(8, dtype=np.int8)
+    assert addr(NT._pi8(i8)) == i8.ctypes.data
+    with pytest.raises(AssertionError):
+        _lib.ptr_u32(a[::2])
+    with pytest.raises(AssertionError):
+        _lib.ptr_u32(a.astype(np.int64))
+    # a native call writes through the pointer into the array itself
+    libc = ctypes.CDLL(None)
+    libc.memset.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.c_int, ctypes.c_size_t]
+    libc.memset(_lib.ptr_u32(a), 0, a.nbytes)
+    assert not a.any()
