@@ -277,5 +277,8 @@ typedef struct pf_set_desc {
 #define PF_FLAG_SHORTCIRCUIT 1u  /* stop a wave's set evaluation once all its lanes are false */
 #define PF_FLAG_EARLY_EXIT 2u    /* stop a set once any candidate satisfies it             */
 #define PF_FLAG_COUNT_OPS 4u     /* accumulate algorithmic int32-op counts                  */
+#define PF_FLAG_NO_PROBE 8u      /* no candidate-0 probe launch before an early-exit search:  \
+                                    the caller knows some set's candidate 0 misses (its host \
+                                    hint model leaves a root false); answers are unchanged    */
 
 #endif /* PF_BYTECODE_H */

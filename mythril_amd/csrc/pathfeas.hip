@@ -78,6 +78,10 @@ uint32_t g_early_chunk_groups = 8;
 // 0.071 ms and sets without a candidate-0 witness (16 unplanted: 0.237 -> 0.321 ms) lose, hence
 // the conditions.  (Round 4 before the striped counters: a single funnel query 0.686 -> 0.770 ms
 // with the probe on for every batch.)  PF_PROBE_MAX_SETS sets the bound, 0 turns it off.
+// A set without variables counts as parented (all its candidates are candidate 0), and the
+// caller's PF_FLAG_NO_PROBE skips the probe when it knows a set's candidate 0 misses (check_sets:
+// a host hint model that leaves a root false — the probe of a long program then only delays
+// the search behind it; profiles/r06_probe_rule.md).
 uint32_t g_probe_max_sets = 64;
 
 int fail(const char* fmt, ...) {
@@ -117,7 +121,8 @@ struct Batch {
     uint32_t* d_parents = nullptr;
     uint32_t* d_found = nullptr;
     uint32_t* d_order = nullptr;    // set ids, most expensive first (search-kernel wave order)
-    bool all_parented = false;      // every set carries a parent / hint model (candidate 0)
+    bool all_parented = false;      // every set carries a parent / hint model (candidate 0) or
+                                    // has no variables
     uint32_t* d_scratch = nullptr;  // this batch's t0 (u64 [4]), queue heads and counter lines (pf_bytecode.h)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     ~Batch() {  // the device block goes back to its device's pool first (release_batch)
@@ -298,7 +303,7 @@ int check_enqueue(Batch* B, uint64_t gseed, uint32_t budget, uint32_t flags, uin
     // phase 0: the probe (early exit, small batches: candidates 0..63 of every set, one wave
     // per set); phase 1: the search over the whole budget, whose waves skip decided sets
     const bool probe = early && budget > 64u && B->n_sets >= 2 && B->n_sets <= g_probe_max_sets &&
-                       B->all_parented;
+                       B->all_parented && !(flags & PF_FLAG_NO_PROBE);
     for (int phase = probe ? 0 : 1; phase < 2; ++phase) {
     const uint32_t pbudget = phase == 0 ? 64u : budget;
     // the 8-register sets first, then the 16-register ones (usually none)
@@ -1017,7 +1022,11 @@ int pf_batch_create_on(int device, const uint32_t* code, size_t n_ins, const uin
         B->n_sets = n_sets;
         B->max_vars = max_vars;
         B->n_narrow = (size_t)std::count(wide.begin(), wide.end(), (uint8_t)0);
-        B->all_parented = std::all_of(descs, descs + n_sets, [](const pf_set_desc& d) { return d.parent_off != PF_NO_PARENT; });
+        // a set without variables counts as parented: its every candidate is candidate 0 (a
+        // single query's ground keccak bucket left every such batch without the probe launch)
+        B->all_parented = std::all_of(descs, descs + n_sets, [](const pf_set_desc& d) {
+            return d.parent_off != PF_NO_PARENT || d.n_vars == 0;
+        });
         B->h_descs.assign(descs, descs + n_sets);
         B->d_mem = pool_acquire(Dv, total, &B->mem_cap);
         if (!B->d_mem) {

@@ -118,6 +118,7 @@ def cdbyte_hints(name: str) -> Tuple[int, int]:
 FLAG_SHORTCIRCUIT = 1
 FLAG_EARLY_EXIT = 2
 FLAG_COUNT_OPS = 4
+FLAG_NO_PROBE = 8     # include/pf_bytecode.h: skip the candidate-0 probe launch
 
 # ---- algorithmic int32-op cost table -----------------------------
 # Ops not in the table (moves, constant loads, candidate generation) cost 0: they are

@@ -318,6 +318,17 @@ def _probe_candidate0(eng, progs, lows, keys, reg, cfg) -> Dict[int, np.ndarray]
     return out
 
 
+def _long_hint_miss(prog, min_ins: int) -> bool:
+    """A native program of at least ``min_ins`` instructions (min_ins > 0) with variables whose
+    host hint model (candidate 0) satisfies fewer roots than the DAG has.  info[13] n_sat
+    counts the distinct roots the host evaluator finds true (a UF application it cannot
+    evaluate reads as false) against info[10], all of them: a short program's "miss" may be
+    no miss, and its probe walk is cheap anyway."""
+    r = getattr(prog, "native_result", None)
+    return (r is not None and 0 < min_ins <= int(r.info[6]) and int(r.info[0]) > 0
+            and int(r.info[13]) < int(r.info[10]))
+
+
 def _native_batch() -> bool:
     """check_sets' native pipeline (libpflower.so batch entry points): buckets lowered on
     host threads, packed, re-checked and recorded in C++ — no Python term decoding."""
@@ -574,11 +585,16 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
             # one batch per device of the engine (cost-balanced shards), searched concurrently
             dbs = eng.upload_sharded(sprogs) if hasattr(eng, "upload_sharded") else [eng.upload(sprogs)]
             lap("upload")
+            flags = cfg.flags
+            if nat and cfg.hints and any(_long_hint_miss(p, cfg.probe_min_ins) for p in sprogs):
+                # the device's candidate-0 probe launch would walk that long program once in
+                # vain before the search walks it again
+                flags |= ir.FLAG_NO_PROBE
             if len(dbs) == 1:
-                res = eng.check(dbs[0], budget=cfg.budget, seed=cfg.seed, flags=cfg.flags,
+                res = eng.check(dbs[0], budget=cfg.budget, seed=cfg.seed, flags=flags,
                                 timeout_ms=cfg.timeout_ms)
             else:
-                res = eng.check_many(dbs, budget=cfg.budget, seed=cfg.seed, flags=cfg.flags,
+                res = eng.check_many(dbs, budget=cfg.budget, seed=cfg.seed, flags=flags,
                                      timeout_ms=cfg.timeout_ms)
             timed_out = bool(res.timed_out)
             lap("search")

@@ -187,14 +187,39 @@ def test_parented_small_batches_match_oracle(engine, n_sets):
                     v.parent = (v.parent + 1) & ((1 << v.width) - 1)
         progs.append(p)
     assert all(p.has_parent for p in progs)
-    res = engine.check(engine.upload(progs), budget=budget, seed=seed,
-                       flags=ir.FLAG_EARLY_EXIT | ir.FLAG_SHORTCIRCUIT)
+    db = engine.upload(progs)
+    res = engine.check(db, budget=budget, seed=seed, flags=ir.FLAG_EARLY_EXIT | ir.FLAG_SHORTCIRCUIT)
     for i, p in enumerate(progs):
         want = _oracle_first(p, budget, seed)
         got = None if res.found[i] == 0xFFFFFFFF else int(res.found[i])
         assert got == want, (n_sets, i, got, want)
         if i % 3 != 1:
             assert got == 0
+    # PF_FLAG_NO_PROBE (the caller's "candidate 0 misses") changes no answer
+    res2 = engine.check(db, budget=budget, seed=seed,
+                        flags=ir.FLAG_EARLY_EXIT | ir.FLAG_SHORTCIRCUIT | ir.FLAG_NO_PROBE)
+    assert (res2.found == res.found).all()
+
+
+@pytest.mark.parametrize("truth", [True, False])
+def test_varless_set_in_a_parented_batch(engine, truth):
+    """A set without variables counts as parented (pathfeas.hip: the batch takes the probe
+    launch): a true ground set is answered at candidate 0, a false one never, and the
+    parented sets beside it keep their oracle witnesses."""
+    budget, seed = 2048, 0x5EED_0043
+    progs = [synth.random_dag_set(600 + i, plant=True)[0] for i in range(3)]
+    ground = ir.Program(name=f"ground_{truth}")
+    ground.emit(ir.W_CONST, 256, dst=0, aux0=ground.const_index(7))
+    ground.emit(ir.W_CONST, 256, dst=1, aux0=ground.const_index(7 if truth else 8))
+    ground.emit(ir.B_EQ, 256, dst=0, a=0, b=1)
+    ground.emit(ir.ASSERT, 1, a=0)
+    ground.finish().validate()
+    progs.insert(1, ground)
+    res = engine.check(engine.upload(progs), budget=budget, seed=seed,
+                       flags=ir.FLAG_EARLY_EXIT | ir.FLAG_SHORTCIRCUIT)
+    assert int(res.found[1]) == (0 if truth else 0xFFFFFFFF)
+    for i in (0, 2, 3):
+        assert int(res.found[i]) == _oracle_first(progs[i], budget, seed) == 0
 
 
 def test_materialize_matches_generator(engine):
