@@ -390,12 +390,18 @@ int check_collect(Batch* B, hipStream_t st, pf_stats* stats, std::vector<uint32_
     const size_t nf = std::max<size_t>(B->n_sets, 1);
     unsigned long long hs[PF_COUNTER_STRIPES * 16];
     uint8_t* pin = pinned_staging(cbytes + (found ? nf * 4 : 0));
-    HIPCHK(hipMemcpyAsync(pin ? static_cast<void*>(pin) : static_cast<void*>(hs), B->d_scratch + PF_COUNTER_OFF / 4,
-                          cbytes, hipMemcpyDeviceToHost, st));
-    if (found) {
-        found->assign(nf, 0u);
-        HIPCHK(hipMemcpyAsync(pin ? static_cast<void*>(pin + cbytes) : static_cast<void*>(found->data()), B->d_found,
-                              nf * 4, hipMemcpyDeviceToHost, st));
+    const uint32_t* d_counters = B->d_scratch + PF_COUNTER_OFF / 4;
+    if (found) found->assign(nf, 0u);
+    if (found && pin && B->d_found == d_counters + cbytes / 4) {
+        // the batch block keeps found[] right after the counter lines: one copy (each copy is
+        // a blit dispatch serialised behind the search)
+        HIPCHK(hipMemcpyAsync(pin, d_counters, cbytes + nf * 4, hipMemcpyDeviceToHost, st));
+    } else {
+        HIPCHK(hipMemcpyAsync(pin ? static_cast<void*>(pin) : static_cast<void*>(hs), d_counters, cbytes,
+                              hipMemcpyDeviceToHost, st));
+        if (found)
+            HIPCHK(hipMemcpyAsync(pin ? static_cast<void*>(pin + cbytes) : static_cast<void*>(found->data()),
+                                  B->d_found, nf * 4, hipMemcpyDeviceToHost, st));
     }
     HIPCHK(hipStreamSynchronize(st));
     if (pin) {
@@ -966,7 +972,8 @@ int pf_batch_create_on(int device, const uint32_t* code, size_t n_ins, const uin
     });
 
     // One device block, one copy: [code | consts + one zero entry | schema | parents | descs |
-    // order | found | scratch], each region 256-byte aligned.  The zero entry past the
+    // order | scratch | found], each region 256-byte aligned (found[] right after the scratch's
+    // counter lines, so a search reads both back in one copy, check_collect).  The zero entry past the
     // constant pool: the generator's constant gather is issued before it knows whether the
     // set has constants (pf_eval.hip gen_var), so a set with none reads the entry at its own
     // const_off, which may be the pool's end.
@@ -975,12 +982,14 @@ int pf_batch_create_on(int device, const uint32_t* code, size_t n_ins, const uin
     // slot after an END before its dispatch leaves the program (pf_eval.hip run_program)
     const size_t o_code = 0, o_const = o_code + al(n_ins * 16 + 16), o_schema = o_const + al(n_const * 32 + 32),
                  o_par = o_schema + al(n_vars * 16), o_desc = o_par + al(n_parents * 32),
-                 o_order = o_desc + al(n_sets * sizeof(pf_set_desc)), o_found = o_order + al(n_sets * 4),
-                 o_scr = o_found + al(std::max<size_t>(n_sets, 1) * 4),
-                 total = o_scr + PF_SCRATCH_BYTES;
-    // found / scratch are cleared by every search: the copy ends at o_found
+                 o_order = o_desc + al(n_sets * sizeof(pf_set_desc)), o_scr = o_order + al(n_sets * 4),
+                 o_found = o_scr + PF_SCRATCH_BYTES,
+                 total = o_found + al(std::max<size_t>(n_sets, 1) * 4);
+    static_assert(PF_SCRATCH_BYTES % 256 == 0 && PF_COUNTER_OFF + PF_COUNTER_STRIPES * 128 == PF_SCRATCH_BYTES,
+                  "found[] follows the counter lines");
+    // scratch / found are cleared by every search: the copy ends at o_scr
     auto fill = [&](uint8_t* stage) {
-        memset(stage, 0, o_found);
+        memset(stage, 0, o_scr);
         auto put = [&](size_t off, const void* src, size_t bytes) {
             if (bytes && src) memcpy(stage + off, src, bytes);
         };
@@ -1057,22 +1066,22 @@ int pf_batch_create_on(int device, const uint32_t* code, size_t n_ins, const uin
     {
         std::lock_guard<std::mutex> lk(g_up_mu);
         ok = hipSetDevice(dev_id) == hipSuccess;
-        uint8_t* pin = ok ? upload_staging(o_found) : nullptr;
+        uint8_t* pin = ok ? upload_staging(o_scr) : nullptr;
         if (pin) {
             fill(pin);
-            ok = hipMemcpyAsync(B->d_mem, pin, o_found, hipMemcpyHostToDevice, ups) == hipSuccess &&
+            ok = hipMemcpyAsync(B->d_mem, pin, o_scr, hipMemcpyHostToDevice, ups) == hipSuccess &&
                  hipStreamSynchronize(ups) == hipSuccess;
         } else if (ok) {
-            std::vector<uint8_t> stage(o_found);
+            std::vector<uint8_t> stage(o_scr);
             fill(stage.data());
-            ok = hipMemcpy(B->d_mem, stage.data(), o_found, hipMemcpyHostToDevice) == hipSuccess;
+            ok = hipMemcpy(B->d_mem, stage.data(), o_scr, hipMemcpyHostToDevice) == hipSuccess;
         }
     }
     if (!ok) {
         // the copy may still be in flight: drain the device and free the block rather than
         // pool it (the next pool_acquire would hand out memory still being written)
         t_defer_err = true;
-        const int rc = fail("pf_batch_create: hipMemcpy of %zu bytes failed", o_found);
+        const int rc = fail("pf_batch_create: hipMemcpy of %zu bytes failed", o_scr);
         if (hipDeviceSynchronize() == hipSuccess) hipFree(B->d_mem);
         B->d_mem = nullptr;
         delete B;
