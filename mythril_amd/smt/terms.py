@@ -29,7 +29,7 @@ def M(w: int) -> int:
 
 
 class Term:
-    __slots__ = ("op", "sort", "args", "val", "_h", "__weakref__")
+    __slots__ = ("op", "sort", "args", "val", "__weakref__")
     _table: Dict[tuple, "Term"] = {}
 
     def __new__(cls, op: str, sort: tuple, args: Tuple["Term", ...] = (), val=None):
@@ -39,7 +39,6 @@ class Term:
             return t
         t = object.__new__(cls)
         t.op, t.sort, t.args, t.val = op, sort, tuple(args), val
-        t._h = hash(key)
         cls._table[key] = t
         return t
 
@@ -48,12 +47,9 @@ class Term:
     def __reduce__(self):
         return (Term, (self.op, self.sort, self.args, self.val))
 
-    # identity semantics: hash-consing makes structural equality == object identity
-    def __hash__(self):
-        return self._h
-
-    def __eq__(self, other):
-        return self is other
+    # identity semantics: hash-consing makes structural equality == object identity, so
+    # object's own (C-level) __eq__ / __hash__ are the right ones — a Python-level __hash__
+    # cost every bucket-key tuple lookup one interpreted call per conjunct
 
     @property
     def width(self) -> int:
