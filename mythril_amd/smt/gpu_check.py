@@ -235,9 +235,10 @@ def _union_thunk(parts, reg: UFRegistry):
 
 
 def _set_seed(constraints: Sequence[T.Term]) -> int:
-    h = 0
+    memo, h = T._SHASH, 0
     for c in constraints:
-        h = (h * 1000003) ^ T.struct_hash(c)
+        v = memo.get(c)
+        h = (h * 1000003) ^ (v if v is not None else T.struct_hash(c))
     return h & 0xFFFFFFFF
 
 
@@ -679,9 +680,8 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
                     while len(_CACHE) > cfg.cache_size:
                         _CACHE.popitem(last=False)
                     _note_witness(lows[k], v, cfg)
-        if nat:
-            for lo in lows:   # programs are uploaded: keep only the witness metadata
-                native_terms.shrink(lo)
+        if nat:   # programs are uploaded: keep only the witness metadata
+            native_terms.shrink_many(lows)
         lap("recheck")
 
     n_sat = 0

@@ -169,6 +169,14 @@ class TermStore:
         except Exception:  # noqa: BLE001
             pass
 
+    def export_many(self, terms) -> List[int]:
+        """Store ids of ``terms`` (export each): the stored ones by one C-level dict pass —
+        a query exports its conjuncts several times (buckets, parents, lowering)."""
+        out = list(map(self.ids.get, terms))
+        if None in out:
+            out = [i if i is not None else self.export(t) for i, t in zip(out, terms)]
+        return out
+
     def export(self, root: T.Term) -> int:
         """Store id of ``root``, adding it and every new subterm (children first)."""
         nid = self.ids.get(root)
@@ -463,7 +471,7 @@ def lower_native(bucket: List[T.Term], reg: UFRegistry, parent: Optional[dict], 
     if st is None:
         raise RuntimeError("libpflower.so without the term store")
     with st.lock:
-        roots = np.array([st.export(c) for c in bucket] or [0], dtype=np.uint32)
+        roots = np.array(st.export_many(bucket) or [0], dtype=np.uint32)
         regb = _registry_blob(reg)
         pn, pnv, npn, pr, prv, npr = _parent_args(st, parent)
         rc = ctypes.c_int(0)
@@ -543,7 +551,7 @@ def buckets(constraints: List[T.Term]) -> Optional[List[List[T.Term]]]:
                                    _u32p, ctypes.c_size_t]
         L._buckets_bound = True
     with st.lock:
-        roots = np.array([st.export(c) for c in constraints] or [0], dtype=np.uint32)
+        roots = np.array(st.export_many(constraints) or [0], dtype=np.uint32)
         cap = 4 * len(constraints) + 256
         while True:
             ids = np.zeros(cap, dtype=np.uint32)
@@ -665,7 +673,7 @@ def recent_parent_handle(bucket: List[T.Term], st: Optional[TermStore] = None):
     (lower_many) and freed with the same store even if new_generation retires it meanwhile."""
     st = st or batch_api()
     with st.lock:
-        roots = np.array([st.export(c) for c in bucket] or [0], dtype=np.uint32)
+        roots = np.array(st.export_many(bucket) or [0], dtype=np.uint32)
         return st.L.pflt_recent_parent(st.h, _p32(roots), len(bucket)) or None
 
 
@@ -749,14 +757,10 @@ def lower_many(jobs: List[Tuple[List[T.Term], object]], reg: UFRegistry, hints: 
     if n == 0:
         return []
     with st.lock:
-        ex = st.export
-        flat: List[int] = []
+        flat = st.export_many([c for b, _ in jobs for c in b])
+        lens = np.array([len(b) for b, _ in jobs], dtype=np.uint64)
         offs = np.zeros(n, dtype=np.uint64)
-        lens = np.zeros(n, dtype=np.uint64)
-        for j, (b, _) in enumerate(jobs):
-            offs[j] = len(flat)
-            lens[j] = len(b)
-            flat += [ex(c) for c in b]
+        np.cumsum(lens[:-1], out=offs[1:])
         roots = np.array(flat or [0], dtype=np.uint32)
         arr = np.zeros(n, dtype=_JOB)
         arr["roots"] = roots.ctypes.data + 4 * offs
@@ -836,6 +840,14 @@ def recheck_many(los: List[NativeLowered], limbs: np.ndarray, reg: UFRegistry, t
 def shrink(lo: NativeLowered) -> None:
     """Free the program tables of a result whose program was uploaded (the cache keeps it)."""
     lo.res.st.L.pflt_result_shrink(lo.res.h)
+
+
+def shrink_many(los: List[NativeLowered]) -> None:
+    """shrink() of every result (one library: the entry point is looked up once)."""
+    if los:
+        f = los[0].res.st.L.pflt_result_shrink
+        for lo in los:
+            f(lo.res.h)
 
 
 def ints_of(limbs: np.ndarray) -> List[int]:
@@ -933,7 +945,7 @@ def witness_values_many(ws: List[NativeWitness], terms: List[T.Term], reg: UFReg
     blob, serial = _registry_blob_serial(reg)
     hs = (ctypes.c_void_p * n)(*[w.h for w in ws])
     with st.lock:
-        ids = np.array([st.export(t) for t in terms], dtype=np.uint32)
+        ids = np.array(st.export_many(terms), dtype=np.uint32)
         slots, fresh, epoch = _slots_of(terms)
         if not fresh:
             # every term was read before: mostly 32-byte copies, cheaper than waking the pool
