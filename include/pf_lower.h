@@ -129,6 +129,9 @@ int pfl_version(void);
 #define PFLT_GET_FORCED 9
 #define PFLT_GET_IN_ROOTS 10  /* the bucket's conjuncts as given */
 
+/* A new term store.  Also throws and catches one C++ exception, so the process's one-time
+ * unwinder set-up (~80 ms with PyTorch's libraries loaded) happens here, not inside the first
+ * lowering whose hint solver meets a conflict. */
 void* pflt_store_new(void);
 /* optional pflt_lower modes this build has (PFLT_FEAT_*) */
 #define PFLT_FEAT_EXPLICIT 1u

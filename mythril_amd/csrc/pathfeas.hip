@@ -13,6 +13,7 @@
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -741,6 +742,21 @@ int pf_device_count(void) {
     return n;
 }
 
+// The host lowering (libpflower.so) reports conflicts as C++ exceptions, and the first one
+// thrown in a process has libgcc's unwinder set up its frame tables for every library then
+// loaded — ~80 ms once the HIP runtime's are (tools/slow_job_probe.py: the corpus's first
+// bucket whose hints meet a conflict took 80 ms, then 0.05 ms).  Both initialisers take that
+// one-time cost here, with the runtime loaded, instead of the first query that conflicts.
+void warm_unwinder() {
+    static std::once_flag once;
+    std::call_once(once, [] {
+        try {
+            throw std::runtime_error("unwinder warm-up");
+        } catch (const std::exception&) {
+        }
+    });
+}
+
 // launch-geometry knobs from the environment, read by both initialisers
 void read_env_knobs() {
     if (const char* e = getenv("PF_WAVES_PER_CU")) {
@@ -797,6 +813,7 @@ int pf_init(uint64_t device_mask) {
         if (!((device_mask >> id) & 1ull) || find_dev(id)) continue;
         if (add_dev(id, id, "pf_init")) return -1;
     }
+    warm_unwinder();
     return 0;
 }
 
@@ -814,6 +831,7 @@ int pf_init_contexts(const int32_t* devices, size_t n, int32_t* ctx_out) {
         if (add_dev(id, next, "pf_init_contexts")) return -1;
         ctx_out[i] = next++;
     }
+    warm_unwinder();
     return 0;
 }
 

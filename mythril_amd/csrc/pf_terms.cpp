@@ -2228,7 +2228,19 @@ void synth_dag(uint32_t dag_id, bool plant, const double* cdf, Result* R, std::v
 
 extern "C" {
 
-void* pflt_store_new(void) { return new Store(); }
+void* pflt_store_new(void) {
+    // The hint solver and the lowering report conflicts as C++ exceptions, and the first one
+    // thrown in a process has libgcc's unwinder set up its frame tables for every library
+    // loaded: ~80 ms once PyTorch's are (tools/slow_job_probe.py: the corpus's first bucket
+    // whose hints hit a conflict took 80 ms, then 0.05 ms; 0.03 ms without torch loaded).
+    // A store is made once per process (and per retired generation), before any lowering:
+    // take that one-time cost here rather than inside the first query that conflicts.
+    try {
+        throw TermError{0};
+    } catch (const TermError&) {
+    }
+    return new Store();
+}
 
 uint32_t pflt_features(void) { return PFLT_FEAT_EXPLICIT | PFLT_FEAT_SYNTH; }
 
