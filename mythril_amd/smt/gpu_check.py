@@ -235,11 +235,14 @@ def _union_thunk(parts, reg: UFRegistry):
 
 
 def _set_seed(constraints: Sequence[T.Term]) -> int:
+    # (h * 1000003) ^ hash over all conjuncts, mod 2^32: multiplication and xor only carry
+    # upwards, so masking every step gives the unmasked chain's low 32 bits without the
+    # big integer growing by ~20 bits per conjunct
     memo, h = T._SHASH, 0
     for c in constraints:
         v = memo.get(c)
-        h = (h * 1000003) ^ (v if v is not None else T.struct_hash(c))
-    return h & 0xFFFFFFFF
+        h = ((h * 1000003) ^ (v if v is not None else T.struct_hash(c))) & 0xFFFFFFFF
+    return h
 
 
 _NATIVE_TERMS = os.environ.get("PF_NATIVE_TERMS", "1") != "0"
