@@ -3,7 +3,7 @@
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out/var
-B="python bench.py --steps 3 --warmup 1 --no-cpu-baseline --corpus-scenarios 0 --keccak-log2 0"
+B="python bench.py --steps 3 --warmup 1 --no-cpu-baseline --corpus-scenarios 0 --keccak-log2 0 --full-pass-dags 0 --quick-sat-queries 0"
 for v in base "$@"; do
   if [ "$v" = base ]; then L=""; else L="--lib build_var/lib_$v.so"; fi
   timeout -k 10 300 $B $L > gpurun_out/var/$v.log 2>&1 || { echo "variant $v failed"; exit 1; }
