@@ -234,6 +234,11 @@ struct Store {
     std::vector<std::vector<uint32_t>> keysets, finvs;
     std::unordered_map<std::string, uint32_t> key_ids;
     std::vector<std::string> key_names;
+    // per key id, for pflt_buckets: the id of the keccak family a "k:<n>" key belongs to (the
+    // key "<n>"), -2 for any other key, -1 while "<n>" has no id yet (looked up again), -3 not
+    // classified yet; and the per-call union-find / group scratch, indexed by key id (-1 =
+    // untouched; reset through the touched list after each call)
+    std::vector<int32_t> kfam, uf, ugrp;
 };
 
 // ---- the DAG (mythril_amd/lower.py Dag) ---------------------------------------------------
@@ -2421,70 +2426,100 @@ int64_t pflt_buckets(void* st, const uint32_t* roots, size_t n_roots, uint32_t* 
             cs.push_back(c);
         }
     }
+    // flat arrays and key-indexed scratch instead of per-call maps and vectors of vectors (a
+    // query's bucketing was ~20 us, mostly allocation and string lookups)
     std::vector<uint32_t> families;
     std::vector<int32_t> kidx(cs.size());
     for (size_t i = 0; i < cs.size(); i++) {
         kidx[i] = dep_keys(S, cs[i]);
-        merge_sorted(&families, S->finvs[kidx[i]]);
+        const auto& fv = S->finvs[kidx[i]];
+        families.insert(families.end(), fv.begin(), fv.end());
     }
-    // union-find over key ids
-    std::unordered_map<uint32_t, uint32_t> parent;
+    std::sort(families.begin(), families.end());
+    families.erase(std::unique(families.begin(), families.end()), families.end());
+    const size_t nk = S->key_names.size();
+    if (S->kfam.size() < nk) S->kfam.resize(nk, -3);
+    if (S->uf.size() < nk) {
+        S->uf.resize(nk, -1);
+        S->ugrp.resize(nk, -1);
+    }
+    std::vector<int32_t>& uf = S->uf;
+    std::vector<uint32_t> touched;
     auto find = [&](uint32_t k) {
-        while (parent[k] != k) {
-            parent[k] = parent[parent[k]];
-            k = parent[k];
+        while ((uint32_t)uf[k] != k) {
+            uf[k] = uf[uf[k]];
+            k = (uint32_t)uf[k];
         }
         return k;
     };
-    std::vector<std::vector<uint32_t>> kept(cs.size());
+    // kept keys of conjunct i: kept[off[i] .. off[i + 1])
+    std::vector<uint32_t> kept, off(cs.size() + 1, 0);
     for (size_t i = 0; i < cs.size(); i++) {
         for (uint32_t k : S->keysets[kidx[i]]) {
-            const std::string& nm = S->key_names[k];
-            if (nm.compare(0, 2, "k:") == 0) {
-                auto it = S->key_ids.find(nm.substr(2));
-                if (it == S->key_ids.end() || !std::binary_search(families.begin(), families.end(), it->second))
-                    continue;
+            int32_t fam = S->kfam[k];
+            if (fam == -3 || fam == -1) {
+                const std::string& nm = S->key_names[k];
+                if (nm.compare(0, 2, "k:") != 0) {
+                    fam = -2;
+                } else {
+                    auto it = S->key_ids.find(nm.substr(2));
+                    fam = it == S->key_ids.end() ? -1 : (int32_t)it->second;
+                }
+                S->kfam[k] = fam;
             }
-            kept[i].push_back(k);
+            if (fam == -1 || (fam >= 0 && !std::binary_search(families.begin(), families.end(), (uint32_t)fam)))
+                continue;
+            kept.push_back(k);
         }
+        off[i + 1] = (uint32_t)kept.size();
         bool have = false;
         uint32_t first = 0;
-        for (uint32_t k : kept[i]) {
-            if (!parent.count(k)) parent[k] = k;
+        for (uint32_t j = off[i]; j < off[i + 1]; j++) {
+            const uint32_t k = kept[j];
+            if (uf[k] < 0) {
+                uf[k] = (int32_t)k;
+                touched.push_back(k);
+            }
             if (!have) {
                 first = find(k);
                 have = true;
             } else {
                 const uint32_t rk = find(k);
-                if (rk != first) parent[rk] = first;
+                if (rk != first) uf[rk] = (int32_t)first;
             }
         }
     }
-    std::vector<uint32_t> group_root, ground;
-    std::vector<std::vector<uint32_t>> groups;
-    std::unordered_map<uint32_t, size_t> gpos;
+    // group of each conjunct, numbered in order of first appearance; the ground conjuncts
+    // (no kept key) form the last group
+    std::vector<int32_t>& ugrp = S->ugrp;
+    std::vector<uint32_t> gi(cs.size()), gsize;
+    uint32_t n_ground = 0;
     for (size_t i = 0; i < cs.size(); i++) {
-        if (kept[i].empty()) {
-            ground.push_back(cs[i]);
+        if (off[i] == off[i + 1]) {
+            gi[i] = UINT32_MAX;
+            n_ground++;
             continue;
         }
-        const uint32_t rt = find(kept[i][0]);
-        auto it = gpos.find(rt);
-        if (it == gpos.end()) {
-            gpos.emplace(rt, groups.size());
-            groups.push_back({cs[i]});
-        } else {
-            groups[it->second].push_back(cs[i]);
+        const uint32_t rt = find(kept[off[i]]);
+        if (ugrp[rt] < 0) {
+            ugrp[rt] = (int32_t)gsize.size();
+            gsize.push_back(0);
         }
+        gi[i] = (uint32_t)ugrp[rt];
+        gsize[gi[i]]++;
     }
-    if (!ground.empty()) groups.push_back(ground);
-    if (cs.size() > cap_ids || groups.size() > cap_sizes) return -1;
-    size_t o = 0;
-    for (size_t g = 0; g < groups.size(); g++) {
-        out_sizes[g] = (uint32_t)groups[g].size();
-        for (uint32_t c : groups[g]) out_ids[o++] = c;
+    for (uint32_t k : touched) uf[k] = ugrp[k] = -1;
+    const size_t ng = gsize.size() + (n_ground ? 1 : 0);
+    if (cs.size() > cap_ids || ng > cap_sizes) return -1;
+    // bucket by bucket, conjuncts in query order within each
+    std::vector<uint32_t> pos(ng, 0);
+    for (size_t g = 0; g < gsize.size(); g++) {
+        out_sizes[g] = gsize[g];
+        if (g + 1 < ng) pos[g + 1] = pos[g] + gsize[g];
     }
-    return (int64_t)groups.size();
+    if (n_ground) out_sizes[ng - 1] = n_ground;
+    for (size_t i = 0; i < cs.size(); i++) out_ids[pos[gi[i] == UINT32_MAX ? ng - 1 : gi[i]]++] = cs[i];
+    return (int64_t)ng;
 }
 
 int pflt_view(void* st, uint32_t id, pflt_term_view* out) {

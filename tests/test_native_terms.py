@@ -464,3 +464,27 @@ def test_parent_handle_survives_store_retirement(monkeypatch):
     native_terms.free_parent(h, st)
     lo, prog, err = out[0]
     assert err is None and lo.res.st is st
+
+
+def test_native_buckets_match_random_queries():
+    """pflt_buckets = independence.buckets on random queries over shared variables, an array
+    and keccak applications with and without a free inverse (partition, bucket order,
+    conjunct order), asked repeatedly so the per-store key scratch is reused across calls."""
+    rng = random.Random(11)
+    xs = [T.var(f"nbr_x{i}", 256) for i in range(6)]
+    arr = T.Term("array", T.array_sort(256, 256), (), "nbr_storage")
+    ks = [T.apply("keccak256_512", 256, T.concat(x, T.const(1, 256))) for x in xs[:3]]
+    inv = T.eq(T.apply("keccak256_512-1", 512, xs[5]), T.concat(xs[0], T.const(1, 256)))
+    atoms = [inv, T.eq(T.const(1, 8), T.const(1, 8))]
+    for i in range(6):
+        atoms.append(T.eq(T.select(arr, xs[i]), T.const(i, 256)))
+        for j in range(i + 1, 6):
+            atoms.append(T.cmp("bvult", xs[i], xs[j]))
+    for k in ks:
+        atoms.append(T.cmp("bvult", k, T.const(99, 256)))
+    for _ in range(3):
+        for _ in range(60):
+            q = rng.sample(atoms, rng.randint(1, 9))
+            if rng.random() < 0.3 and len(q) >= 2:
+                q = [T.and_(q[0], q[1])] + q[2:]
+            assert NT.buckets(q) == buckets(q), q
