@@ -15,6 +15,7 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/pathfeas.h"
@@ -460,11 +461,10 @@ bool const_fits(const uint32_t* consts, size_t n_const, uint32_t idx, uint32_t w
     return true;
 }
 
-void device_program(const std::vector<uint32_t>& code_fixed, std::vector<pf_set_desc>& descs_out,
-                    std::vector<uint32_t>& code_out, const uint32_t* consts = nullptr, size_t n_const = 0) {
-    code_out.clear();
-    code_out.reserve(code_fixed.size());
-    const size_t n_sets = descs_out.size();
+// Sets [s0, s1) of the batch: their device programs appended to code_out, each set's
+// code_off rewritten to its offset in code_out.
+void device_program_range(const uint32_t* code_fixed, std::vector<pf_set_desc>& descs_out, size_t s0, size_t s1,
+                          std::vector<uint32_t>& code_out, const uint32_t* consts, size_t n_const) {
     std::vector<uint32_t> P;      // the set being rewritten
     std::vector<uint8_t> drop;
     struct Pending {              // pass 3: the W_CONST a register holds, and its readers
@@ -473,10 +473,10 @@ void device_program(const std::vector<uint32_t>& code_fixed, std::vector<pf_set_
         std::vector<uint32_t> readers;
     };
     Pending pend[PF_NW + 1];
-    for (size_t s = 0; s < n_sets; s++) {
+    for (size_t s = s0; s < s1; s++) {
         pf_set_desc& d = descs_out[s];
         const uint32_t n = d.n_ins;
-        P.assign(code_fixed.begin() + 4 * (size_t)d.code_off, code_fixed.begin() + 4 * ((size_t)d.code_off + n));
+        P.assign(code_fixed + 4 * (size_t)d.code_off, code_fixed + 4 * ((size_t)d.code_off + n));
         drop.assign(n, 0);
         auto tr_of = [&](uint32_t i) { return (P[4 * i] >> 18) & 7u; };
         // ---- 1. ASSERT -> PF_I_ASSERT on the last writer of its register
@@ -683,10 +683,69 @@ void device_program(const std::vector<uint32_t>& code_fixed, std::vector<pf_set_
         }
 #endif
         const size_t first = code_out.size() / 4;
+        size_t kept = 0;
+        for (uint32_t i = 0; i < n; i++) kept += !drop[i];
+        code_out.resize(4 * (first + kept));
+        uint32_t* o = code_out.data() + 4 * first;
         for (uint32_t i = 0; i < n; i++)
-            if (!drop[i]) code_out.insert(code_out.end(), P.begin() + 4 * (size_t)i, P.begin() + 4 * (size_t)i + 4);
+            if (!drop[i]) {
+                memcpy(o, P.data() + 4 * (size_t)i, 16);
+                o += 4;
+            }
         d.code_off = (uint32_t)first;
-        d.n_ins = (uint32_t)(code_out.size() / 4 - first);
+        d.n_ins = (uint32_t)kept;
+    }
+}
+
+// Host threads for a batch's preparation and the set ranges they take (about equal
+// instruction counts): one for small batches (a single query's), up to 8 for large ones.
+std::vector<size_t> prep_ranges(const pf_set_desc* descs, size_t n_sets, size_t n_ins) {
+    const size_t hw = std::max<size_t>(1, std::thread::hardware_concurrency());
+    const size_t nt = (n_sets >= 64 && n_ins >= (1u << 15)) ? std::min<size_t>({8, hw, n_sets / 32}) : 1;
+    std::vector<size_t> cut(nt + 1, n_sets);
+    cut[0] = 0;
+    uint64_t total = 0, acc = 0;
+    for (size_t s = 0; s < n_sets; s++) total += descs[s].n_ins;
+    size_t t = 1;
+    for (size_t s = 0; s < n_sets && t < nt; s++) {
+        acc += descs[s].n_ins;
+        if (acc * nt >= total * t) cut[t++] = s + 1;
+    }
+    return cut;
+}
+
+// fn(t) for t in [0, n) on the caller and n - 1 spawned threads
+template <typename F>
+void run_ranges(size_t n, F&& fn) {
+    std::vector<std::thread> th;
+    for (size_t t = 1; t < n; t++) th.emplace_back(fn, t);
+    fn(0);
+    for (auto& x : th) x.join();
+}
+
+// The device program of every set: each range of `cut` rewritten into its own buffer (on its
+// own thread), then concatenated in set order — the program one pass over all sets gives.
+void device_program(const uint32_t* code_fixed, size_t n_fixed, std::vector<pf_set_desc>& descs_out,
+                    const std::vector<size_t>& cut, std::vector<uint32_t>& code_out, const uint32_t* consts,
+                    size_t n_const) {
+    const size_t nt = cut.size() - 1;
+    code_out.clear();
+    if (nt == 1) {
+        code_out.reserve(n_fixed);
+        device_program_range(code_fixed, descs_out, 0, descs_out.size(), code_out, consts, n_const);
+        return;
+    }
+    std::vector<std::vector<uint32_t>> outs(nt);
+    run_ranges(nt, [&](size_t t) {
+        device_program_range(code_fixed, descs_out, cut[t], cut[t + 1], outs[t], consts, n_const);
+    });
+    size_t total = 0;
+    for (const auto& o : outs) total += o.size();
+    code_out.reserve(total);
+    for (size_t t = 0; t < nt; t++) {
+        const uint32_t base = (uint32_t)(code_out.size() / 4);
+        for (size_t s = cut[t]; s < cut[t + 1]; s++) descs_out[s].code_off += base;
+        code_out.insert(code_out.end(), outs[t].begin(), outs[t].end());
     }
 }
 
@@ -710,7 +769,7 @@ int pf_device_program(const uint32_t* code, size_t n_ins, const uint32_t* consts
     }
     std::vector<pf_set_desc> d(descs, descs + n_sets);
     std::vector<uint32_t> out;
-    device_program(fixed, d, out, consts, n_const);
+    device_program(fixed.data(), fixed.size(), d, prep_ranges(descs, n_sets, n_ins), out, consts, n_const);
     memcpy(code_out, out.data(), out.size() * 4);
     *n_ins_out = out.size() / 4;
     memcpy(descs_out, d.data(), n_sets * sizeof(pf_set_desc));
@@ -858,16 +917,12 @@ int pf_shutdown(void) {
     return 0;
 }
 
-// Host-side checks of packed programs and their device form (pf_batch_create and
-// pf_eval_program): every kernel index is derived from these, so nothing the caller packed is
-// trusted.  Fills the device program (device_program), the per-set wide flags and the largest
-// variable count; returns 0 or fail().
-static int prepare_program(const uint32_t* code, size_t n_ins, const uint32_t* consts, size_t n_const,
-                           const uint32_t* schema, size_t n_vars, size_t n_parents, const pf_set_desc* descs,
-                           size_t n_sets, std::vector<uint32_t>& code_out, std::vector<pf_set_desc>& descs_out,
-                           std::vector<uint8_t>& wide, uint32_t& max_vars) {
-    max_vars = 0;
-    for (size_t s = 0; s < n_sets; s++) {
+// Set s: its ranges, operands and schema checked against the batch, and its instructions
+// copied into fixed[] (the set's own range) with the traffic / unit bits recomputed and
+// register def-before-use checked; wide[s] set.  0 or fail().
+static int check_set(size_t s, const uint32_t* code, size_t n_ins, size_t n_const, const uint32_t* schema,
+                     size_t n_vars, size_t n_parents, const pf_set_desc* descs, uint32_t* fixed, uint8_t* wide) {
+    {
         const pf_set_desc& d = descs[s];
         if ((uint64_t)d.code_off + d.n_ins > n_ins || d.n_ins == 0)
             return fail("set %zu: code range [%u,+%u) outside %zu instructions", s, d.code_off, d.n_ins, n_ins);
@@ -898,18 +953,16 @@ static int prepare_program(const uint32_t* code, size_t n_ins, const uint32_t* c
                                          (sc[1] >> 20) + ((sc[1] >> 8) & 0xfffu) > d.n_const))
                 return fail("set %zu var %u: calldata word constants", s, v);
         }
-        max_vars = std::max(max_vars, d.n_vars);
     }
     // traffic bits and register def-before-use, recomputed here so the kernel can trust
     // them whatever the caller packed (w0 bits 18..23)
-    std::vector<uint32_t> code_fixed(code, code + 4 * n_ins);
-    wide.assign(n_sets, 0);
-    for (size_t s = 0; s < n_sets; s++) {
+    {
         const pf_set_desc& d = descs[s];
+        memcpy(fixed + 4 * (size_t)d.code_off, code + 4 * (size_t)d.code_off, 16 * (size_t)d.n_ins);
         uint32_t wdef = 0u, bdef = 0u, max_wreg = 0u;
         uint64_t sdef = 0ull;
         for (uint32_t i = 0; i < d.n_ins; i++) {
-            uint32_t* I = code_fixed.data() + 4 * ((size_t)d.code_off + i);
+            uint32_t* I = fixed + 4 * ((size_t)d.code_off + i);
             const uint32_t op = I[0] & 0xffu, tr = pf_op_traffic(op);
             I[0] = (I[0] & 0x3ffffu) | (tr << 18) | (pf_op_unit(op) << 21);
             const uint32_t rd = I[1] & 0xffu, ra = (I[1] >> 8) & 0xffu, rb = (I[1] >> 16) & 0xffu,
@@ -939,8 +992,48 @@ static int prepare_program(const uint32_t* code, size_t n_ins, const uint32_t* c
             if (bres) bdef |= 1u << (rd & 31u);
         }
     }
+    return 0;
+}
+
+// Host-side checks of packed programs and their device form (pf_batch_create and
+// pf_eval_program): every kernel index is derived from these, so nothing the caller packed is
+// trusted.  Fills the device program (device_program), the per-set wide flags and the largest
+// variable count; returns 0 or fail().  A large batch (the corpus pass: 1,023 sets, 376k
+// instructions, ~10 ms on one host thread) is checked and rewritten in set ranges on host
+// threads, each range's device program appended to its own buffer, then concatenated in set
+// order — the same program as the serial pass; a range that fails sends the whole batch
+// through the serial pass, so the error reported is the first set's, as before.
+static int prepare_program(const uint32_t* code, size_t n_ins, const uint32_t* consts, size_t n_const,
+                           const uint32_t* schema, size_t n_vars, size_t n_parents, const pf_set_desc* descs,
+                           size_t n_sets, std::vector<uint32_t>& code_out, std::vector<pf_set_desc>& descs_out,
+                           std::vector<uint8_t>& wide, uint32_t& max_vars) {
+    max_vars = 0;
+    for (size_t s = 0; s < n_sets; s++) max_vars = std::max(max_vars, descs[s].n_vars);
+    std::vector<uint32_t> code_fixed(4 * n_ins);
+    wide.assign(n_sets, 0);
     descs_out.assign(descs, descs + n_sets);
-    device_program(code_fixed, descs_out, code_out, consts, n_const);
+    const std::vector<size_t> cut = prep_ranges(descs, n_sets, n_ins);
+    const size_t nt = cut.size() - 1;
+    bool bad = false;
+    if (nt > 1) {
+        std::vector<uint8_t> bad_t(nt, 0);
+        const bool defer = t_defer_err;
+        run_ranges(nt, [&](size_t t) {
+            t_defer_err = true;  // a failing range's message stays on its thread: the serial pass reports
+            for (size_t s = cut[t]; s < cut[t + 1] && !bad_t[t]; s++)
+                bad_t[t] = check_set(s, code, n_ins, n_const, schema, n_vars, n_parents, descs, code_fixed.data(),
+                                     wide.data()) != 0;
+        });
+        t_defer_err = defer;
+        bad = std::find(bad_t.begin(), bad_t.end(), (uint8_t)1) != bad_t.end();
+    }
+    if (nt == 1 || bad) {
+        for (size_t s = 0; s < n_sets; s++)
+            if (check_set(s, code, n_ins, n_const, schema, n_vars, n_parents, descs, code_fixed.data(),
+                          wide.data()))
+                return -1;
+    }
+    device_program(code_fixed.data(), code_fixed.size(), descs_out, cut, code_out, consts, n_const);
     return 0;
 }
 

@@ -294,3 +294,19 @@ def test_forwarding_keeps_the_write_back_of_a_result_read_again():
     for _ in range(64):
         vals = [rng.getrandbits(256) for _ in range(3)]
         assert eval_device(sv, rows_t, vals) == sv.evaluate(vals)
+
+
+def test_large_batch_program_equals_per_set_programs():
+    """A batch large enough for the threaded preparation (>= 64 sets, >= 32,768 instructions:
+    set ranges rewritten on host threads, then concatenated) gets, set by set, exactly the
+    device program the set gets alone."""
+    progs = [synth.mythril_like_set(i) for i in range(150)] + \
+        [synth.random_dag_set(900 + i, plant=True)[0] for i in range(150)]
+    b = ir.Batch(progs)
+    assert len(b.descs) >= 64 and len(b.code) >= 32768
+    out, dout = device_program(b)
+    for s, p in enumerate(progs):
+        one, d1 = device_program(ir.Batch([p]))
+        lo, n = int(dout[s][0]), int(dout[s][1])
+        assert n == int(d1[0][1]), s
+        assert (out[lo:lo + n] == one[:n]).all(), s
