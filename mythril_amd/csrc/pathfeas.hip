@@ -700,8 +700,14 @@ void device_program_range(const uint32_t* code_fixed, std::vector<pf_set_desc>& 
 // Host threads for a batch's preparation and the set ranges they take (about equal
 // instruction counts): one for small batches (a single query's), up to 8 for large ones.
 std::vector<size_t> prep_ranges(const pf_set_desc* descs, size_t n_sets, size_t n_ins) {
-    const size_t hw = std::max<size_t>(1, std::thread::hardware_concurrency());
-    const size_t nt = (n_sets >= 64 && n_ins >= (1u << 15)) ? std::min<size_t>({8, hw, n_sets / 32}) : 1;
+    size_t nt = 1;
+#ifndef PF_PREP_SERIAL
+    if (n_sets >= 64 && n_ins >= (1u << 15)) {
+        // hardware_concurrency reads sysfs: once per process, and not on a small batch's path
+        static const size_t hw = std::max<size_t>(1, std::thread::hardware_concurrency());
+        nt = std::min<size_t>({8, hw, n_sets / 32});
+    }
+#endif
     std::vector<size_t> cut(nt + 1, n_sets);
     cut[0] = 0;
     uint64_t total = 0, acc = 0;
