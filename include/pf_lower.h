@@ -164,6 +164,9 @@ void* pflt_lower(void* store, const uint32_t* roots, size_t n_roots, const uint3
 const char* pflt_last_error(void);
 void pflt_result_free(void* result);
 void pflt_result_info(void* result, uint64_t* info);  /* 17 sizes, see pf_terms.cpp */
+/* n results at once (pflt_lower_many's): out = n rows of 18 u64, the result's status
+ * (pflt_result_status) then its 17 pflt_result_info sizes (zeros for a failed result). */
+void pflt_result_info_many(void* const* results, size_t n, uint64_t* out);
 void pflt_result_get(void* result, uint32_t which, uint32_t* out, char* names_out);
 /* Candidate 0 of the result's program when every variable carries a parent value: the
  * parents masked to their widths, 8 u32 per variable, into out (the generator keeps every

@@ -2549,6 +2549,18 @@ void pflt_result_free(void* res) { delete (Result*)res; }
 /* sizes: [0] n_vars, [1] names bytes, [2] n_var_terms, [3] n_uf_apps, [4] n_arrays,
  * [5] n_reads, [6] n_ins, [7] n_const, [8] n_nodes, [9] n_pool, [10] n_roots, [11] n_forced,
  * [12] n_wregs, [13] n_sat, [14] n_in_roots, [15] parented, [16] some variable has a parent value */
+void pflt_result_info_many(void* const* results, size_t n, uint64_t* out) {
+    for (size_t j = 0; j < n; j++) {
+        uint64_t* row = out + 18 * j;
+        const Result* R = (const Result*)results[j];
+        row[0] = (uint64_t)(int64_t)R->rc;
+        if (R->rc == 0)
+            pflt_result_info(results[j], row + 1);
+        else
+            memset(row + 1, 0, 17 * sizeof(uint64_t));
+    }
+}
+
 void pflt_result_info(void* res, uint64_t* info) {
     const Result* R = (const Result*)res;
     info[0] = R->dag.vars.size();

@@ -130,6 +130,8 @@ def _bind(L):
         L.pflt_result_error.restype = ctypes.c_char_p
         L.pflt_result_error.argtypes = [vp]
         L.pflt_result_shrink.argtypes = [vp]
+        if hasattr(L, "pflt_result_info_many"):
+            L.pflt_result_info_many.argtypes = [ctypes.POINTER(vp), sz, ctypes.POINTER(ctypes.c_uint64)]
         L.pflt_pack_sizes.argtypes = [ctypes.POINTER(vp), sz, ctypes.POINTER(ctypes.c_uint64)]
         L.pflt_pack_batch.argtypes = [ctypes.POINTER(vp), sz, _u32p, _u32p, u32, _u32p, _u32p, _u32p, _u32p, _u32p]
         L.pflt_recheck_many.argtypes = [vp, ctypes.POINTER(vp), sz, _u32p, _u32p, sz, u32,
@@ -355,11 +357,13 @@ def _registry_blob_build(reg: UFRegistry) -> np.ndarray:
 class _Result:
     """One pflt_lower result: the program, the variables and the witness metadata."""
 
-    def __init__(self, st: TermStore, h):
+    def __init__(self, st: TermStore, h, info: Optional[List[int]] = None):
         self.st, self.h = st, h
-        info = (ctypes.c_uint64 * 17)()
-        st.L.pflt_result_info(h, info)
-        self.info = [int(x) for x in info]
+        if info is None:
+            buf = (ctypes.c_uint64 * 17)()
+            st.L.pflt_result_info(h, buf)
+            info = [int(x) for x in buf]
+        self.info = info
 
     def __del__(self):
         try:
@@ -773,15 +777,21 @@ def lower_many(jobs: List[Tuple[List[T.Term], object]], reg: UFRegistry, hints: 
         st.L.pflt_lower_many(st.h, arr.ctypes.data, n, _p32(regb), len(regb),
                              max(1, threads), res)
     out = []
+    rows = None
+    if hasattr(st.L, "pflt_result_info_many"):
+        # every result's status and sizes in one call (a _Result per job otherwise asks twice)
+        info = np.zeros((n, 18), dtype=np.uint64)
+        st.L.pflt_result_info_many(res, n, info.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)))
+        rows = info.tolist()
     for j in range(n):
         h = res[j]
-        rc = st.L.pflt_result_status(h)
+        rc = ctypes.c_int64(rows[j][0]).value if rows is not None else st.L.pflt_result_status(h)
         if rc != 0:
             msg = st.L.pflt_result_error(h).decode(errors="replace")
             st.L.pflt_result_free(h)
             out.append((None, None, msg if rc == -2 else f"ValueError: pflt_lower failed ({rc}): {msg}"))
             continue
-        r = _Result(st, h)
+        r = _Result(st, h, rows[j][1:] if rows is not None else None)
         out.append((NativeLowered(r), NativeProgram(r, seeds[j]), None))
     return out
 

@@ -488,3 +488,24 @@ def test_native_buckets_match_random_queries():
             if rng.random() < 0.3 and len(q) >= 2:
                 q = [T.and_(q[0], q[1])] + q[2:]
             assert NT.buckets(q) == buckets(q), q
+
+
+def test_result_info_many_matches_per_result_info(corpus_buckets):
+    """lower_many reads every result's status and sizes in one pflt_result_info_many call:
+    the same sizes pflt_result_info gives result by result, and a failed job keeps its error."""
+    import ctypes as C
+
+    reg, bks = corpus_buckets
+    st = NT.batch_api()
+    jobs = [(list(b), None) for b in bks[:40]]
+    out = NT.lower_many(jobs, reg, True, [0] * len(jobs), 1, st)
+    for lo, prog, err in out:
+        assert err is None
+        buf = (C.c_uint64 * 17)()
+        st.L.pflt_result_info(lo.res.h, buf)
+        assert lo.res.info == [int(x) for x in buf]
+    deep = T.var("rim_x", 256)
+    for _ in range(6000):
+        deep = T.Term("bvadd", T.bv_sort(256), (deep, T.const(1, 256)))
+    bad = NT.lower_many([([T.eq(deep, T.const(0, 256))], None)], reg, True, [0], 1, st)
+    assert bad[0][0] is None and "deep" in bad[0][2]
