@@ -192,6 +192,13 @@ int pflt_view(void* store, uint32_t id, pflt_term_view* out);
  * -1 when a capacity is too small, -2 on an unknown id.  Keys are memoised per term. */
 int64_t pflt_buckets(void* store, const uint32_t* roots, size_t n_roots, uint32_t* out_ids, size_t cap_ids,
                      uint32_t* out_sizes, size_t cap_sizes);
+/* pflt_buckets over n_queries queries at once (check_sets' batch): query q's constraints are
+ * roots[offsets[q] .. offsets[q + 1]); its buckets follow the previous queries' in out_ids /
+ * out_sizes and out_counts[q] gets their number.  Returns the total number of buckets, or
+ * pflt_buckets' -1 (a capacity too small: retry larger) / -2. */
+int64_t pflt_buckets_many(void* store, const uint32_t* roots, const uint64_t* offsets, size_t n_queries,
+                          uint32_t* out_ids, size_t cap_ids, uint32_t* out_sizes, size_t cap_sizes,
+                          int64_t* out_counts);
 
 /* Host re-check of a bucket witness (csrc/pf_recheck.cpp; mythril_amd/smt/interp.py
  * Witness.ev, bit for bit): var_desc = n_vars x 4 u32 (the result's var_terms descriptors:

@@ -2526,6 +2526,21 @@ int64_t pflt_buckets(void* st, const uint32_t* roots, size_t n_roots, uint32_t* 
     return (int64_t)ng;
 }
 
+int64_t pflt_buckets_many(void* st, const uint32_t* roots, const uint64_t* offsets, size_t n_queries,
+                          uint32_t* out_ids, size_t cap_ids, uint32_t* out_sizes, size_t cap_sizes,
+                          int64_t* out_counts) {
+    size_t oi = 0, os = 0;
+    for (size_t q = 0; q < n_queries; q++) {
+        const int64_t nb = pflt_buckets(st, roots + offsets[q], (size_t)(offsets[q + 1] - offsets[q]), out_ids + oi,
+                                        cap_ids - oi, out_sizes + os, cap_sizes - os);
+        if (nb < 0) return nb;
+        out_counts[q] = nb;
+        for (int64_t g = 0; g < nb; g++) oi += out_sizes[os + (size_t)g];
+        os += (size_t)nb;
+    }
+    return (int64_t)os;
+}
+
 int pflt_view(void* st, uint32_t id, pflt_term_view* out) {
     const Store* S = (const Store*)st;
     if (id >= S->t.size()) return -1;

@@ -485,14 +485,23 @@ def check_sets(sets: Sequence[Sequence[T.Term]], registry: Optional[UFRegistry] 
         phases[name] = phases.get(name, 0.0) + now - tp[0]
         tp[0] = now
 
-    for i, cs in enumerate(sets):
-        cs = [c for c in cs if c is not T.TRUE]
+    csets = [[c for c in cs if c is not T.TRUE] for cs in sets]
+    pre_bks: Dict[int, list] = {}
+    if cfg.split and _NATIVE_TERMS and len(csets) > 1:
+        # a batch's queries bucketed in one native call (pflt_buckets_many)
+        from . import native_terms
+
+        live = [i for i, cs in enumerate(csets) if not any(c is T.FALSE for c in cs)]
+        many = native_terms.buckets_many([csets[i] for i in live]) if live else None
+        if many is not None:
+            pre_bks = dict(zip(live, many))
+    for i, cs in enumerate(csets):
         if any(c is T.FALSE for c in cs):
             set_buckets.append(None)
             continue
         parent = parents[i] if parents else None
-        bks = None
-        if cfg.split and _NATIVE_TERMS:
+        bks = pre_bks.get(i)
+        if bks is None and cfg.split and _NATIVE_TERMS:
             from . import native_terms
 
             bks = native_terms.buckets(cs)      # the same partition (pflt_buckets)

@@ -576,6 +576,55 @@ def buckets(constraints: List[T.Term]) -> Optional[List[List[T.Term]]]:
         return out
 
 
+def buckets_many(queries: List[List[T.Term]]) -> Optional[List[List[List[T.Term]]]]:
+    """[buckets(q) for q in queries] in one native call (pflt_buckets_many: a batch's queries
+    without a ctypes round trip and its arrays per query); None when the library lacks it."""
+    st = store()
+    if st is None or not hasattr(st.L, "pflt_buckets_many"):
+        return None
+    L = st.L
+    if not getattr(L, "_buckets_many_bound", False):
+        L.pflt_buckets_many.restype = ctypes.c_int64
+        L.pflt_buckets_many.argtypes = [ctypes.c_void_p, _u32p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t,
+                                        _u32p, ctypes.c_size_t, _u32p, ctypes.c_size_t,
+                                        ctypes.POINTER(ctypes.c_int64)]
+        L._buckets_many_bound = True
+    n = len(queries)
+    if n == 0:
+        return []
+    with st.lock:
+        flat = st.export_many([c for q in queries for c in q])
+        roots = np.array(flat or [0], dtype=np.uint32)
+        offs = np.zeros(n + 1, dtype=np.uint64)
+        np.cumsum(np.array([len(q) for q in queries], dtype=np.uint64), out=offs[1:])
+        counts = np.zeros(n, dtype=np.int64)
+        cap = 4 * len(flat) + 256
+        while True:
+            ids = np.zeros(cap, dtype=np.uint32)
+            sizes = np.zeros(cap, dtype=np.uint32)
+            nb = L.pflt_buckets_many(st.h, _p32(roots), offs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), n,
+                                     _p32(ids), cap, _p32(sizes), cap,
+                                     counts.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)))
+            if nb != -1:
+                break
+            cap *= 4
+        if nb < 0:
+            return None
+        terms = st.terms
+        idl, szl = ids.tolist(), sizes[:nb].tolist()
+        out: List[List[List[T.Term]]] = []
+        o = g = 0
+        for k in counts.tolist():
+            qb = []
+            for _ in range(k):
+                m = szl[g]
+                qb.append([terms[i] for i in idl[o:o + m]])
+                o += m
+                g += 1
+            out.append(qb)
+        return out
+
+
 # ---- batches: parent models, concurrent lowering, native batch packing and re-check ---------
 # (include/pf_lower.h "batches"; gpu_check.check_sets' native pipeline)
 

@@ -509,3 +509,22 @@ def test_result_info_many_matches_per_result_info(corpus_buckets):
         deep = T.Term("bvadd", T.bv_sort(256), (deep, T.const(1, 256)))
     bad = NT.lower_many([([T.eq(deep, T.const(0, 256))], None)], reg, True, [0], 1, st)
     assert bad[0][0] is None and "deep" in bad[0][2]
+
+
+def test_buckets_many_equals_per_query_buckets(corpus_buckets):
+    """pflt_buckets_many over a batch = pflt_buckets query by query (partition, bucket order,
+    conjunct order), an empty query and nested ands included."""
+    if not hasattr(NT.store().L, "pflt_buckets_many"):
+        pytest.skip("libpflower.so without pflt_buckets_many")
+    rng = random.Random(5)
+    xs = [T.var(f"bmq_x{i}", 256) for i in range(6)]
+    atoms = [T.cmp("bvult", xs[i], xs[j]) for i in range(6) for j in range(i + 1, 6)]
+    atoms += [T.eq(x, T.const(k, 256)) for k, x in enumerate(xs)]
+    queries = [[]]
+    for _ in range(50):
+        q = rng.sample(atoms, rng.randint(1, 7))
+        if rng.random() < 0.3 and len(q) >= 2:
+            q = [T.and_(q[0], q[1])] + q[2:]
+        queries.append(q)
+    queries += [list(b) for _, bs in [(None, corpus_buckets[1][:30])] for b in bs]
+    assert NT.buckets_many(queries) == [NT.buckets(q) for q in queries]
